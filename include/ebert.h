@@ -1,0 +1,183 @@
+/*
+ * ebert.h -- C ABI of the MI355X-native embedding-similarity retrieval engine (libebert.so).
+ *
+ * This is the drop-in boundary for the reference's recommend/top-K hot path:
+ *   /root/reference/src/backend/app/lib.py:51-55   cosine_similarity -> mean -> exclude rated
+ *                                                   -> sort_values(desc)[:k]
+ *   /root/reference/src/backend/app/lib.py:105-106  the same mean-cosine for search re-weighting
+ *   /root/reference/src/backend/app/constants.py:55-56  catalog residency (load-time)
+ * The reference has no plugin/operator API for this path; the seam is that inline block, so the
+ * entry points below are what its Python binding (ctypes) calls in place of
+ * scikit-learn `cosine_similarity` (metrics/pairwise.py:1683-1738) and the pandas sort.
+ *
+ * Conventions
+ *   - Every pointer argument is DEVICE memory owned by the caller (torch tensors), except where
+ *     a comment says "host". The library never allocates or frees caller memory; scratch space
+ *     is a caller-provided workspace sized by ebt_cosine_topk_workspace().
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream). Every entry point only
+ *     enqueues work on that stream and returns; nothing synchronises except ebt_timer_query().
+ *   - Return value: EBT_OK (0) or a negative EBT_E* code; the message of the last failure on the
+ *     calling thread is available from ebt_last_error(). All entry points are reentrant: no
+ *     mutable global state apart from the thread-local error string.
+ *   - Row ids: catalog rows are addressed by their row number inside the (shard-local) matrix;
+ *     results carry GLOBAL row ids = local row + row_offset (a catalog row-sharded over ranks).
+ *   - Ordering of every top-k result: score descending, then row ascending. The reference's
+ *     pandas sort is an unstable introsort (pandas core/sorting.py:436-441), so its tie order is
+ *     unspecified; this is the deterministic order the build defines.
+ */
+#ifndef EBERT_H_
+#define EBERT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------------------------- */
+#define EBT_OK 0
+#define EBT_EINVAL (-1)      /* bad argument (shape, dtype, null pointer, k/kprime range)   */
+#define EBT_EHIP (-2)        /* a HIP runtime call or kernel launch failed                    */
+#define EBT_ENOMEM (-3)      /* workspace too small                                           */
+#define EBT_EUNSUPPORTED (-4)
+
+/* ---- element types --------------------------------------------------------------------- */
+#define EBT_F32 0
+#define EBT_BF16 1
+#define EBT_F16 2
+#define EBT_F64 3
+
+/* Library version (major*10000 + minor*100 + patch). */
+int ebt_version(void);
+
+/* Message for the last non-zero return on this thread ("" if none). */
+const char* ebt_last_error(void);
+
+/* ---- catalog load: constants.py:55-56 (+ sklearn row_norms, preprocessing/_data.py:2011) ---
+ * Guarded L2 norm of every row in float64: gnorm[i] = ||x_i|| unless ||x_i|| < 10*DBL_EPSILON,
+ * in which case 1.0 (sklearn _handle_zeros_in_scale, preprocessing/_data.py:118-123), and the
+ * float32 reciprocal inv32[i] = 1/gnorm[i] used by the screening epilogue. inv32 may be NULL.
+ * x: n rows of d elements of `dtype`, row stride `ld` ELEMENTS. */
+int ebt_row_norms(const void* x, int dtype, int64_t n, int32_t d, int64_t ld,
+                  double* gnorm64, float* inv32, void* stream);
+
+/* Screening image of a matrix: img[i][j] = round_to(img_dtype, x[i][j] * s_i) for j < d and 0 for
+ * d <= j < ld_img, where s_i = 1/gnorm64[i] if `normalize` else 1. img_dtype is EBT_F16 or
+ * EBT_BF16; ld_img (row stride in elements) must be a multiple of 64 and >= d. Rows of the
+ * image past n are not touched. */
+int ebt_screen_image(const void* x, int dtype, int64_t n, int32_t d, int64_t ld,
+                     const double* gnorm64, int normalize, int img_dtype, void* img,
+                     int32_t ld_img, void* stream);
+
+/* ---- queries: lib.py:51-52 folded into one query vector per user -------------------------
+ * Dense queries (one vector per query, the L = 1 case of lib.py:51):
+ *   q64[b] = q[b] / gnorm(q[b])  (float64, sklearn normalize semantics).
+ * Liked-rows queries (the collaborative path): for CSR lists liked_off[B+1] / liked_rows[] of
+ * LOCAL catalog rows, q64[b] = sum_l cat[l] / gnorm64_cat[l]  (a SUM; the caller divides by the
+ * user's liked count L_b after an optional cross-shard all-reduce). liked_off/liked_rows NULL
+ * selects the dense form. q64 is B x d float64, row stride d. */
+int ebt_query_dense(const void* q, int dtype, int64_t B, int32_t d, int64_t ldq, double* q64,
+                    void* stream);
+int ebt_query_liked_sum(const void* cat, int dtype, int32_t d, int64_t ld,
+                        const double* gnorm64_cat, int64_t B, const int64_t* liked_off,
+                        const int64_t* liked_rows, double* q64, void* stream);
+/* q64[b] *= scale[b] (scale is device float64[B]); used for the 1/L of lib.py:52. */
+int ebt_scale_rows_f64(double* q64, int64_t B, int32_t d, const double* scale, void* stream);
+
+/* Screening image + certification bound of a query batch.
+ *   qimg[b][j] = round_to(img_dtype, q64[b][j]) (rows B..B_pad-1 and columns d..ld_img-1 = 0),
+ *   qscale[b]  = 1,
+ *   eps[b]     = a rigorous bound on |approx score - exact float64 score| for every catalog
+ *                row, given the catalog image rounding `u_cat` (0 for a native image whose
+ *                values are exact, 2^-11 for a float16-rounded normalised image):
+ *                eps = 1.05*(|q|*(u_q + u_cat + u_q*u_cat) + (d+8)*2^-24*(|q|+1)) + 1e-9,
+ *                with u_q the unit round-off of img_dtype.
+ * With `native_q` != 0 the image is instead the raw query `q` (same dtype as img_dtype, the
+ * native-catalog screening mode): qimg = q, qscale[b] = 1/gnorm(q[b]) and u_q = 0. */
+int ebt_query_image(const double* q64, int64_t B, int64_t B_pad, int32_t d, int img_dtype,
+                    const void* q_native, int64_t ldq, int native_q, float u_cat, void* qimg,
+                    int32_t ld_img, float* qscale, float* eps, void* stream);
+
+/* ---- kernels of the search pipeline (exposed for tests and the bench) --------------------
+ * Screening GEMM on MFMA: scores[b][i] = qscale[b]*cscale[i]*sum_j qimg[b][j]*cimg[i][j] for
+ * b < B_pad (multiple of 128) and i < n_rows; f16 or bf16 inputs, float32 accumulate.
+ * cscale may be NULL (= 1). ld_scores must be a multiple of 4 and >= n_rows. */
+int ebt_screen_scores(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
+                      int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
+                      const float* cscale, float* scores, int64_t ld_scores, void* stream);
+
+/* Excluded rows (lib.py:48,55: rated movies are not candidates): for every b < B and every
+ * GLOBAL row g in excl_rows[excl_off[b] .. excl_off[b+1]) with col_begin <= g < col_end,
+ * scores[b][g - col_begin] = -inf. */
+int ebt_mask_excluded(float* scores, int64_t ld_scores, int64_t B, int64_t col_begin,
+                      int64_t col_end, const int64_t* excl_off, const int64_t* excl_rows,
+                      void* stream);
+
+/* Streaming top-k' select (one HBM pass over the scores): for each row b < B and each of `segs`
+ * equal segments of its n entries, write the kprime largest (value desc, index asc) entries,
+ * sorted, to out_vals/out_idx[b*ld_out + seg*kprime + j]. Entries that are NaN or -inf are
+ * never selected; missing slots get -inf / -1. Dense form (idx == NULL): the index of entry j
+ * is idx_base + j. Candidate-list form: idx[b*ld + j] gives it (values < 2^31, -1 = empty).
+ * 1 <= kprime <= 4096. */
+int ebt_select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B, int64_t n,
+                    int64_t idx_base, int32_t kprime, int32_t segs, float* out_vals,
+                    int64_t* out_idx, int64_t ld_out, void* stream);
+
+/* Exact float64 rescore of the screened candidates + final top-k + certification.
+ * For each b: candidates cand_rows[b*kprime + j] (LOCAL rows, -1 = empty), sorted by their
+ * approx scores cand_vals (desc). score = (q64[b] . cat[row]) / gnorm64[row] in float64; the k
+ * best by (score desc, row asc) go to out_scores/out_rows[b*k + j] (rows + row_offset; empty
+ * slots NaN / -1). certified[b] = 1 iff the candidate set provably contains the exact top-k:
+ * kprime >= n_rows (every row is a candidate),
+ * fewer than kprime valid candidates, or approx[kprime-1] < approx[k-1] - 2*eps[b]. */
+int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype, int64_t ld,
+                const double* gnorm64, int64_t row_offset, const float* cand_vals,
+                const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
+                double* out_scores, int64_t* out_rows, int32_t* certified, void* stream);
+
+/* Merge R partial top-k lists (scores/rows [R][B][k], each sorted) into the global top-k per
+ * query -- the post-all-gather step of a row-sharded catalog. R*k <= 8192. */
+int ebt_merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, int32_t k,
+                   double* out_scores, int64_t* out_rows, void* stream);
+
+/* ---- the whole pipeline -------------------------------------------------------------------
+ * Workspace bytes needed by ebt_cosine_topk for these sizes. */
+size_t ebt_cosine_topk_workspace(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
+                                 int64_t chunk_rows);
+
+/* Query x catalog cosine top-k over one (shard of a) catalog:
+ *   for every catalog chunk of chunk_rows rows: screening GEMM -> mask excluded -> streaming
+ *   select of kprime candidates; then a select across chunks; then the exact float64 rescore.
+ * Inputs: the query batch prepared by ebt_query_* (q64, qimg, qscale, eps; B real rows, B_pad
+ * image rows), the catalog (cat/dtype/ld with gnorm64; its screening image cimg with cscale or
+ * NULL, ld_img, d_pad), exclusions as CSR of GLOBAL rows (NULL = none), k <= kprime.
+ * Outputs: out_scores (float64 [B][k]), out_rows (int64 [B][k], global), certified (int32 [B]).
+ * timer (NULL or an ebt_timer) collects per-stage GPU time. */
+int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, const float* eps,
+                    int64_t B, int64_t B_pad, const void* cat, int dtype, int64_t ld,
+                    const double* gnorm64, const void* cimg, const float* cscale, int img_dtype,
+                    int32_t ld_img, int64_t n_rows, int32_t d, int32_t d_pad, int64_t row_offset,
+                    const int64_t* excl_off, const int64_t* excl_rows, int32_t k, int32_t kprime,
+                    int64_t chunk_rows, void* workspace, size_t ws_bytes, double* out_scores,
+                    int64_t* out_rows, int32_t* certified, void* timer, void* stream);
+
+/* ---- per-stage GPU timing (hipEvents recorded on the launch stream) -----------------------
+ * Stages: 0 screening GEMM, 1 exclusion mask, 2 chunk select, 3 cross-chunk select, 4 rescore.
+ * ebt_timer_query synchronises the recorded events and returns the total milliseconds and the
+ * number of launches of `stage` since the last reset. Host pointers. */
+#define EBT_STAGE_GEMM 0
+#define EBT_STAGE_MASK 1
+#define EBT_STAGE_SELECT 2
+#define EBT_STAGE_MERGE_SELECT 3
+#define EBT_STAGE_RESCORE 4
+#define EBT_NUM_STAGES 5
+void* ebt_timer_create(void);
+void ebt_timer_destroy(void* timer);
+int ebt_timer_reset(void* timer);
+int ebt_timer_query(void* timer, int stage, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EBERT_H_ */

@@ -1,0 +1,140 @@
+"""ctypes binding of libebert.so (the C ABI declared in include/ebert.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``make -C robot_ebert_amd/csrc``).
+There is no fallback: if the shared object is missing or fails to load, every entry point
+raises ``EbertError`` -- the product path never silently computes on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("EBERT_LIB", os.path.join(_HERE, "libebert.so"))
+
+EBT_F32, EBT_BF16, EBT_F16, EBT_F64 = 0, 1, 2, 3
+DTYPE_CODE = {torch.float32: EBT_F32, torch.bfloat16: EBT_BF16, torch.float16: EBT_F16,
+              torch.float64: EBT_F64}
+STAGES = {"gemm": 0, "mask": 1, "select": 2, "merge_select": 3, "rescore": 4}
+
+
+class EbertError(RuntimeError):
+    """A libebert call failed (or the library could not be loaded)."""
+
+
+_VP, _I32, _I64, _SZ, _F32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t, ctypes.c_float
+_INT = ctypes.c_int
+
+_SIGNATURES = {
+    "ebt_version": ([], _INT),
+    "ebt_last_error": ([], ctypes.c_char_p),
+    "ebt_row_norms": ([_VP, _INT, _I64, _I32, _I64, _VP, _VP, _VP], _INT),
+    "ebt_screen_image": ([_VP, _INT, _I64, _I32, _I64, _VP, _INT, _INT, _VP, _I32, _VP], _INT),
+    "ebt_query_dense": ([_VP, _INT, _I64, _I32, _I64, _VP, _VP], _INT),
+    "ebt_query_liked_sum": ([_VP, _INT, _I32, _I64, _VP, _I64, _VP, _VP, _VP, _VP], _INT),
+    "ebt_scale_rows_f64": ([_VP, _I64, _I32, _VP, _VP], _INT),
+    "ebt_query_image": ([_VP, _I64, _I64, _I32, _INT, _VP, _I64, _INT, _F32, _VP, _I32, _VP, _VP,
+                         _VP], _INT),
+    "ebt_screen_scores": ([_VP, _I64, _VP, _I64, _I32, _I32, _INT, _VP, _VP, _VP, _I64, _VP],
+                          _INT),
+    "ebt_mask_excluded": ([_VP, _I64, _I64, _I64, _I64, _VP, _VP, _VP], _INT),
+    "ebt_select_topk": ([_VP, _VP, _I64, _I64, _I64, _I64, _I32, _I32, _VP, _VP, _I64, _VP],
+                        _INT),
+    "ebt_rescore": ([_VP, _I64, _I32, _VP, _INT, _I64, _VP, _I64, _VP, _VP, _I32, _I32, _I64, _VP,
+                     _VP, _VP, _VP, _VP], _INT),
+    "ebt_merge_topk": ([_VP, _VP, _I32, _I64, _I32, _VP, _VP, _VP], _INT),
+    "ebt_cosine_topk_workspace": ([_I64, _I64, _I64, _I32, _I64], _SZ),
+    "ebt_cosine_topk": ([_VP, _VP, _VP, _VP, _I64, _I64, _VP, _INT, _I64, _VP, _VP, _VP, _INT,
+                         _I32, _I64, _I32, _I32, _I64, _VP, _VP, _I32, _I32, _I64, _VP, _SZ, _VP,
+                         _VP, _VP, _VP, _VP], _INT),
+    "ebt_timer_create": ([], _VP),
+    "ebt_timer_destroy": ([_VP], None),
+    "ebt_timer_reset": ([_VP], _INT),
+    "ebt_timer_query": ([_VP, _INT, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64)], _INT),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+_lock = threading.Lock()
+
+
+def load() -> ctypes.CDLL:
+    """Load libebert.so once; raise EbertError if it is absent (no CPU fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise EbertError(
+                    f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; "
+                    "g.build()'` (make -C robot_ebert_amd/csrc)")
+            try:
+                lib = ctypes.CDLL(LIB_PATH)
+            except OSError as e:
+                raise EbertError(f"cannot load {LIB_PATH}: {e}") from e
+            for name, (args, res) in _SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.argtypes = args
+                fn.restype = res
+            _lib = lib
+    return _lib
+
+
+def call(name: str, *args) -> int:
+    """Call an ``int``-returning entry point and raise EbertError on a negative status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.ebt_last_error().decode(errors="replace")
+        raise EbertError(f"{name} failed with status {rc}: {msg}")
+    return rc
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_of(device: torch.device) -> int:
+    """The current torch (HIP) stream of `device`: every libebert call enqueues on it."""
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_cuda(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise EbertError(f"{what} must be a CUDA (HIP) tensor; libebert has no CPU path")
+
+
+class Timer:
+    """Per-stage GPU time collected with hipEvents on the launch stream (ebt_timer_*)."""
+
+    def __init__(self) -> None:
+        self._h = load().ebt_timer_create()
+        if not self._h:
+            raise EbertError("ebt_timer_create failed")
+
+    def reset(self) -> None:
+        call("ebt_timer_reset", self._h)
+
+    def query(self, stage: str):
+        tot = ctypes.c_double(0.0)
+        n = ctypes.c_int64(0)
+        call("ebt_timer_query", self._h, STAGES[stage], ctypes.byref(tot), ctypes.byref(n))
+        return tot.value, n.value
+
+    @property
+    def handle(self) -> int:
+        return self._h
+
+    def __del__(self):
+        try:
+            if self._h and _lib is not None:
+                _lib.ebt_timer_destroy(self._h)
+        except Exception:
+            pass
+        self._h = None

@@ -1,0 +1,341 @@
+// extern "C" entry points of libebert.so (declared in include/ebert.h), the pipeline
+// orchestrator ebt_cosine_topk, the per-stage hipEvent timer and error reporting.
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+
+namespace ebt {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return EBT_OK;
+  set_error("%s: %s", what, hipGetErrorString(e));
+  return EBT_EHIP;
+}
+
+int launch_check(const char* what) { return hip_check(hipGetLastError(), what); }
+
+// kernels (defined in the other translation units)
+int screen_gemm(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int, const float*,
+                const float*, float*, int64_t, hipStream_t);
+int select_topk(const float*, const int64_t*, int64_t, int64_t, int64_t, int64_t, int32_t,
+                int32_t, float*, int64_t*, int64_t, hipStream_t);
+int row_norms(const void*, int, int64_t, int32_t, int64_t, double*, float*, hipStream_t);
+int screen_image(const void*, int, int64_t, int32_t, int64_t, const double*, int, int, void*,
+                 int32_t, hipStream_t);
+int query_dense(const void*, int, int64_t, int32_t, int64_t, double*, hipStream_t);
+int query_liked_sum(const void*, int, int32_t, int64_t, const double*, int64_t, const int64_t*,
+                    const int64_t*, double*, hipStream_t);
+int scale_rows_f64(double*, int64_t, int32_t, const double*, hipStream_t);
+int query_image(const double*, int64_t, int64_t, int32_t, int, const void*, int64_t, int, float,
+                void*, int32_t, float*, float*, hipStream_t);
+int mask_excluded(float*, int64_t, int64_t, int64_t, int64_t, const int64_t*, const int64_t*,
+                  hipStream_t);
+int rescore(const double*, int64_t, int32_t, const void*, int, int64_t, const double*, int64_t,
+            const float*, const int64_t*, int32_t, int32_t, int64_t, const float*, double*, int64_t*,
+            int32_t*, hipStream_t);
+int merge_topk(const double*, const int64_t*, int32_t, int64_t, int32_t, double*, int64_t*,
+               hipStream_t);
+
+// ------------------------------------------------------------------------------ timer ------
+struct Timer {
+  struct Rec {
+    int stage;
+    hipEvent_t a, b;
+  };
+  std::vector<hipEvent_t> pool;
+  size_t used = 0;
+  std::vector<Rec> recs;
+  std::mutex mu;
+
+  hipEvent_t get() {
+    if (used == pool.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      pool.push_back(e);
+    }
+    return pool[used++];
+  }
+  ~Timer() {
+    for (auto e : pool) (void)hipEventDestroy(e);
+  }
+};
+
+struct StageScope {
+  Timer* t;
+  int stage;
+  hipStream_t st;
+  hipEvent_t a = nullptr, b = nullptr;
+  StageScope(void* timer, int s, hipStream_t stream) : t((Timer*)timer), stage(s), st(stream) {
+    if (t) {
+      std::lock_guard<std::mutex> g(t->mu);
+      a = t->get();
+      b = t->get();
+      if (a) (void)hipEventRecord(a, st);
+    }
+  }
+  ~StageScope() {
+    if (t && a && b) {
+      (void)hipEventRecord(b, st);
+      std::lock_guard<std::mutex> g(t->mu);
+      t->recs.push_back({stage, a, b});
+    }
+  }
+};
+
+// --------------------------------------------------------------------- workspace layout ----
+struct WsLayout {
+  int64_t chunk, ld_s, n_chunks;
+  int segs;
+  size_t off_s, off_segv, off_segi, off_chv, off_chi, off_fv, off_fi, bytes;
+};
+
+static size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
+
+static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
+                          int64_t chunk_rows) {
+  WsLayout L{};
+  L.chunk = chunk_rows < n_rows ? chunk_rows : n_rows;
+  if (L.chunk < 1) L.chunk = 1;
+  L.ld_s = (L.chunk + 3) & ~(int64_t)3;
+  L.n_chunks = ceil_div(n_rows, L.chunk);
+  // enough select workgroups to fill the chip: >= 512 (2 per CU)
+  int64_t segs = B > 0 ? ceil_div(512, B) : 1;
+  int64_t max_segs = L.chunk / (2 * 4096);
+  if (max_segs < 1) max_segs = 1;
+  if (segs > max_segs) segs = max_segs;
+  if (segs < 1) segs = 1;
+  L.segs = (int)segs;
+  size_t o = 0;
+  L.off_s = o;
+  o = align_up(o + (size_t)B_pad * L.ld_s * 4);
+  L.off_segv = o;
+  if (L.segs > 1) o = align_up(o + (size_t)B * L.segs * kprime * 4);
+  L.off_segi = o;
+  if (L.segs > 1) o = align_up(o + (size_t)B * L.segs * kprime * 8);
+  L.off_chv = o;
+  if (L.n_chunks > 1) o = align_up(o + (size_t)B * L.n_chunks * kprime * 4);
+  L.off_chi = o;
+  if (L.n_chunks > 1) o = align_up(o + (size_t)B * L.n_chunks * kprime * 8);
+  L.off_fv = o;
+  o = align_up(o + (size_t)B * kprime * 4);
+  L.off_fi = o;
+  o = align_up(o + (size_t)B * kprime * 8);
+  L.bytes = o;
+  return L;
+}
+
+}  // namespace ebt
+
+using namespace ebt;
+
+extern "C" {
+
+int ebt_version(void) { return 100; }
+
+const char* ebt_last_error(void) { return g_err; }
+
+int ebt_row_norms(const void* x, int dtype, int64_t n, int32_t d, int64_t ld, double* gnorm64,
+                  float* inv32, void* stream) {
+  return row_norms(x, dtype, n, d, ld, gnorm64, inv32, (hipStream_t)stream);
+}
+
+int ebt_screen_image(const void* x, int dtype, int64_t n, int32_t d, int64_t ld,
+                     const double* gnorm64, int normalize, int img_dtype, void* img,
+                     int32_t ld_img, void* stream) {
+  return screen_image(x, dtype, n, d, ld, gnorm64, normalize, img_dtype, img, ld_img,
+                      (hipStream_t)stream);
+}
+
+int ebt_query_dense(const void* q, int dtype, int64_t B, int32_t d, int64_t ldq, double* q64,
+                    void* stream) {
+  return query_dense(q, dtype, B, d, ldq, q64, (hipStream_t)stream);
+}
+
+int ebt_query_liked_sum(const void* cat, int dtype, int32_t d, int64_t ld,
+                        const double* gnorm64_cat, int64_t B, const int64_t* liked_off,
+                        const int64_t* liked_rows, double* q64, void* stream) {
+  return query_liked_sum(cat, dtype, d, ld, gnorm64_cat, B, liked_off, liked_rows, q64,
+                         (hipStream_t)stream);
+}
+
+int ebt_scale_rows_f64(double* q64, int64_t B, int32_t d, const double* scale, void* stream) {
+  return scale_rows_f64(q64, B, d, scale, (hipStream_t)stream);
+}
+
+int ebt_query_image(const double* q64, int64_t B, int64_t B_pad, int32_t d, int img_dtype,
+                    const void* q_native, int64_t ldq, int native_q, float u_cat, void* qimg,
+                    int32_t ld_img, float* qscale, float* eps, void* stream) {
+  return query_image(q64, B, B_pad, d, img_dtype, q_native, ldq, native_q, u_cat, qimg, ld_img,
+                     qscale, eps, (hipStream_t)stream);
+}
+
+int ebt_screen_scores(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
+                      int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
+                      const float* cscale, float* scores, int64_t ld_scores, void* stream) {
+  return screen_gemm(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale, cscale, scores,
+                     ld_scores, (hipStream_t)stream);
+}
+
+int ebt_mask_excluded(float* scores, int64_t ld_scores, int64_t B, int64_t col_begin,
+                      int64_t col_end, const int64_t* excl_off, const int64_t* excl_rows,
+                      void* stream) {
+  return mask_excluded(scores, ld_scores, B, col_begin, col_end, excl_off, excl_rows,
+                       (hipStream_t)stream);
+}
+
+int ebt_select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B, int64_t n,
+                    int64_t idx_base, int32_t kprime, int32_t segs, float* out_vals,
+                    int64_t* out_idx, int64_t ld_out, void* stream) {
+  return select_topk(vals, idx, ld, B, n, idx_base, kprime, segs, out_vals, out_idx, ld_out,
+                     (hipStream_t)stream);
+}
+
+int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype, int64_t ld,
+                const double* gnorm64, int64_t row_offset, const float* cand_vals,
+                const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
+                double* out_scores, int64_t* out_rows, int32_t* certified, void* stream) {
+  return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, cand_vals, cand_rows, kprime, k, n_rows,
+                 eps, out_scores, out_rows, certified, (hipStream_t)stream);
+}
+
+int ebt_merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, int32_t k,
+                   double* out_scores, int64_t* out_rows, void* stream) {
+  return merge_topk(scores, rows, R, B, k, out_scores, out_rows, (hipStream_t)stream);
+}
+
+size_t ebt_cosine_topk_workspace(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
+                                 int64_t chunk_rows) {
+  if (B < 0 || B_pad < B || n_rows < 1 || kprime < 1 || chunk_rows < 1) return 0;
+  return ws_layout(B, B_pad, n_rows, kprime, chunk_rows).bytes;
+}
+
+int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, const float* eps,
+                    int64_t B, int64_t B_pad, const void* cat, int dtype, int64_t ld,
+                    const double* gnorm64, const void* cimg, const float* cscale, int img_dtype,
+                    int32_t ld_img, int64_t n_rows, int32_t d, int32_t d_pad, int64_t row_offset,
+                    const int64_t* excl_off, const int64_t* excl_rows, int32_t k, int32_t kprime,
+                    int64_t chunk_rows, void* workspace, size_t ws_bytes, double* out_scores,
+                    int64_t* out_rows, int32_t* certified, void* timer, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!q64 || !qimg || !qscale || !eps || !cat || !gnorm64 || !cimg || !workspace ||
+      !out_scores || !out_rows || !certified) {
+    set_error("ebt_cosine_topk: null pointer");
+    return EBT_EINVAL;
+  }
+  if (B < 1 || B_pad < B || B_pad % 128 != 0 || n_rows < 1 || d < 1 || d_pad < d ||
+      d_pad % 64 != 0 || ld_img < d_pad || k < 1 || kprime < k || kprime > 4096 ||
+      kprime % 4 != 0 || chunk_rows < 128 || chunk_rows % 128 != 0 || ((excl_off == nullptr) != (excl_rows == nullptr))) {
+    set_error("ebt_cosine_topk: bad arguments (B=%lld B_pad=%lld n=%lld d=%d d_pad=%d k=%d "
+              "kprime=%d chunk=%lld)", (long long)B, (long long)B_pad, (long long)n_rows, d,
+              d_pad, k, kprime, (long long)chunk_rows);
+    return EBT_EINVAL;
+  }
+  const WsLayout L = ws_layout(B, B_pad, n_rows, kprime, chunk_rows);
+  if (ws_bytes < L.bytes) {
+    set_error("ebt_cosine_topk: workspace %zu < %zu bytes", ws_bytes, L.bytes);
+    return EBT_ENOMEM;
+  }
+  char* ws = (char*)workspace;
+  float* S = (float*)(ws + L.off_s);
+  float* segv = (float*)(ws + L.off_segv);
+  int64_t* segi = (int64_t*)(ws + L.off_segi);
+  float* chv = (float*)(ws + L.off_chv);
+  int64_t* chi = (int64_t*)(ws + L.off_chi);
+  float* fv = (float*)(ws + L.off_fv);
+  int64_t* fi = (int64_t*)(ws + L.off_fi);
+  const int es_img = 2;
+  int rc;
+  for (int64_t c = 0; c < L.n_chunks; ++c) {
+    const int64_t c0 = c * L.chunk;
+    const int64_t nc = (n_rows - c0) < L.chunk ? (n_rows - c0) : L.chunk;
+    {
+      StageScope s(timer, EBT_STAGE_GEMM, st);
+      rc = screen_gemm(qimg, B_pad, (const char*)cimg + c0 * ld_img * es_img, nc, d_pad, ld_img,
+                       img_dtype, qscale, cscale ? cscale + c0 : nullptr, S, L.ld_s, st);
+    }
+    if (rc) return rc;
+    if (excl_off) {
+      StageScope s(timer, EBT_STAGE_MASK, st);
+      rc = mask_excluded(S, L.ld_s, B, row_offset + c0, row_offset + c0 + nc, excl_off,
+                         excl_rows, st);
+      if (rc) return rc;
+    }
+    float* dv = L.n_chunks == 1 ? fv : chv + c * kprime;
+    int64_t* di = L.n_chunks == 1 ? fi : chi + c * kprime;
+    const int64_t ld_d = L.n_chunks == 1 ? kprime : L.n_chunks * kprime;
+    {
+      StageScope s(timer, EBT_STAGE_SELECT, st);
+      if (L.segs == 1) {
+        rc = select_topk(S, nullptr, L.ld_s, B, nc, c0, kprime, 1, dv, di, ld_d, st);
+      } else {
+        rc = select_topk(S, nullptr, L.ld_s, B, nc, c0, kprime, L.segs, segv, segi,
+                         (int64_t)L.segs * kprime, st);
+        if (!rc)
+          rc = select_topk(segv, segi, (int64_t)L.segs * kprime, B, (int64_t)L.segs * kprime, 0,
+                           kprime, 1, dv, di, ld_d, st);
+      }
+    }
+    if (rc) return rc;
+  }
+  if (L.n_chunks > 1) {
+    StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
+    rc = select_topk(chv, chi, L.n_chunks * kprime, B, L.n_chunks * kprime, 0, kprime, 1, fv, fi,
+                     kprime, st);
+    if (rc) return rc;
+  }
+  {
+    StageScope s(timer, EBT_STAGE_RESCORE, st);
+    rc = rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, fv, fi, kprime, k, n_rows, eps,
+                 out_scores, out_rows, certified, st);
+  }
+  return rc;
+}
+
+void* ebt_timer_create(void) { return new (std::nothrow) Timer(); }
+
+void ebt_timer_destroy(void* timer) { delete (Timer*)timer; }
+
+int ebt_timer_reset(void* timer) {
+  if (!timer) return EBT_EINVAL;
+  Timer* t = (Timer*)timer;
+  std::lock_guard<std::mutex> g(t->mu);
+  t->recs.clear();
+  t->used = 0;
+  return EBT_OK;
+}
+
+int ebt_timer_query(void* timer, int stage, double* total_ms, int64_t* launches) {
+  if (!timer || !total_ms || !launches) return EBT_EINVAL;
+  Timer* t = (Timer*)timer;
+  std::lock_guard<std::mutex> g(t->mu);
+  double tot = 0.0;
+  int64_t cnt = 0;
+  for (auto& r : t->recs) {
+    if (r.stage != stage) continue;
+    int rc = hip_check(hipEventSynchronize(r.b), "hipEventSynchronize");
+    if (rc) return rc;
+    float ms = 0.f;
+    rc = hip_check(hipEventElapsedTime(&ms, r.a, r.b), "hipEventElapsedTime");
+    if (rc) return rc;
+    tot += ms;
+    ++cnt;
+  }
+  *total_ms = tot;
+  *launches = cnt;
+  return EBT_OK;
+}
+
+}  // extern "C"

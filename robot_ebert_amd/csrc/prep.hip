@@ -1,0 +1,340 @@
+// Load-time and per-batch preparation kernels (all HBM-bound, vectorised 16 B per lane).
+//
+//  * row_norms      -- sklearn row_norms + _handle_zeros_in_scale (utils/extmath.py:76,
+//                      preprocessing/_data.py:118-123,2011): guarded float64 L2 norm per row.
+//                      The reference recomputes this for the whole catalog on EVERY call
+//                      (metrics/pairwise.py:1730-1734); here it runs once at catalog load
+//                      (constants.py:55-56) and is kept resident in HBM.
+//  * screen_image   -- the f16/bf16 MFMA operand of a matrix (normalised or raw), zero-padded to
+//                      a multiple of 64 columns.
+//  * query_dense / query_liked_sum / scale_rows -- q64 = normalize(q), or the liked-row mean of
+//                      lib.py:51-52 folded into ONE query vector per user (sum here, 1/L later).
+//  * query_image    -- the query's MFMA operand, its epilogue scale and the certification bound.
+//  * mask_excluded  -- rated movies are not candidates (lib.py:48,55).
+#include "common.h"
+
+namespace ebt {
+
+// ---------------------------------------------------------------------------- row norms ----
+template <int DT, bool VEC>
+__global__ __launch_bounds__(256) void row_norms_kernel(const void* __restrict__ x, int64_t n,
+                                                         int d, int64_t ld,
+                                                         double* __restrict__ gnorm,
+                                                         float* __restrict__ inv32) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  double s = 0.0;
+  if constexpr (VEC) {
+    constexpr int ES = (DT == EBT_F64) ? 8 : (DT == EBT_F32 ? 4 : 2);
+    constexpr int PER = 16 / ES;  // elements per 16-byte chunk
+    const char* base = (const char*)x + row * ld * ES;
+    const int nchunks = d / PER;
+    for (int c = lane; c < nchunks; c += 64) {
+      const uint4 raw = *(const uint4*)(base + (int64_t)c * 16);
+      if constexpr (DT == EBT_F32) {
+        const float* f = (const float*)&raw;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s += (double)f[e] * (double)f[e];
+      } else if constexpr (DT == EBT_F64) {
+        const double* f = (const double*)&raw;
+        s += f[0] * f[0] + f[1] * f[1];
+      } else {
+        const uint16_t* h = (const uint16_t*)&raw;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const double v = DT == EBT_BF16 ? bf16_bits_to_f64(h[e]) : f16_bits_to_f64(h[e]);
+          s += v * v;
+        }
+      }
+    }
+  } else {
+    for (int j = lane; j < d; j += 64) {
+      const double v = load_as_f64<DT>(x, row * ld + j);
+      s += v * v;
+    }
+  }
+  s = wave_sum_f64(s);
+  if (lane == 0) {
+    const double g = guard_norm(sqrt(s));
+    gnorm[row] = g;
+    if (inv32) inv32[row] = (float)(1.0 / g);
+  }
+}
+
+static bool vec_ok(const void* p, int dtype, int64_t ld, int d) {
+  const int es = dtype == EBT_F64 ? 8 : (dtype == EBT_F32 ? 4 : 2);
+  return (((uintptr_t)p & 15) == 0) && ((ld * es) % 16 == 0) && (((int64_t)d * es) % 16 == 0);
+}
+
+int row_norms(const void* x, int dtype, int64_t n, int32_t d, int64_t ld, double* gnorm,
+              float* inv32, hipStream_t st) {
+  if (!x || !gnorm || n < 0 || d <= 0 || ld < d || dtype < 0 || dtype > 3) {
+    set_error("ebt_row_norms: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (n == 0) return EBT_OK;
+  const bool v = vec_ok(x, dtype, ld, d);
+  dim3 grid((unsigned)ceil_div(n, 4)), block(256);
+#define EBT_RN(DT)                                                                         \
+  if (v) hipLaunchKernelGGL((row_norms_kernel<DT, true>), grid, block, 0, st, x, n, d, ld, \
+                            gnorm, inv32);                                                 \
+  else hipLaunchKernelGGL((row_norms_kernel<DT, false>), grid, block, 0, st, x, n, d, ld,  \
+                          gnorm, inv32);
+  switch (dtype) {
+    case EBT_F32: EBT_RN(EBT_F32) break;
+    case EBT_BF16: EBT_RN(EBT_BF16) break;
+    case EBT_F16: EBT_RN(EBT_F16) break;
+    default: EBT_RN(EBT_F64) break;
+  }
+#undef EBT_RN
+  return launch_check("row_norms_kernel");
+}
+
+// ------------------------------------------------------------------------- screen image ----
+template <int DT, int IMG>
+__global__ __launch_bounds__(256) void screen_image_kernel(const void* __restrict__ x, int64_t n,
+                                                            int d, int64_t ld,
+                                                            const double* __restrict__ gnorm,
+                                                            int normalize,
+                                                            uint16_t* __restrict__ img,
+                                                            int ld_img) {
+  const int cpr = ld_img / 8;  // 16-byte chunks per image row
+  const int64_t total = n * cpr;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = t / cpr;
+    const int c = (int)(t - row * cpr);
+    const double s = normalize ? 1.0 / gnorm[row] : 1.0;
+    u16x8_t o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int j = c * 8 + e;
+      const double v = j < d ? load_as_f64<DT>(x, row * ld + j) * s : 0.0;
+      o[e] = f64_to_img<IMG>(v);
+    }
+    *(u16x8_t*)(img + row * ld_img + c * 8) = o;
+  }
+}
+
+int screen_image(const void* x, int dtype, int64_t n, int32_t d, int64_t ld,
+                 const double* gnorm, int normalize, int img_dtype, void* img, int32_t ld_img,
+                 hipStream_t st) {
+  if (!x || !img || n < 0 || d <= 0 || ld < d || ld_img < d || ld_img % 64 != 0 ||
+      (normalize && !gnorm) || (img_dtype != EBT_F16 && img_dtype != EBT_BF16) || dtype < 0 ||
+      dtype > 3 || ((uintptr_t)img & 15)) {
+    set_error("ebt_screen_image: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (n == 0) return EBT_OK;
+  const int64_t total = n * (ld_img / 8);
+  int64_t blocks = ceil_div(total, 256);
+  if (blocks > 65536) blocks = 65536;
+  dim3 grid((unsigned)blocks), block(256);
+#define EBT_SI(DT)                                                                             \
+  if (img_dtype == EBT_F16)                                                                    \
+    hipLaunchKernelGGL((screen_image_kernel<DT, EBT_F16>), grid, block, 0, st, x, n, d, ld,    \
+                       gnorm, normalize, (uint16_t*)img, ld_img);                              \
+  else                                                                                         \
+    hipLaunchKernelGGL((screen_image_kernel<DT, EBT_BF16>), grid, block, 0, st, x, n, d, ld,   \
+                       gnorm, normalize, (uint16_t*)img, ld_img);
+  switch (dtype) {
+    case EBT_F32: EBT_SI(EBT_F32) break;
+    case EBT_BF16: EBT_SI(EBT_BF16) break;
+    case EBT_F16: EBT_SI(EBT_F16) break;
+    default: EBT_SI(EBT_F64) break;
+  }
+#undef EBT_SI
+  return launch_check("screen_image_kernel");
+}
+
+// --------------------------------------------------------------------------- block sums ----
+__device__ __forceinline__ double block_sum_f64(double v, double* red) {
+  v = wave_sum_f64(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+  return s;
+}
+
+// ------------------------------------------------------------------------------ queries ----
+template <int DT>
+__global__ __launch_bounds__(256) void query_dense_kernel(const void* __restrict__ q, int d,
+                                                           int64_t ldq, double* __restrict__ q64) {
+  __shared__ double red[4];
+  const int64_t b = blockIdx.x;
+  double s = 0.0;
+  for (int j = threadIdx.x; j < d; j += blockDim.x) {
+    const double v = load_as_f64<DT>(q, b * ldq + j);
+    s += v * v;
+  }
+  const double g = guard_norm(sqrt(block_sum_f64(s, red)));
+  for (int j = threadIdx.x; j < d; j += blockDim.x)
+    q64[b * d + j] = load_as_f64<DT>(q, b * ldq + j) / g;
+}
+
+int query_dense(const void* q, int dtype, int64_t B, int32_t d, int64_t ldq, double* q64,
+                hipStream_t st) {
+  if (!q || !q64 || B < 0 || d <= 0 || ldq < d || dtype < 0 || dtype > 3) {
+    set_error("ebt_query_dense: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  dim3 grid((unsigned)B), block(256);
+  switch (dtype) {
+    case EBT_F32: hipLaunchKernelGGL(query_dense_kernel<EBT_F32>, grid, block, 0, st, q, d, ldq, q64); break;
+    case EBT_BF16: hipLaunchKernelGGL(query_dense_kernel<EBT_BF16>, grid, block, 0, st, q, d, ldq, q64); break;
+    case EBT_F16: hipLaunchKernelGGL(query_dense_kernel<EBT_F16>, grid, block, 0, st, q, d, ldq, q64); break;
+    default: hipLaunchKernelGGL(query_dense_kernel<EBT_F64>, grid, block, 0, st, q, d, ldq, q64); break;
+  }
+  return launch_check("query_dense_kernel");
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void query_liked_kernel(const void* __restrict__ cat, int d,
+                                                           int64_t ld,
+                                                           const double* __restrict__ gnorm,
+                                                           const int64_t* __restrict__ off,
+                                                           const int64_t* __restrict__ rows,
+                                                           double* __restrict__ q64) {
+  const int64_t b = blockIdx.x;
+  const int64_t l0 = off[b], l1 = off[b + 1];
+  for (int j = threadIdx.x; j < d; j += blockDim.x) {
+    double acc = 0.0;
+    for (int64_t l = l0; l < l1; ++l) {
+      const int64_t r = rows[l];
+      acc += load_as_f64<DT>(cat, r * ld + j) / gnorm[r];
+    }
+    q64[b * d + j] = acc;
+  }
+}
+
+int query_liked_sum(const void* cat, int dtype, int32_t d, int64_t ld, const double* gnorm,
+                    int64_t B, const int64_t* off, const int64_t* rows, double* q64,
+                    hipStream_t st) {
+  if (!cat || !gnorm || !off || !q64 || B < 0 || d <= 0 || ld < d || dtype < 0 || dtype > 3) {
+    set_error("ebt_query_liked_sum: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  dim3 grid((unsigned)B), block(256);
+  switch (dtype) {
+    case EBT_F32: hipLaunchKernelGGL(query_liked_kernel<EBT_F32>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, q64); break;
+    case EBT_BF16: hipLaunchKernelGGL(query_liked_kernel<EBT_BF16>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, q64); break;
+    case EBT_F16: hipLaunchKernelGGL(query_liked_kernel<EBT_F16>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, q64); break;
+    default: hipLaunchKernelGGL(query_liked_kernel<EBT_F64>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, q64); break;
+  }
+  return launch_check("query_liked_kernel");
+}
+
+__global__ void scale_rows_kernel(double* q64, int64_t total, int d, const double* scale) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x)
+    q64[t] *= scale[t / d];
+}
+
+int scale_rows_f64(double* q64, int64_t B, int32_t d, const double* scale, hipStream_t st) {
+  if (!q64 || !scale || B < 0 || d <= 0) {
+    set_error("ebt_scale_rows_f64: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  int64_t blocks = ceil_div(B * d, 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(scale_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, q64, B * d, d,
+                     scale);
+  return launch_check("scale_rows_kernel");
+}
+
+// ---------------------------------------------------------------------- query image/eps ----
+template <int IMG>
+__global__ __launch_bounds__(256) void query_image_kernel(
+    const double* __restrict__ q64, int64_t B, int d, const uint16_t* __restrict__ qn,
+    int64_t ldq, int native_q, float u_cat, uint16_t* __restrict__ qimg, int ld_img,
+    float* __restrict__ qscale, float* __restrict__ eps) {
+  __shared__ double red[4];
+  const int64_t b = blockIdx.x;
+  uint16_t* orow = qimg + b * ld_img;
+  if (b >= B) {  // padding rows
+    for (int j = threadIdx.x; j < ld_img; j += blockDim.x) orow[j] = 0;
+    if (threadIdx.x == 0) {
+      qscale[b] = 1.f;
+      if (eps) eps[b] = 0.f;
+    }
+    return;
+  }
+  double s = 0.0, sn = 0.0;
+  for (int j = threadIdx.x; j < d; j += blockDim.x) {
+    const double v = q64[b * d + j];
+    s += v * v;
+    if (native_q) {
+      const double w = IMG == EBT_F16 ? f16_bits_to_f64(qn[b * ldq + j]) : bf16_bits_to_f64(qn[b * ldq + j]);
+      sn += w * w;
+    }
+  }
+  const double qnrm = sqrt(block_sum_f64(s, red));
+  const double nrm_native = native_q ? sqrt(block_sum_f64(sn, red)) : 1.0;
+  for (int j = threadIdx.x; j < ld_img; j += blockDim.x) {
+    uint16_t o = 0;
+    if (j < d) o = native_q ? qn[b * ldq + j] : f64_to_img<IMG>(q64[b * d + j]);
+    orow[j] = o;
+  }
+  if (threadIdx.x == 0) {
+    qscale[b] = native_q ? (float)(1.0 / guard_norm(nrm_native)) : 1.f;
+    const double uq = native_q ? 0.0 : (IMG == EBT_F16 ? 0x1p-11 : 0x1p-8);
+    const double uc = (double)u_cat;
+    const double e = 1.05 * (qnrm * (uq + uc + uq * uc) + (d + 8) * 0x1p-24 * (qnrm + 1.0)) + 1e-9;
+    if (eps) eps[b] = (float)e;
+  }
+}
+
+int query_image(const double* q64, int64_t B, int64_t B_pad, int32_t d, int img_dtype,
+                const void* q_native, int64_t ldq, int native_q, float u_cat, void* qimg,
+                int32_t ld_img, float* qscale, float* eps, hipStream_t st) {
+  if (!q64 || !qimg || !qscale || B < 0 || B_pad < B || d <= 0 || ld_img < d ||
+      ld_img % 64 != 0 || (native_q && (!q_native || ldq < d)) ||
+      (img_dtype != EBT_F16 && img_dtype != EBT_BF16)) {
+    set_error("ebt_query_image: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (B_pad == 0) return EBT_OK;
+  dim3 grid((unsigned)B_pad), block(256);
+  if (img_dtype == EBT_F16)
+    hipLaunchKernelGGL(query_image_kernel<EBT_F16>, grid, block, 0, st, q64, B, d,
+                       (const uint16_t*)q_native, ldq, native_q, u_cat, (uint16_t*)qimg, ld_img,
+                       qscale, eps);
+  else
+    hipLaunchKernelGGL(query_image_kernel<EBT_BF16>, grid, block, 0, st, q64, B, d,
+                       (const uint16_t*)q_native, ldq, native_q, u_cat, (uint16_t*)qimg, ld_img,
+                       qscale, eps);
+  return launch_check("query_image_kernel");
+}
+
+// ------------------------------------------------------------------------- exclusions ------
+__global__ __launch_bounds__(256) void mask_excluded_kernel(float* __restrict__ s, int64_t ld,
+                                                             int64_t c0, int64_t c1,
+                                                             const int64_t* __restrict__ off,
+                                                             const int64_t* __restrict__ rows) {
+  const int64_t b = blockIdx.x;
+  for (int64_t i = off[b] + threadIdx.x; i < off[b + 1]; i += blockDim.x) {
+    const int64_t g = rows[i];
+    if (g >= c0 && g < c1) s[b * ld + (g - c0)] = -__builtin_inff();
+  }
+}
+
+int mask_excluded(float* s, int64_t ld, int64_t B, int64_t c0, int64_t c1, const int64_t* off,
+                  const int64_t* rows, hipStream_t st) {
+  if (!s || !off || B < 0 || c1 < c0 || ld < c1 - c0) {
+    set_error("ebt_mask_excluded: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  hipLaunchKernelGGL(mask_excluded_kernel, dim3((unsigned)B), dim3(256), 0, st, s, ld, c0, c1,
+                     off, rows);
+  return launch_check("mask_excluded_kernel");
+}
+
+}  // namespace ebt

@@ -1,0 +1,243 @@
+// Exact float64 rescore of the screened candidates, final top-k, certification; and the
+// cross-shard merge of partial top-k lists.
+//
+// The reference's arithmetic is float64 end to end (constants.py:56 builds a float64 DataFrame;
+// sklearn keeps float64 unless both inputs are float32, metrics/pairwise.py:67). The screening
+// GEMM runs in f16/bf16 MFMA, so its scores are approximations with a per-query error bound
+// eps (prep.hip). Here every candidate is recomputed as (q64 . c) / gnorm64(c) in float64 --
+// the same value as sklearn's normalize-then-dot up to float64 round-off -- and the k best are
+// chosen by (score desc, row asc). The candidate set is PROVABLY a superset of the true top-k
+// when approx[k'-1] < approx[k-1] - 2 eps ("certified-margin rescore");
+// otherwise certified[b] = 0 and the host retries that query with a larger k'.
+#include "common.h"
+
+namespace ebt {
+
+constexpr int RTHREADS = 256;
+
+__device__ __forceinline__ bool pair_before(double sa, int64_t ra, double sb, int64_t rb) {
+  return sa > sb || (sa == sb && ra < rb);
+}
+
+// Sort (score, row) pairs: score desc, row asc. P power of two.
+__device__ void bitonic_pairs(double* sc, int64_t* rw, int P) {
+  const int tid = threadIdx.x;
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < (P >> 1); t += blockDim.x) {
+        const int lo = 2 * stride * (t / stride) + (t % stride);
+        const int hi = lo + stride;
+        const double a = sc[lo], b = sc[hi];
+        const int64_t ra = rw[lo], rb = rw[hi];
+        const bool first = (lo & size) == 0;  // this segment ends up in "before" order
+        const bool swap = first ? pair_before(b, rb, a, ra) : pair_before(a, ra, b, rb);
+        if (swap) {
+          sc[lo] = b;
+          sc[hi] = a;
+          rw[lo] = rb;
+          rw[hi] = ra;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+static int next_pow2_h(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+template <int DT, bool VEC>
+__global__ __launch_bounds__(RTHREADS) void rescore_kernel(
+    const double* __restrict__ q64, int d, const void* __restrict__ cat, int64_t ld,
+    const double* __restrict__ gnorm, int64_t row_offset, const float* __restrict__ cand_vals,
+    const int64_t* __restrict__ cand_rows, int kprime, int kpp, int k, int64_t n_rows,
+    const float* __restrict__ eps, double* __restrict__ out_s, int64_t* __restrict__ out_r,
+    int32_t* __restrict__ certified) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* qs = (double*)smem;                 // d
+  double* sc = qs + ((d + 1) & ~1);           // kpp
+  int64_t* rw = (int64_t*)(sc + kpp);         // kpp
+  __shared__ int nvalid;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = blockIdx.x;
+  if (tid == 0) nvalid = 0;
+  for (int j = tid; j < d; j += RTHREADS) qs[j] = q64[b * d + j];
+  __syncthreads();
+  const int64_t* cr = cand_rows + b * kprime;
+  int myvalid = 0;
+  for (int c = wave; c < kprime; c += RTHREADS / 64) {
+    const int64_t row = cr[c];
+    double s = 0.0;
+    if (row >= 0) {
+      if constexpr (VEC) {
+        constexpr int ES = (DT == EBT_F64) ? 8 : (DT == EBT_F32 ? 4 : 2);
+        constexpr int PER = 16 / ES;
+        const char* base = (const char*)cat + row * ld * ES;
+        for (int ch = lane; ch < d / PER; ch += 64) {
+          const uint4 raw = *(const uint4*)(base + (int64_t)ch * 16);
+          const int j0 = ch * PER;
+          if constexpr (DT == EBT_F32) {
+            const float* f = (const float*)&raw;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s += qs[j0 + e] * (double)f[e];
+          } else if constexpr (DT == EBT_F64) {
+            const double* f = (const double*)&raw;
+            s += qs[j0] * f[0] + qs[j0 + 1] * f[1];
+          } else {
+            const uint16_t* h = (const uint16_t*)&raw;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              s += qs[j0 + e] * (DT == EBT_BF16 ? bf16_bits_to_f64(h[e]) : f16_bits_to_f64(h[e]));
+          }
+        }
+      } else {
+        for (int j = lane; j < d; j += 64) s += qs[j] * load_as_f64<DT>(cat, row * ld + j);
+      }
+    }
+    s = wave_sum_f64(s);
+    if (lane == 0) {
+      if (row >= 0) {
+        const double v = s / gnorm[row];
+        sc[c] = (v == v) ? v : -__builtin_inf();
+        rw[c] = row;
+        ++myvalid;
+      } else {
+        sc[c] = -__builtin_inf();
+        rw[c] = INT64_MAX;
+      }
+    }
+  }
+  for (int c = kprime + tid; c < kpp; c += RTHREADS) {
+    sc[c] = -__builtin_inf();
+    rw[c] = INT64_MAX;
+  }
+  if (lane == 0 && myvalid) atomicAdd(&nvalid, myvalid);
+  __syncthreads();
+  bitonic_pairs(sc, rw, kpp);
+  for (int j = tid; j < k; j += RTHREADS) {
+    const int64_t r = rw[j];
+    if (r == INT64_MAX) {
+      out_s[b * k + j] = __builtin_nan("");
+      out_r[b * k + j] = -1;
+    } else {
+      out_s[b * k + j] = sc[j];
+      out_r[b * k + j] = r + row_offset;
+    }
+  }
+  if (tid == 0) {
+    int ok = 1;
+    if (nvalid >= kprime && n_rows > kprime) {  // kprime >= n_rows: every row is a candidate
+      const float* cv = cand_vals + b * kprime;
+      const double T = (double)cv[k - 1];
+      const double amin = (double)cv[kprime - 1];
+      ok = amin < T - 2.0 * (double)eps[b];
+    }
+    certified[b] = ok;
+  }
+}
+
+size_t rescore_lds_bytes(int d, int kprime) {
+  const int kpp = next_pow2_h(kprime);
+  return 8 * (size_t)((d + 1) & ~1) + 16 * (size_t)kpp;
+}
+
+int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype, int64_t ld,
+            const double* gnorm, int64_t row_offset, const float* cand_vals,
+            const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
+            double* out_s, int64_t* out_r, int32_t* certified, hipStream_t st) {
+  if (!q64 || !cat || !gnorm || !cand_vals || !cand_rows || !eps || !out_s || !out_r ||
+      !certified || B < 0 || d <= 0 || ld < d || k < 1 || kprime < k || kprime > 4096 ||
+      dtype < 0 || dtype > 3) {
+    set_error("ebt_rescore: bad arguments (d=%d k=%d kprime=%d)", d, k, kprime);
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  const int kpp = next_pow2_h(kprime);
+  const size_t lds = rescore_lds_bytes(d, kprime);
+  if (lds > 150 * 1024) {
+    set_error("ebt_rescore: d=%d with kprime=%d exceeds LDS", d, kprime);
+    return EBT_EUNSUPPORTED;
+  }
+  const int es = dtype == EBT_F64 ? 8 : (dtype == EBT_F32 ? 4 : 2);
+  const bool vec = (((uintptr_t)cat & 15) == 0) && ((ld * es) % 16 == 0) &&
+                   (((int64_t)d * es) % 16 == 0);
+  dim3 grid((unsigned)B), block(RTHREADS);
+#define EBT_RS(DT)                                                                              \
+  (void)hipFuncSetAttribute((const void*)rescore_kernel<DT, true>,                              \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
+  (void)hipFuncSetAttribute((const void*)rescore_kernel<DT, false>,                             \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
+  if (vec)                                                                                      \
+    hipLaunchKernelGGL((rescore_kernel<DT, true>), grid, block, lds, st, q64, d, cat, ld,       \
+                       gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps, out_s, \
+                       out_r, certified);                                                       \
+  else                                                                                          \
+    hipLaunchKernelGGL((rescore_kernel<DT, false>), grid, block, lds, st, q64, d, cat, ld,      \
+                       gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps, out_s, \
+                       out_r, certified);
+  switch (dtype) {
+    case EBT_F32: EBT_RS(EBT_F32) break;
+    case EBT_BF16: EBT_RS(EBT_BF16) break;
+    case EBT_F16: EBT_RS(EBT_F16) break;
+    default: EBT_RS(EBT_F64) break;
+  }
+#undef EBT_RS
+  return launch_check("rescore_kernel");
+}
+
+// ------------------------------------------------------------------------------- merge -----
+__global__ __launch_bounds__(RTHREADS) void merge_topk_kernel(const double* __restrict__ scores,
+                                                               const int64_t* __restrict__ rows,
+                                                               int R, int64_t B, int k, int P,
+                                                               double* __restrict__ out_s,
+                                                               int64_t* __restrict__ out_r) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* sc = (double*)smem;
+  int64_t* rw = (int64_t*)(sc + P);
+  const int64_t b = blockIdx.x;
+  const int n = R * k;
+  for (int i = threadIdx.x; i < P; i += RTHREADS) {
+    double s = -__builtin_inf();
+    int64_t r = INT64_MAX;
+    if (i < n) {
+      const int rr = i / k, j = i - rr * k;
+      const int64_t off = ((int64_t)rr * B + b) * k + j;
+      const int64_t row = rows[off];
+      if (row >= 0) {
+        const double v = scores[off];
+        s = (v == v) ? v : -__builtin_inf();
+        r = row;
+      }
+    }
+    sc[i] = s;
+    rw[i] = r;
+  }
+  __syncthreads();
+  bitonic_pairs(sc, rw, P);
+  for (int j = threadIdx.x; j < k; j += RTHREADS) {
+    const int64_t r = rw[j];
+    out_s[b * k + j] = r == INT64_MAX ? __builtin_nan("") : sc[j];
+    out_r[b * k + j] = r == INT64_MAX ? -1 : r;
+  }
+}
+
+int merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, int32_t k,
+               double* out_s, int64_t* out_r, hipStream_t st) {
+  if (!scores || !rows || !out_s || !out_r || R < 1 || B < 0 || k < 1 ||
+      (int64_t)R * k > 8192) {
+    set_error("ebt_merge_topk: bad arguments (R=%d k=%d; R*k must be <= 8192)", R, k);
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  const int P = next_pow2_h(R * k);
+  (void)hipFuncSetAttribute((const void*)merge_topk_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(P * 16));
+  hipLaunchKernelGGL(merge_topk_kernel, dim3((unsigned)B), dim3(RTHREADS), (size_t)P * 16, st,
+                     scores, rows, R, B, k, P, out_s, out_r);
+  return launch_check("merge_topk_kernel");
+}
+
+}  // namespace ebt

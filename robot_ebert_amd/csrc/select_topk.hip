@@ -1,0 +1,382 @@
+// Streaming top-k' select: one HBM pass over each score row.
+//
+// Replaces `movie_scores.loc[unrated].sort_values(ascending=False)[:k]` (lib.py:55; pandas
+// core/series.py:3706-3716, a full O(N log N) argsort) with a single streaming pass per row
+// segment. One 256-thread workgroup owns a (row, segment); it streams the segment in 4096-entry
+// tiles (16 values per lane, float4 loads, next tile prefetched into registers) and keeps a
+// candidate buffer in LDS:
+//   * an entry is admitted when its order-preserving key >= thr (initially every valid entry);
+//     admission is wave-aggregated: one ballot + one LDS atomic per wave per value slot;
+//   * when the buffer cannot take another full tile, it is compacted to exactly its k' best
+//     entries by an adaptive-range radix select (11-bit histograms over the live [min, max] of
+//     the 64-bit composite (key, ~index), so hot bins stay spread out), and thr rises to the
+//     k'-th key -- after the first couple of tiles almost nothing passes the filter;
+//   * at the end the k' survivors are bitonic-sorted in LDS by (value desc, index asc).
+// Composites are unique (indices are), so the result is deterministic: exactly the k' largest
+// (value, -index) pairs. NaN and -inf (masked / excluded) entries have key 0 and never enter.
+#include "common.h"
+
+namespace ebt {
+
+constexpr int STHREADS = 256;
+constexpr int SE = 16;                  // values per lane per tile
+constexpr int STILE = STHREADS * SE;    // 4096 entries per tile
+constexpr int SHIST = 2048;             // histogram bins (11 bits)
+constexpr int KPRIME_MAX = 4096;
+
+__host__ __device__ inline int next_pow2(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+struct SelLayout {
+  int cap;       // buffer capacity (entries)
+  int kpp;       // next pow2 >= kprime
+  size_t off_key, off_idx, off_keep, off_misc, bytes;
+};
+
+__host__ __device__ inline SelLayout sel_layout(int kprime) {
+  SelLayout L;
+  L.cap = kprime + 2 * STILE;
+  L.kpp = next_pow2(kprime);
+  L.off_key = 0;
+  L.off_idx = L.off_key + 4 * (size_t)L.cap;
+  L.off_keep = L.off_idx + 4 * (size_t)L.cap;
+  L.off_keep = (L.off_keep + 15) & ~(size_t)15;
+  size_t keep_bytes = 8 * (size_t)L.kpp;
+  if (keep_bytes < 4 * (size_t)SHIST) keep_bytes = 4 * (size_t)SHIST;  // aliased with hist
+  L.off_misc = L.off_keep + keep_bytes;
+  L.bytes = L.off_misc + 256;
+  return L;
+}
+
+__device__ __forceinline__ uint64_t comp_of(uint32_t key, uint32_t idx) {
+  return ((uint64_t)key << 32) | (uint64_t)(~idx);
+}
+
+// block-wide min / max of u64 (all threads get the result). red: >= 8 u64 of LDS.
+__device__ __forceinline__ void block_minmax_u64(uint64_t& mn, uint64_t& mx, uint64_t* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    red[w] = mn;
+    red[4 + w] = mx;
+  }
+  __syncthreads();
+  mn = red[0];
+  mx = red[4];
+#pragma unroll
+  for (int i = 1; i < 4; ++i) {
+    mn = red[i] < mn ? red[i] : mn;
+    mx = red[4 + i] > mx ? red[4 + i] : mx;
+  }
+}
+
+// theta = the rank-th largest composite among the n buffer entries (1 <= rank <= n).
+__device__ uint64_t select_rank(const uint32_t* bkey, const uint32_t* bidx, int n, int rank,
+                                uint32_t* hist, uint64_t* red, uint32_t* misc) {
+  const int tid = threadIdx.x;
+  uint64_t lo = 0, hi = ~0ull;
+  int r = rank;
+  for (int iter = 0; iter < 16; ++iter) {
+    uint64_t mn = ~0ull, mx = 0;
+    for (int i = tid; i < n; i += STHREADS) {
+      const uint64_t c = comp_of(bkey[i], bidx[i]);
+      if (c >= lo && c <= hi) {
+        mn = c < mn ? c : mn;
+        mx = c > mx ? c : mx;
+      }
+    }
+    block_minmax_u64(mn, mx, red);
+    if (mn == mx) return mn;
+    const uint64_t span = mx - mn;
+    const int bits = 64 - __builtin_clzll(span);
+    const int shift = bits > 11 ? bits - 11 : 0;
+#pragma unroll
+    for (int j = 0; j < SHIST / STHREADS; ++j) hist[tid * (SHIST / STHREADS) + j] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += STHREADS) {
+      const uint64_t c = comp_of(bkey[i], bidx[i]);
+      if (c >= mn && c <= mx) atomicAdd(&hist[(uint32_t)((c - mn) >> shift)], 1u);
+    }
+    __syncthreads();
+    // suffix scan: thread t owns bins [8t, 8t+8)
+    uint32_t hv[SHIST / STHREADS];
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < SHIST / STHREADS; ++j) {
+      hv[j] = hist[tid * (SHIST / STHREADS) + j];
+      s += hv[j];
+    }
+    uint32_t x = s;  // inclusive suffix within the wave (lanes >= me)
+    const int lane = tid & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      uint32_t y = __shfl_down(x, o, 64);
+      if (lane + o < 64) x += y;
+    }
+    uint32_t* wtot = misc + 8;
+    if (lane == 0) wtot[tid >> 6] = x;
+    __syncthreads();
+    uint32_t above = x - s;
+    for (int w2 = (tid >> 6) + 1; w2 < 4; ++w2) above += wtot[w2];
+    if (above < (uint32_t)r && (uint32_t)r <= above + s) {
+      uint32_t cum = above;
+      for (int j = SHIST / STHREADS - 1; j >= 0; --j) {
+        if (cum + hv[j] >= (uint32_t)r) {
+          misc[0] = tid * (SHIST / STHREADS) + j;
+          misc[1] = cum;
+          break;
+        }
+        cum += hv[j];
+      }
+    }
+    __syncthreads();
+    const uint32_t b = misc[0];
+    r -= (int)misc[1];
+    __syncthreads();  // misc reused next iteration
+    lo = mn + ((uint64_t)b << shift);
+    const uint64_t w = (shift >= 64) ? ~0ull : ((1ull << shift) - 1);
+    hi = (mx - lo) < w ? mx : lo + w;
+    if (shift == 0) return lo;
+  }
+  return lo;  // not reached for unique composites
+}
+
+// Keep exactly min(rank, n) best entries: buffer -> keep (unordered) -> buffer[0..).
+// Returns theta (rank-th composite). n > rank required.
+__device__ uint64_t compact(uint32_t* bkey, uint32_t* bidx, int n, int rank, uint64_t* keep,
+                            uint32_t* hist, uint64_t* red, uint32_t* misc) {
+  const uint64_t theta = select_rank(bkey, bidx, n, rank, hist, red, misc);
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (tid == 0) misc[2] = 0;
+  __syncthreads();  // hist (aliased with keep) is dead from here
+  for (int base = 0; base < n; base += STHREADS) {
+    const int i = base + tid;
+    uint64_t c = 0;
+    bool take = false;
+    if (i < n) {
+      c = comp_of(bkey[i], bidx[i]);
+      take = c >= theta;
+    }
+    const uint64_t m = __ballot(take);
+    if (m) {
+      uint32_t wb = 0;
+      if (lane == 0) wb = atomicAdd(&misc[2], (uint32_t)__popcll(m));
+      wb = __shfl(wb, 0, 64);
+      if (take) {
+        const uint32_t pos = wb + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+        keep[pos] = c;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < rank; i += STHREADS) {
+    const uint64_t c = keep[i];
+    bkey[i] = (uint32_t)(c >> 32);
+    bidx[i] = ~(uint32_t)c;
+  }
+  __syncthreads();
+  return theta;
+}
+
+// Descending bitonic sort of keep[0..P) (P power of two).
+__device__ void bitonic_desc(uint64_t* keep, int P) {
+  const int tid = threadIdx.x;
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < (P >> 1); t += STHREADS) {
+        const int lo = 2 * stride * (t / stride) + (t % stride);
+        const int hi = lo + stride;
+        const uint64_t a = keep[lo], b = keep[hi];
+        const bool desc = (lo & size) == 0;
+        if ((a < b) == desc) {
+          keep[lo] = b;
+          keep[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <bool HAS_IDX, bool VEC>
+__global__ __launch_bounds__(STHREADS, 2) void select_topk_kernel(
+    const float* __restrict__ vals, const int64_t* __restrict__ idxs, int64_t ld, int64_t n,
+    int64_t seg_len, int64_t idx_base, int kprime, float* __restrict__ out_vals,
+    int64_t* __restrict__ out_idx, int64_t ld_out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const SelLayout Lo = sel_layout(kprime);
+  uint32_t* bkey = (uint32_t*)(smem + Lo.off_key);
+  uint32_t* bidx = (uint32_t*)(smem + Lo.off_idx);
+  uint64_t* keep = (uint64_t*)(smem + Lo.off_keep);
+  uint32_t* hist = (uint32_t*)(smem + Lo.off_keep);  // aliased
+  uint64_t* red = (uint64_t*)(smem + Lo.off_misc);
+  uint32_t* misc = (uint32_t*)(smem + Lo.off_misc + 64);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int64_t row = blockIdx.y;
+  const int seg = blockIdx.x;
+  const int64_t s0 = (int64_t)seg * seg_len;
+  int64_t s1 = s0 + seg_len;
+  s1 = s1 < n ? s1 : n;
+  const float* vrow = vals + row * ld;
+  const int64_t* irow = HAS_IDX ? idxs + row * ld : nullptr;
+
+  if (tid == 0) misc[3] = 0;  // nbuf counter
+  __syncthreads();
+  uint32_t thr = 1;
+  int nbuf = 0;
+
+  float cur[SE], nxt[SE];
+  int64_t curi[SE], nxti[SE];
+  auto load_tile = [&](int64_t t0, float* v, int64_t* ix) {
+#pragma unroll
+    for (int j = 0; j < SE / 4; ++j) {
+      const int64_t p = t0 + j * (STHREADS * 4) + tid * 4;
+      if constexpr (VEC) {
+        if (p < s1) {
+          const float4 f = *(const float4*)(vrow + p);
+          v[4 * j + 0] = f.x;
+          v[4 * j + 1] = f.y;
+          v[4 * j + 2] = f.z;
+          v[4 * j + 3] = f.w;
+          if constexpr (HAS_IDX) {
+            const longlong2 a = *(const longlong2*)(irow + p);
+            const longlong2 b = *(const longlong2*)(irow + p + 2);
+            ix[4 * j + 0] = a.x;
+            ix[4 * j + 1] = a.y;
+            ix[4 * j + 2] = b.x;
+            ix[4 * j + 3] = b.y;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[4 * j + e] = -__builtin_inff();
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t pe = p + e;
+          v[4 * j + e] = pe < s1 ? vrow[pe] : -__builtin_inff();
+          if constexpr (HAS_IDX) ix[4 * j + e] = pe < s1 ? irow[pe] : -1;
+        }
+      }
+    }
+  };
+
+  const int64_t ntiles = (s1 - s0 + STILE - 1) / STILE;
+  if (ntiles > 0) load_tile(s0, cur, curi);
+  for (int64_t t = 0; t < ntiles; ++t) {
+    const int64_t t0 = s0 + t * STILE;
+    if (nbuf + STILE > Lo.cap) {
+      const uint64_t theta = compact(bkey, bidx, nbuf, kprime, keep, hist, red, misc);
+      nbuf = kprime;
+      const uint32_t tau = (uint32_t)(theta >> 32);
+      thr = HAS_IDX ? tau : tau + 1u;
+      if (tid == 0) misc[3] = (uint32_t)nbuf;
+      __syncthreads();
+    }
+    if (t + 1 < ntiles) load_tile(t0 + STILE, nxt, nxti);
+#pragma unroll
+    for (int e = 0; e < SE; ++e) {
+      const int64_t p = t0 + (e >> 2) * (STHREADS * 4) + tid * 4 + (e & 3);
+      uint32_t key = p < s1 ? f2key(cur[e]) : 0u;
+      uint32_t ix;
+      if constexpr (HAS_IDX) {
+        if (curi[e] < 0) key = 0u;
+        ix = (uint32_t)curi[e];
+      } else {
+        ix = (uint32_t)p;
+      }
+      const bool take = key >= thr;
+      const uint64_t m = __ballot(take);
+      if (m) {
+        uint32_t wb = 0;
+        if (lane == 0) wb = atomicAdd(&misc[3], (uint32_t)__popcll(m));
+        wb = __shfl(wb, 0, 64);
+        if (take) {
+          const uint32_t pos = wb + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+          bkey[pos] = key;
+          bidx[pos] = ix;
+        }
+      }
+    }
+    __syncthreads();
+    nbuf = (int)misc[3];
+    if (t + 1 < ntiles) {
+#pragma unroll
+      for (int e = 0; e < SE; ++e) {
+        cur[e] = nxt[e];
+        if constexpr (HAS_IDX) curi[e] = nxti[e];
+      }
+    }
+  }
+
+  // final: exactly min(kprime, nbuf) survivors, sorted
+  int nk = nbuf;
+  if (nbuf > kprime) {
+    compact(bkey, bidx, nbuf, kprime, keep, hist, red, misc);
+    nk = kprime;
+  }
+  const int P = Lo.kpp;
+  for (int i = tid; i < P; i += STHREADS) keep[i] = i < nk ? comp_of(bkey[i], bidx[i]) : 0ull;
+  __syncthreads();
+  bitonic_desc(keep, P);
+  float* ov = out_vals + row * ld_out + (int64_t)seg * kprime;
+  int64_t* oi = out_idx + row * ld_out + (int64_t)seg * kprime;
+  for (int i = tid; i < kprime; i += STHREADS) {
+    const uint64_t c = keep[i];
+    const uint32_t key = (uint32_t)(c >> 32);
+    if (key == 0u) {
+      ov[i] = -__builtin_inff();
+      oi[i] = -1;
+    } else {
+      ov[i] = key2f(key);
+      const uint32_t ix = ~(uint32_t)c;
+      oi[i] = HAS_IDX ? (int64_t)(int32_t)ix : idx_base + (int64_t)ix;
+    }
+  }
+}
+
+size_t select_lds_bytes(int kprime) { return sel_layout(kprime).bytes; }
+
+int select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B, int64_t n,
+                int64_t idx_base, int32_t kprime, int32_t segs, float* out_vals,
+                int64_t* out_idx, int64_t ld_out, hipStream_t stream) {
+  if (!vals || !out_vals || !out_idx || B < 0 || n < 0 || ld < n || segs < 1 || kprime < 1 ||
+      kprime > KPRIME_MAX || ld_out < (int64_t)segs * kprime || n >= 0x7fffffffLL) {
+    set_error("ebt_select_topk: bad arguments (B=%lld n=%lld ld=%lld kprime=%d segs=%d)",
+              (long long)B, (long long)n, (long long)ld, kprime, segs);
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  int64_t seg_len = ceil_div(n > 0 ? n : 1, segs);
+  seg_len = (seg_len + 3) & ~(int64_t)3;
+  const bool vec = (ld % 4 == 0) && (((uintptr_t)vals & 15) == 0) &&
+                   (!idx || ((uintptr_t)idx & 15) == 0);
+  const size_t lds = select_lds_bytes(kprime);
+  dim3 grid((unsigned)segs, (unsigned)B), block(STHREADS);
+#define EBT_SEL_LAUNCH(H, V)                                                                  \
+  (void)hipFuncSetAttribute((const void*)select_topk_kernel<H, V>,                            \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
+  hipLaunchKernelGGL((select_topk_kernel<H, V>), grid, block, lds, stream, vals, idx, ld, n, \
+                     seg_len, idx_base, (int)kprime, out_vals, out_idx, ld_out)
+  if (idx) {
+    if (vec) { EBT_SEL_LAUNCH(true, true); }
+    else { EBT_SEL_LAUNCH(true, false); }
+  } else {
+    if (vec) { EBT_SEL_LAUNCH(false, true); }
+    else { EBT_SEL_LAUNCH(false, false); }
+  }
+#undef EBT_SEL_LAUNCH
+  return launch_check("select_topk_kernel");
+}
+
+}  // namespace ebt

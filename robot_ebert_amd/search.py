@@ -1,0 +1,265 @@
+"""Query x catalog cosine top-k on the GPU: the replacement of ``lib.py:51-55``.
+
+    pairwise_similarities = cosine_similarity(catalog.loc[liked], catalog)      # lib.py:51
+    movie_scores = pd.Series(pairwise_similarities.mean(axis=0), ...)           # lib.py:52
+    recommended = movie_scores.loc[unrated].sort_values(ascending=False)[:k]    # lib.py:55
+
+``score_topk`` takes a batch of queries -- either dense vectors (the L = 1 case, BASELINE
+configs C2-C5) or per-user lists of liked catalog rows (the collaborative path, folded into one
+query vector per user: q = mean_l normalize(x_l), lib.py:51-52) -- plus optional per-query
+excluded rows (the rated movies, lib.py:48,55), and returns the top-k (score desc, row asc) with
+float64 scores equal to the reference's float64 arithmetic.
+
+Pipeline (all on the caller's current HIP stream, see include/ebert.h):
+  query prep -> [per catalog chunk: MFMA screening GEMM -> mask excluded -> streaming top-k'
+  select] -> select across chunks -> exact float64 rescore + certification. Queries whose
+candidate set cannot be certified (a tie cluster wider than k' at the k-th score) are re-run
+with a 4x larger k'; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence, Tuple, Union
+
+import torch
+
+from . import _lib
+from ._lib import DTYPE_CODE, EbertError, call, ptr, require_cuda, stream_of
+from .catalog import Catalog
+
+KPRIME_MAX = 4096
+DEFAULT_SCORE_BUDGET = int(os.environ.get("EBT_SCORE_BUDGET", str(4 << 30)))  # bytes of f32 scores
+
+
+def _round_up(v: int, m: int) -> int:
+    return (v + m - 1) // m * m
+
+
+@dataclass
+class QueryBatch:
+    """Device-side prepared queries (ebt_query_* outputs)."""
+    q64: torch.Tensor      # [B, d] float64 (normalised query / mean of normalised liked rows)
+    qimg: torch.Tensor     # [B_pad, ld_img] f16/bf16 MFMA operand
+    qscale: torch.Tensor   # [B_pad] float32 epilogue scale
+    eps: torch.Tensor      # [B_pad] float32 certification bound
+    B: int
+
+    @property
+    def B_pad(self) -> int:
+        return int(self.qimg.shape[0])
+
+    def subset(self, idx: torch.Tensor) -> "QueryBatch":
+        n = int(idx.numel())
+        B_pad = _round_up(max(n, 1), 128)
+        qimg = torch.zeros((B_pad, self.qimg.shape[1]), dtype=self.qimg.dtype, device=self.qimg.device)
+        qimg[:n] = self.qimg.index_select(0, idx)
+        qscale = torch.ones(B_pad, dtype=torch.float32, device=self.qimg.device)
+        qscale[:n] = self.qscale.index_select(0, idx)
+        eps = torch.zeros(B_pad, dtype=torch.float32, device=self.qimg.device)
+        eps[:n] = self.eps.index_select(0, idx)
+        return QueryBatch(self.q64.index_select(0, idx).contiguous(), qimg, qscale, eps, n)
+
+
+def csr_from_lists(lists: Sequence[Sequence[int]], device) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Host lists of row ids -> device CSR (offsets int64 [B+1], rows int64 [nnz])."""
+    off = [0]
+    flat = []
+    for l in lists:
+        flat.extend(int(v) for v in l)
+        off.append(len(flat))
+    o = torch.tensor(off, dtype=torch.int64, device=device)
+    r = torch.tensor(flat if flat else [0], dtype=torch.int64, device=device)
+    return o, r
+
+
+def csr_subset(off: torch.Tensor, rows: torch.Tensor, idx: torch.Tensor):
+    """Rows `idx` of a device CSR (torch ops only; used for the certification retry)."""
+    starts = off.index_select(0, idx)
+    lens = off.index_select(0, idx + 1) - starts
+    new_off = torch.zeros(idx.numel() + 1, dtype=torch.int64, device=off.device)
+    new_off[1:] = torch.cumsum(lens, 0)
+    total = int(new_off[-1].item())
+    if total == 0:
+        return new_off, torch.zeros(1, dtype=torch.int64, device=off.device)
+    seg = torch.repeat_interleave(torch.arange(idx.numel(), device=off.device), lens)
+    pos = torch.arange(total, device=off.device) - new_off[:-1].index_select(0, seg)
+    return new_off, rows.index_select(0, starts.index_select(0, seg) + pos)
+
+
+def prepare_queries(catalog: Catalog, queries: Optional[torch.Tensor] = None,
+                    liked: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                    liked_counts: Optional[torch.Tensor] = None,
+                    liked_sum_hook=None) -> QueryBatch:
+    """Build q64 / qimg / qscale / eps for a batch.
+
+    queries : dense [B, d] CUDA tensor (any supported dtype), or
+    liked   : device CSR (offsets [B+1], LOCAL rows) of liked catalog rows per user; the query is
+              sum_l x_l/||x_l|| divided by liked_counts (default: the CSR lengths). liked_sum_hook,
+              if given, is applied to the float64 sums before the division (the cross-shard
+              all-reduce of a row-sharded catalog).
+    """
+    dev = catalog.device
+    st = stream_of(dev)
+    d = catalog.d
+    if (queries is None) == (liked is None):
+        raise EbertError("pass exactly one of queries= or liked=")
+    native_q = False
+    if queries is not None:
+        require_cuda(queries, "queries")
+        if queries.dim() != 2 or queries.shape[1] != d:
+            raise EbertError(f"queries must be [B, {d}], got {tuple(queries.shape)}")
+        if queries.dtype not in DTYPE_CODE:
+            raise EbertError(f"unsupported query dtype {queries.dtype}")
+        if queries.stride(1) != 1:
+            queries = queries.contiguous()
+        B = int(queries.shape[0])
+        q64 = torch.empty((B, d), dtype=torch.float64, device=dev)
+        call("ebt_query_dense", ptr(queries), DTYPE_CODE[queries.dtype], B, d,
+             int(queries.stride(0)), ptr(q64), st)
+        native_q = catalog.native and queries.dtype == catalog.img_torch_dtype
+    else:
+        off, rows = liked
+        B = int(off.numel()) - 1
+        q64 = torch.empty((B, d), dtype=torch.float64, device=dev)
+        local = rows - catalog.row_offset if catalog.row_offset else rows
+        call("ebt_query_liked_sum", ptr(catalog.data), catalog.dtype_code, d, catalog.ld,
+             ptr(catalog.gnorm), B, ptr(off), ptr(local), ptr(q64), st)
+        if liked_sum_hook is not None:
+            q64 = liked_sum_hook(q64)
+        counts = liked_counts if liked_counts is not None else (off[1:] - off[:-1])
+        if bool((counts <= 0).any().item()):
+            raise ValueError(
+                f"Found array with 0 sample(s) (shape=(0, {d})) while a minimum of 1 is required "
+                "by check_pairwise_arrays.")
+        scale = (1.0 / counts.to(torch.float64)).contiguous()
+        call("ebt_scale_rows_f64", ptr(q64), B, d, ptr(scale), st)
+    B_pad = _round_up(max(B, 1), 128)
+    qimg = torch.empty((B_pad, catalog.ld_img), dtype=catalog.img_torch_dtype, device=dev)
+    qscale = torch.empty(B_pad, dtype=torch.float32, device=dev)
+    eps = torch.empty(B_pad, dtype=torch.float32, device=dev)
+    call("ebt_query_image", ptr(q64), B, B_pad, d, catalog.img_dtype,
+         ptr(queries) if native_q else None, int(queries.stride(0)) if native_q else 0,
+         1 if native_q else 0, float(catalog.u_cat), ptr(qimg), catalog.ld_img, ptr(qscale),
+         ptr(eps), st)
+    return QueryBatch(q64, qimg, qscale, eps, B)
+
+
+def default_kprime(catalog: Catalog, k: int) -> int:
+    """Screening width: native images have a tiny error bound, f16 images need more slack."""
+    kp = k + 16 if catalog.native else max(2 * k, k + 32)
+    return min(_round_up(kp, 8), KPRIME_MAX)
+
+
+def _chunk_rows(catalog: Catalog, B_pad: int, budget: int) -> int:
+    rows = budget // (4 * B_pad)
+    rows = max(128, rows // 128 * 128)
+    return min(rows, _round_up(catalog.n, 128))
+
+
+def run_pipeline(catalog: Catalog, qb: QueryBatch, k: int, kprime: int,
+                 exclude: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                 chunk_rows: Optional[int] = None, timer: Optional[_lib.Timer] = None,
+                 workspace: Optional[torch.Tensor] = None):
+    """One ebt_cosine_topk call. Returns (scores f64 [B,k], rows i64 [B,k], certified i32 [B])."""
+    dev = catalog.device
+    st = stream_of(dev)
+    B, B_pad = qb.B, qb.B_pad
+    chunk = chunk_rows or _chunk_rows(catalog, B_pad, DEFAULT_SCORE_BUDGET)
+    need = _lib.load().ebt_cosine_topk_workspace(B, B_pad, catalog.n, kprime, chunk)
+    if need == 0:
+        raise EbertError("invalid workspace request")
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=dev)
+    out_s = torch.empty((B, k), dtype=torch.float64, device=dev)
+    out_r = torch.empty((B, k), dtype=torch.int64, device=dev)
+    cert = torch.empty(B, dtype=torch.int32, device=dev)
+    eo, er = (exclude if exclude is not None else (None, None))
+    call("ebt_cosine_topk", ptr(qb.q64), ptr(qb.qimg), ptr(qb.qscale), ptr(qb.eps), B, B_pad,
+         ptr(catalog.data), catalog.dtype_code, catalog.ld, ptr(catalog.gnorm), ptr(catalog.image),
+         ptr(catalog.cscale), catalog.img_dtype, catalog.ld_img, catalog.n, catalog.d,
+         catalog.d_pad, catalog.row_offset, ptr(eo), ptr(er), k, kprime, chunk, ptr(workspace),
+         int(workspace.numel()), ptr(out_s), ptr(out_r), ptr(cert),
+         timer.handle if timer is not None else None, st)
+    return out_s, out_r, cert
+
+
+def score_topk(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
+               liked: Optional[Union[Tuple[torch.Tensor, torch.Tensor], Sequence[Sequence[int]]]] = None,
+               exclude: Optional[Union[Tuple[torch.Tensor, torch.Tensor], Sequence[Sequence[int]]]] = None,
+               kprime: Optional[int] = None, chunk_rows: Optional[int] = None,
+               timer: Optional[_lib.Timer] = None, liked_counts: Optional[torch.Tensor] = None,
+               liked_sum_hook=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Top-k by cosine (mean cosine over liked rows) with exclusions.
+
+    Returns (scores float64 [B, k], rows int64 [B, k]) on the catalog's device, ordered by
+    (score desc, row asc); rows are GLOBAL row ids; missing entries (fewer than k candidates)
+    are NaN / -1. ``exclude`` and ``liked`` take device CSR pairs or host lists of global rows.
+    """
+    if k < 1:
+        raise EbertError("k must be >= 1")
+    dev = catalog.device
+    if liked is not None and not isinstance(liked, tuple):
+        liked = csr_from_lists(liked, dev)
+    if exclude is not None and not isinstance(exclude, tuple):
+        exclude = csr_from_lists(exclude, dev)
+    qb = prepare_queries(catalog, queries=queries, liked=liked, liked_counts=liked_counts,
+                         liked_sum_hook=liked_sum_hook)
+    n_cap = _round_up(catalog.n, 4)
+    k_eff = min(k, catalog.n)
+    if k_eff > KPRIME_MAX:
+        raise EbertError(f"k={k} > {KPRIME_MAX} over a {catalog.n}-row catalog is not supported")
+    kp = kprime or default_kprime(catalog, k_eff)
+    kp = max(_round_up(k_eff, 4), min(_round_up(kp, 4), n_cap, KPRIME_MAX))
+    s, r, cert = run_pipeline(catalog, qb, k_eff, kp, exclude, chunk_rows, timer)
+    # certification retry: only queries whose candidate set is not provably complete
+    while True:
+        bad = torch.nonzero(cert == 0).flatten()
+        if bad.numel() == 0:
+            break
+        if kp >= min(n_cap, KPRIME_MAX):
+            raise EbertError(f"{bad.numel()} queries could not be certified at k'={kp} "
+                             "(a tie cluster wider than k' at the k-th score)")
+        kp = min(kp * 4, n_cap, KPRIME_MAX)
+        sub_ex = csr_subset(exclude[0], exclude[1], bad) if exclude is not None else None
+        s2, r2, c2 = run_pipeline(catalog, qb.subset(bad), k_eff, kp, sub_ex, chunk_rows, timer)
+        s[bad], r[bad], cert[bad] = s2, r2, c2
+    if k_eff < k:
+        pad_s = torch.full((qb.B, k - k_eff), float("nan"), dtype=torch.float64, device=dev)
+        pad_r = torch.full((qb.B, k - k_eff), -1, dtype=torch.int64, device=dev)
+        s, r = torch.cat([s, pad_s], 1), torch.cat([r, pad_r], 1)
+    return s, r
+
+
+def merge_topk(scores: torch.Tensor, rows: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Merge [R, B, k] partial lists (the all-gathered shard results) into the global top-k."""
+    require_cuda(scores, "scores")
+    R, B, kk = scores.shape
+    scores = scores.contiguous()
+    rows = rows.contiguous()
+    out_s = torch.empty((B, k), dtype=torch.float64, device=scores.device)
+    out_r = torch.empty((B, k), dtype=torch.int64, device=scores.device)
+    if kk != k:
+        raise EbertError("partial lists must have k entries")
+    call("ebt_merge_topk", ptr(scores), ptr(rows), R, B, k, ptr(out_s), ptr(out_r),
+         stream_of(scores.device))
+    return out_s, out_r
+
+
+def rescore_rows(catalog: Catalog, qb: QueryBatch, cand_rows: torch.Tensor
+                 ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Exact float64 cosine of each query against its OWN candidate rows ([B, m] global rows),
+    sorted (score desc, row asc). This is lib.py:105-106 (mean cosine of the liked movies vs the
+    query matches) when qb holds the liked-row means."""
+    dev = catalog.device
+    B, m = cand_rows.shape
+    local = (cand_rows - catalog.row_offset).contiguous()
+    vals = torch.zeros((B, m), dtype=torch.float32, device=dev)
+    eps = torch.zeros(max(B, 1), dtype=torch.float32, device=dev)
+    out_s = torch.empty((B, m), dtype=torch.float64, device=dev)
+    out_r = torch.empty((B, m), dtype=torch.int64, device=dev)
+    cert = torch.empty(B, dtype=torch.int32, device=dev)
+    call("ebt_rescore", ptr(qb.q64), B, catalog.d, ptr(catalog.data), catalog.dtype_code,
+         catalog.ld, ptr(catalog.gnorm), catalog.row_offset, ptr(vals), ptr(local), m, m, m, ptr(eps),
+         ptr(out_s), ptr(out_r), ptr(cert), stream_of(dev))
+    return out_s, out_r

@@ -1,0 +1,105 @@
+"""CPU: the C-ABI library loads and exports every declared symbol; host-side logic."""
+import os
+import re
+
+import numpy as np
+import pandas as pd
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    with open(os.path.join(ROOT, "include", "ebert.h")) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"\b(ebt_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_symbols_exported():
+    import ctypes
+    from robot_ebert_amd import _lib
+    lib = _lib.load()
+    syms = _declared_symbols()
+    assert len(syms) >= 19
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(_lib._SIGNATURES), set(syms) ^ set(_lib._SIGNATURES)
+    assert lib.ebt_version() >= 100
+    assert isinstance(lib.ebt_last_error(), bytes)
+
+
+def test_invalid_args_return_einval_without_gpu():
+    """Argument validation happens before any HIP call, so it is testable on the host."""
+    from robot_ebert_amd import _lib
+    lib = _lib.load()
+    assert lib.ebt_select_topk(None, None, 0, 1, 0, 0, 0, 1, None, None, 0, None) == -1
+    assert b"ebt_select_topk" in lib.ebt_last_error()
+    assert lib.ebt_cosine_topk_workspace(10, 5, 100, 8, 128) == 0  # B_pad < B
+    assert lib.ebt_cosine_topk_workspace(10, 128, 1000, 104, 512) > 0
+    assert lib.ebt_merge_topk(None, None, 0, 1, 1, None, None, None) == -1
+
+
+def test_workspace_grows_with_chunks():
+    from robot_ebert_amd import _lib
+    lib = _lib.load()
+    one = lib.ebt_cosine_topk_workspace(4096, 4096, 1_000_000, 200, 1_000_064)
+    many = lib.ebt_cosine_topk_workspace(4096, 4096, 1_000_000, 200, 262_144)
+    assert one > 4096 * 1_000_000 * 4
+    assert many < one
+
+
+def test_no_cpu_fallback_on_cpu_tensors():
+    import torch
+    from robot_ebert_amd import EbertError, Catalog
+    with pytest.raises(EbertError):
+        Catalog(torch.zeros((10, 4)))
+
+
+def test_shard_range_partitions():
+    from robot_ebert_amd.distributed import shard_range
+    for n in (1, 7, 100, 2269, 1_000_000):
+        for w in (1, 2, 3, 8):
+            parts = [shard_range(n, r, w) for r in range(w)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+            sizes = [b - a for a, b in parts]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_split_liked_counts():
+    from robot_ebert_amd.distributed import split_liked
+    local, counts = split_liked([[1, 5, 9], [], [4]], 4, 9)
+    assert local == [[5], [], [4]] and counts == [3, 0, 1]
+
+
+def test_csr_from_lists_and_subset():
+    import torch
+    from robot_ebert_amd.search import csr_from_lists, csr_subset
+    off, rows = csr_from_lists([[1, 2], [], [3, 4, 5]], "cpu")
+    assert off.tolist() == [0, 2, 2, 5] and rows.tolist() == [1, 2, 3, 4, 5]
+    o2, r2 = csr_subset(off, rows, torch.tensor([2, 0]))
+    assert o2.tolist() == [0, 3, 5] and r2.tolist() == [3, 4, 5, 1, 2]
+    o3, r3 = csr_subset(off, rows, torch.tensor([1]))
+    assert o3.tolist() == [0, 0]
+
+
+def test_order_recommendations_mirrors_reference():
+    """lib.py:55 sort_index is lexicographic on string ids; lib.py:63 sort is stable."""
+    from robot_ebert_amd.lib import order_recommendations
+    pairs = [("9", 0.5), ("10", 0.7), ("100", 0.5), ("2", 0.9)]
+    assert order_recommendations(pairs) == [("2", 0.9), ("10", 0.7), ("100", 0.5), ("9", 0.5)]
+
+
+def test_user_query_lists():
+    from robot_ebert_amd.lib import user_query_lists
+
+    class FakeCat:
+        row_offset = 0
+        index_pos = {"a": 0, "b": 1, "c": 2}
+
+        def rows_of(self, ids):
+            return [self.index_pos[t] for t in ids]
+
+    df = pd.DataFrame({"tmdb_id": ["a", "c", "b"], "rating": [3.5, 1.0, 5.0]})
+    liked, rated = user_query_lists(df, FakeCat())
+    assert liked == [0, 1] and sorted(rated) == [0, 1, 2]
