@@ -142,13 +142,23 @@ int ebt_merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t
                    double* out_scores, int64_t* out_rows, void* stream);
 
 /* ---- the whole pipeline -------------------------------------------------------------------
- * Workspace bytes needed by ebt_cosine_topk for these sizes. */
+ * flags: EBT_FLAG_NO_FUSE disables the fused screen (every score row is materialised). */
+#define EBT_FLAG_NO_FUSE 1
+/* Workspace bytes needed by ebt_cosine_topk for these sizes. */
 size_t ebt_cosine_topk_workspace(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
-                                 int64_t chunk_rows);
+                                 int64_t chunk_rows, int flags);
 
 /* Query x catalog cosine top-k over one (shard of a) catalog:
- *   for every catalog chunk of chunk_rows rows: screening GEMM -> mask excluded -> streaming
- *   select of kprime candidates; then a select across chunks; then the exact float64 rescore.
+ *   unfused: for every catalog chunk of chunk_rows rows: screening GEMM -> mask excluded ->
+ *   streaming select of kprime candidates; then a select across chunks; then the exact float64
+ *   rescore.
+ *   fused (default when n_rows >= 2*H, H = max(65536, 256*kprime)): the head rows [0, H) go
+ *   through the unfused path; the k'-th best head score of each query is a lower bound of its
+ *   global k'-th best, and the GEMM over the tail rows [H, n) appends only scores >= that bound
+ *   to a per-query candidate list (epilogue filter: no score matrix in HBM); exclusions are
+ *   removed from the list (excl_rows must be sorted ascending per query), the k' best of head +
+ *   tail are selected and rescored. certified[b] = -1 reports a candidate-list overflow (rerun
+ *   the query with EBT_FLAG_NO_FUSE).
  * Inputs: the query batch prepared by ebt_query_* (q64, qimg, qscale, eps; B real rows, B_pad
  * image rows), the catalog (cat/dtype/ld with gnorm64; its screening image cimg with cscale or
  * NULL, ld_img, d_pad), exclusions as CSR of GLOBAL rows (NULL = none), k <= kprime.
@@ -159,11 +169,13 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
                     const double* gnorm64, const void* cimg, const float* cscale, int img_dtype,
                     int32_t ld_img, int64_t n_rows, int32_t d, int32_t d_pad, int64_t row_offset,
                     const int64_t* excl_off, const int64_t* excl_rows, int32_t k, int32_t kprime,
-                    int64_t chunk_rows, void* workspace, size_t ws_bytes, double* out_scores,
-                    int64_t* out_rows, int32_t* certified, void* timer, void* stream);
+                    int64_t chunk_rows, int flags, void* workspace, size_t ws_bytes,
+                    double* out_scores, int64_t* out_rows, int32_t* certified, void* timer,
+                    void* stream);
 
 /* ---- per-stage GPU timing (hipEvents recorded on the launch stream) -----------------------
- * Stages: 0 screening GEMM, 1 exclusion mask, 2 chunk select, 3 cross-chunk select, 4 rescore.
+ * Stages: 0 screening GEMM (score-writing), 1 exclusion mask, 2 chunk select, 3 candidate
+ * select (across chunks / head + fused tail), 4 rescore, 5 fused screening GEMM (filtering).
  * ebt_timer_query synchronises the recorded events and returns the total milliseconds and the
  * number of launches of `stage` since the last reset. Host pointers. */
 #define EBT_STAGE_GEMM 0
@@ -171,7 +183,8 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
 #define EBT_STAGE_SELECT 2
 #define EBT_STAGE_MERGE_SELECT 3
 #define EBT_STAGE_RESCORE 4
-#define EBT_NUM_STAGES 5
+#define EBT_STAGE_GEMM_FILTER 5
+#define EBT_NUM_STAGES 6
 void* ebt_timer_create(void);
 void ebt_timer_destroy(void* timer);
 int ebt_timer_reset(void* timer);

@@ -19,7 +19,8 @@ LIB_PATH = os.environ.get("EBERT_LIB", os.path.join(_HERE, "libebert.so"))
 EBT_F32, EBT_BF16, EBT_F16, EBT_F64 = 0, 1, 2, 3
 DTYPE_CODE = {torch.float32: EBT_F32, torch.bfloat16: EBT_BF16, torch.float16: EBT_F16,
               torch.float64: EBT_F64}
-STAGES = {"gemm": 0, "mask": 1, "select": 2, "merge_select": 3, "rescore": 4}
+STAGES = {"gemm": 0, "mask": 1, "select": 2, "merge_select": 3, "rescore": 4, "gemm_filter": 5}
+EBT_FLAG_NO_FUSE = 1
 
 
 class EbertError(RuntimeError):
@@ -47,10 +48,10 @@ _SIGNATURES = {
     "ebt_rescore": ([_VP, _I64, _I32, _VP, _INT, _I64, _VP, _I64, _VP, _VP, _I32, _I32, _I64, _VP,
                      _VP, _VP, _VP, _VP], _INT),
     "ebt_merge_topk": ([_VP, _VP, _I32, _I64, _I32, _VP, _VP, _VP], _INT),
-    "ebt_cosine_topk_workspace": ([_I64, _I64, _I64, _I32, _I64], _SZ),
+    "ebt_cosine_topk_workspace": ([_I64, _I64, _I64, _I32, _I64, _INT], _SZ),
     "ebt_cosine_topk": ([_VP, _VP, _VP, _VP, _I64, _I64, _VP, _INT, _I64, _VP, _VP, _VP, _INT,
-                         _I32, _I64, _I32, _I32, _I64, _VP, _VP, _I32, _I32, _I64, _VP, _SZ, _VP,
-                         _VP, _VP, _VP, _VP], _INT),
+                         _I32, _I64, _I32, _I32, _I64, _VP, _VP, _I32, _I32, _I64, _INT, _VP, _SZ,
+                         _VP, _VP, _VP, _VP, _VP], _INT),
     "ebt_timer_create": ([], _VP),
     "ebt_timer_destroy": ([_VP], None),
     "ebt_timer_reset": ([_VP], _INT),

@@ -45,7 +45,15 @@ int mask_excluded(float*, int64_t, int64_t, int64_t, int64_t, const int64_t*, co
                   hipStream_t);
 int rescore(const double*, int64_t, int32_t, const void*, int, int64_t, const double*, int64_t,
             const float*, const int64_t*, int32_t, int32_t, int64_t, const float*, double*, int64_t*,
-            int32_t*, hipStream_t);
+            int32_t*, hipStream_t, const int*, int);
+int screen_gemm_filter(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
+                       const float*, const float*, const float*, int*, float*, int64_t*, int64_t,
+                       int64_t, int, int64_t, hipStream_t);
+int select_topk_counted(const float*, const int64_t*, int64_t, int64_t, int64_t, const int*, int,
+                        int32_t, float*, int64_t*, int64_t, hipStream_t);
+int kth_threshold(const float*, int64_t, int64_t, int64_t, int, float*, hipStream_t);
+int mask_candidates(float*, const int64_t*, int64_t, int64_t, int64_t, const int*, int, int64_t,
+                    const int64_t*, const int64_t*, hipStream_t);
 int merge_topk(const double*, const int64_t*, int32_t, int64_t, int32_t, double*, int64_t*,
                hipStream_t);
 
@@ -96,21 +104,41 @@ struct StageScope {
 };
 
 // --------------------------------------------------------------------- workspace layout ----
+// Unfused:  [S: B_pad x chunk f32][seg tmp][per-chunk candidates][final candidates]
+// Fused:    the same for the HEAD rows [0, H) (chunked), plus the candidate rows
+//           [B][kprime + cap] (head top-k' then appended tail candidates), counters and
+//           thresholds. The tail rows [H, n) never materialise scores.
 struct WsLayout {
-  int64_t chunk, ld_s, n_chunks;
+  int64_t chunk, ld_s, n_chunks, head, cap, ld_cand;
   int segs;
-  size_t off_s, off_segv, off_segi, off_chv, off_chi, off_fv, off_fi, bytes;
+  bool fused;
+  size_t off_s, off_segv, off_segi, off_chv, off_chi, off_fv, off_fi, off_cv, off_ci, off_cnt,
+      off_thr, bytes;
 };
 
 static size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 
 static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
-                          int64_t chunk_rows) {
+                          int64_t chunk_rows, int flags) {
   WsLayout L{};
-  L.chunk = chunk_rows < n_rows ? chunk_rows : n_rows;
+  // fused screen: head H rows processed unfused give each query a threshold; the tail is
+  // filtered inside the GEMM epilogue. Expected tail candidates ~ kprime * (n - H) / H.
+  int64_t H = 256LL * kprime;
+  H = H < 65536 ? 65536 : H;
+  H = (H + 255) / 256 * 256;
+  L.fused = !(flags & EBT_FLAG_NO_FUSE) && n_rows >= 2 * H;
+  L.head = L.fused ? H : n_rows;
+  if (L.fused) {
+    int64_t expect = (int64_t)kprime * (n_rows - H) / H;
+    int64_t cap = 4 * expect + 2048;
+    cap = cap > (1LL << 22) ? (1LL << 22) : cap;
+    L.cap = (cap + 255) / 256 * 256;
+    L.ld_cand = (kprime + L.cap + 3) / 4 * 4;
+  }
+  L.chunk = chunk_rows < L.head ? chunk_rows : L.head;
   if (L.chunk < 1) L.chunk = 1;
   L.ld_s = (L.chunk + 3) & ~(int64_t)3;
-  L.n_chunks = ceil_div(n_rows, L.chunk);
+  L.n_chunks = ceil_div(L.head, L.chunk);
   // enough select workgroups to fill the chip: >= 512 (2 per CU)
   int64_t segs = B > 0 ? ceil_div(512, B) : 1;
   int64_t max_segs = L.chunk / (2 * 4096);
@@ -133,8 +161,74 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
   o = align_up(o + (size_t)B * kprime * 4);
   L.off_fi = o;
   o = align_up(o + (size_t)B * kprime * 8);
+  if (L.fused) {
+    L.off_cv = o;
+    o = align_up(o + (size_t)B * L.ld_cand * 4);
+    L.off_ci = o;
+    o = align_up(o + (size_t)B * L.ld_cand * 8);
+    L.off_cnt = o;
+    o = align_up(o + (size_t)B_pad * 4);
+    L.off_thr = o;
+    o = align_up(o + (size_t)B_pad * 4);
+  }
   L.bytes = o;
   return L;
+}
+
+// Top-k' of rows [r0, r0+nrows) of the (shard-local) catalog into dv/di (row stride ld_d), the
+// unfused way: chunked GEMM -> mask -> streaming select (-> select across chunks).
+static int head_topk(const WsLayout& L, char* ws, const void* qimg, const float* qscale,
+                     int64_t B, int64_t B_pad, const void* cimg, const float* cscale,
+                     int img_dtype, int32_t ld_img, int64_t r0, int64_t nrows, int32_t d_pad,
+                     int64_t row_offset, const int64_t* excl_off, const int64_t* excl_rows,
+                     int32_t kprime, float* dv_final, int64_t* di_final, int64_t ld_final,
+                     void* timer, hipStream_t st) {
+  float* S = (float*)(ws + L.off_s);
+  float* segv = (float*)(ws + L.off_segv);
+  int64_t* segi = (int64_t*)(ws + L.off_segi);
+  float* chv = (float*)(ws + L.off_chv);
+  int64_t* chi = (int64_t*)(ws + L.off_chi);
+  const int64_t n_chunks = ceil_div(nrows, L.chunk);
+  int rc;
+  for (int64_t c = 0; c < n_chunks; ++c) {
+    const int64_t c0 = r0 + c * L.chunk;
+    const int64_t nc = (r0 + nrows - c0) < L.chunk ? (r0 + nrows - c0) : L.chunk;
+    {
+      StageScope s(timer, EBT_STAGE_GEMM, st);
+      rc = screen_gemm(qimg, B_pad, (const char*)cimg + c0 * ld_img * 2, nc, d_pad, ld_img,
+                       img_dtype, qscale, cscale ? cscale + c0 : nullptr, S, L.ld_s, st);
+    }
+    if (rc) return rc;
+    if (excl_off) {
+      StageScope s(timer, EBT_STAGE_MASK, st);
+      rc = mask_excluded(S, L.ld_s, B, row_offset + c0, row_offset + c0 + nc, excl_off,
+                         excl_rows, st);
+      if (rc) return rc;
+    }
+    float* dv = n_chunks == 1 ? dv_final : chv + c * kprime;
+    int64_t* di = n_chunks == 1 ? di_final : chi + c * kprime;
+    const int64_t ld_d = n_chunks == 1 ? ld_final : n_chunks * kprime;
+    {
+      StageScope s(timer, EBT_STAGE_SELECT, st);
+      if (L.segs == 1) {
+        rc = select_topk(S, nullptr, L.ld_s, B, nc, c0, kprime, 1, dv, di, ld_d, st);
+      } else {
+        rc = select_topk(S, nullptr, L.ld_s, B, nc, c0, kprime, L.segs, segv, segi,
+                         (int64_t)L.segs * kprime, st);
+        if (!rc)
+          rc = select_topk(segv, segi, (int64_t)L.segs * kprime, B, (int64_t)L.segs * kprime, 0,
+                           kprime, 1, dv, di, ld_d, st);
+      }
+    }
+    if (rc) return rc;
+  }
+  if (n_chunks > 1) {
+    StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
+    rc = select_topk(chv, chi, n_chunks * kprime, B, n_chunks * kprime, 0, kprime, 1, dv_final,
+                     di_final, ld_final, st);
+    if (rc) return rc;
+  }
+  return EBT_OK;
 }
 
 }  // namespace ebt
@@ -208,7 +302,7 @@ int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dt
                 const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
                 double* out_scores, int64_t* out_rows, int32_t* certified, void* stream) {
   return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, cand_vals, cand_rows, kprime, k, n_rows,
-                 eps, out_scores, out_rows, certified, (hipStream_t)stream);
+                 eps, out_scores, out_rows, certified, (hipStream_t)stream, nullptr, 0);
 }
 
 int ebt_merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, int32_t k,
@@ -217,9 +311,9 @@ int ebt_merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t
 }
 
 size_t ebt_cosine_topk_workspace(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
-                                 int64_t chunk_rows) {
+                                 int64_t chunk_rows, int flags) {
   if (B < 0 || B_pad < B || n_rows < 1 || kprime < 1 || chunk_rows < 1) return 0;
-  return ws_layout(B, B_pad, n_rows, kprime, chunk_rows).bytes;
+  return ws_layout(B, B_pad, n_rows, kprime, chunk_rows, flags).bytes;
 }
 
 int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, const float* eps,
@@ -227,8 +321,9 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
                     const double* gnorm64, const void* cimg, const float* cscale, int img_dtype,
                     int32_t ld_img, int64_t n_rows, int32_t d, int32_t d_pad, int64_t row_offset,
                     const int64_t* excl_off, const int64_t* excl_rows, int32_t k, int32_t kprime,
-                    int64_t chunk_rows, void* workspace, size_t ws_bytes, double* out_scores,
-                    int64_t* out_rows, int32_t* certified, void* timer, void* stream) {
+                    int64_t chunk_rows, int flags, void* workspace, size_t ws_bytes,
+                    double* out_scores, int64_t* out_rows, int32_t* certified, void* timer,
+                    void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (!q64 || !qimg || !qscale || !eps || !cat || !gnorm64 || !cimg || !workspace ||
       !out_scores || !out_rows || !certified) {
@@ -237,71 +332,68 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
   }
   if (B < 1 || B_pad < B || B_pad % 128 != 0 || n_rows < 1 || d < 1 || d_pad < d ||
       d_pad % 64 != 0 || ld_img < d_pad || k < 1 || kprime < k || kprime > 4096 ||
-      kprime % 4 != 0 || chunk_rows < 128 || chunk_rows % 128 != 0 || ((excl_off == nullptr) != (excl_rows == nullptr))) {
+      kprime % 4 != 0 || chunk_rows < 128 || chunk_rows % 128 != 0 ||
+      ((excl_off == nullptr) != (excl_rows == nullptr))) {
     set_error("ebt_cosine_topk: bad arguments (B=%lld B_pad=%lld n=%lld d=%d d_pad=%d k=%d "
               "kprime=%d chunk=%lld)", (long long)B, (long long)B_pad, (long long)n_rows, d,
               d_pad, k, kprime, (long long)chunk_rows);
     return EBT_EINVAL;
   }
-  const WsLayout L = ws_layout(B, B_pad, n_rows, kprime, chunk_rows);
+  const WsLayout L = ws_layout(B, B_pad, n_rows, kprime, chunk_rows, flags);
   if (ws_bytes < L.bytes) {
     set_error("ebt_cosine_topk: workspace %zu < %zu bytes", ws_bytes, L.bytes);
     return EBT_ENOMEM;
   }
   char* ws = (char*)workspace;
-  float* S = (float*)(ws + L.off_s);
-  float* segv = (float*)(ws + L.off_segv);
-  int64_t* segi = (int64_t*)(ws + L.off_segi);
-  float* chv = (float*)(ws + L.off_chv);
-  int64_t* chi = (int64_t*)(ws + L.off_chi);
   float* fv = (float*)(ws + L.off_fv);
   int64_t* fi = (int64_t*)(ws + L.off_fi);
-  const int es_img = 2;
   int rc;
-  for (int64_t c = 0; c < L.n_chunks; ++c) {
-    const int64_t c0 = c * L.chunk;
-    const int64_t nc = (n_rows - c0) < L.chunk ? (n_rows - c0) : L.chunk;
-    {
-      StageScope s(timer, EBT_STAGE_GEMM, st);
-      rc = screen_gemm(qimg, B_pad, (const char*)cimg + c0 * ld_img * es_img, nc, d_pad, ld_img,
-                       img_dtype, qscale, cscale ? cscale + c0 : nullptr, S, L.ld_s, st);
-    }
+  if (!L.fused) {
+    rc = head_topk(L, ws, qimg, qscale, B, B_pad, cimg, cscale, img_dtype, ld_img, 0, n_rows,
+                   d_pad, row_offset, excl_off, excl_rows, kprime, fv, fi, kprime, timer, st);
     if (rc) return rc;
-    if (excl_off) {
-      StageScope s(timer, EBT_STAGE_MASK, st);
-      rc = mask_excluded(S, L.ld_s, B, row_offset + c0, row_offset + c0 + nc, excl_off,
-                         excl_rows, st);
-      if (rc) return rc;
-    }
-    float* dv = L.n_chunks == 1 ? fv : chv + c * kprime;
-    int64_t* di = L.n_chunks == 1 ? fi : chi + c * kprime;
-    const int64_t ld_d = L.n_chunks == 1 ? kprime : L.n_chunks * kprime;
-    {
-      StageScope s(timer, EBT_STAGE_SELECT, st);
-      if (L.segs == 1) {
-        rc = select_topk(S, nullptr, L.ld_s, B, nc, c0, kprime, 1, dv, di, ld_d, st);
-      } else {
-        rc = select_topk(S, nullptr, L.ld_s, B, nc, c0, kprime, L.segs, segv, segi,
-                         (int64_t)L.segs * kprime, st);
-        if (!rc)
-          rc = select_topk(segv, segi, (int64_t)L.segs * kprime, B, (int64_t)L.segs * kprime, 0,
-                           kprime, 1, dv, di, ld_d, st);
-      }
-    }
-    if (rc) return rc;
+    StageScope s(timer, EBT_STAGE_RESCORE, st);
+    return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, fv, fi, kprime, k, n_rows, eps,
+                   out_scores, out_rows, certified, st, nullptr, 0);
   }
-  if (L.n_chunks > 1) {
-    StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
-    rc = select_topk(chv, chi, L.n_chunks * kprime, B, L.n_chunks * kprime, 0, kprime, 1, fv, fi,
-                     kprime, st);
+  float* cv = (float*)(ws + L.off_cv);
+  int64_t* ci = (int64_t*)(ws + L.off_ci);
+  int* cnt = (int*)(ws + L.off_cnt);
+  float* thr = (float*)(ws + L.off_thr);
+  // 1. head rows [0, H): exact top-k' per query into the first k' slots of the candidate rows
+  rc = head_topk(L, ws, qimg, qscale, B, B_pad, cimg, cscale, img_dtype, ld_img, 0, L.head, d_pad,
+                 row_offset, excl_off, excl_rows, kprime, cv, ci, L.ld_cand, timer, st);
+  if (rc) return rc;
+  // 2. per-query threshold = the head's k'-th best approx score
+  rc = kth_threshold(cv, L.ld_cand, B, B_pad, kprime, thr, st);
+  if (rc) return rc;
+  rc = hip_check(hipMemsetAsync(cnt, 0, (size_t)B_pad * 4, st), "hipMemsetAsync");
+  if (rc) return rc;
+  // 3. tail rows [H, n): GEMM with the threshold filter in the epilogue
+  {
+    StageScope s(timer, EBT_STAGE_GEMM_FILTER, st);
+    rc = screen_gemm_filter(qimg, B_pad, (const char*)cimg + L.head * ld_img * 2,
+                            n_rows - L.head, d_pad, ld_img, img_dtype, qscale,
+                            cscale ? cscale + L.head : nullptr, thr, cnt, cv, ci, L.ld_cand,
+                            kprime, (int)L.cap, L.head, st);
+  }
+  if (rc) return rc;
+  // 4. exclusions among the appended candidates, then the k' best of head + tail
+  if (excl_off) {
+    StageScope s(timer, EBT_STAGE_MASK, st);
+    rc = mask_candidates(cv, ci, L.ld_cand, kprime, B, cnt, (int)L.cap, row_offset, excl_off,
+                         excl_rows, st);
     if (rc) return rc;
   }
   {
-    StageScope s(timer, EBT_STAGE_RESCORE, st);
-    rc = rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, fv, fi, kprime, k, n_rows, eps,
-                 out_scores, out_rows, certified, st);
+    StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
+    rc = select_topk_counted(cv, ci, L.ld_cand, B, kprime, cnt, (int)L.cap, kprime, fv, fi,
+                             kprime, st);
   }
-  return rc;
+  if (rc) return rc;
+  StageScope s(timer, EBT_STAGE_RESCORE, st);
+  return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, fv, fi, kprime, k, n_rows, eps,
+                 out_scores, out_rows, certified, st, cnt, (int)L.cap);
 }
 
 void* ebt_timer_create(void) { return new (std::nothrow) Timer(); }

@@ -55,7 +55,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     const double* __restrict__ gnorm, int64_t row_offset, const float* __restrict__ cand_vals,
     const int64_t* __restrict__ cand_rows, int kprime, int kpp, int k, int64_t n_rows,
     const float* __restrict__ eps, double* __restrict__ out_s, int64_t* __restrict__ out_r,
-    int32_t* __restrict__ certified) {
+    int32_t* __restrict__ certified, const int* __restrict__ ovf_cnt, int ovf_cap) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* qs = (double*)smem;                 // d
   double* sc = qs + ((d + 1) & ~1);           // kpp
@@ -135,6 +135,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
       const double amin = (double)cv[kprime - 1];
       ok = amin < T - 2.0 * (double)eps[b];
     }
+    if (ovf_cnt && ovf_cnt[b] > ovf_cap) ok = -1;  // fused screen dropped candidates
     certified[b] = ok;
   }
 }
@@ -147,7 +148,8 @@ size_t rescore_lds_bytes(int d, int kprime) {
 int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype, int64_t ld,
             const double* gnorm, int64_t row_offset, const float* cand_vals,
             const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
-            double* out_s, int64_t* out_r, int32_t* certified, hipStream_t st) {
+            double* out_s, int64_t* out_r, int32_t* certified, hipStream_t st,
+            const int* ovf_cnt, int ovf_cap) {
   if (!q64 || !cat || !gnorm || !cand_vals || !cand_rows || !eps || !out_s || !out_r ||
       !certified || B < 0 || d <= 0 || ld < d || k < 1 || kprime < k || kprime > 4096 ||
       dtype < 0 || dtype > 3) {
@@ -173,11 +175,11 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
   if (vec)                                                                                      \
     hipLaunchKernelGGL((rescore_kernel<DT, true>), grid, block, lds, st, q64, d, cat, ld,       \
                        gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps, out_s, \
-                       out_r, certified);                                                       \
+                       out_r, certified, ovf_cnt, ovf_cap);                                     \
   else                                                                                          \
     hipLaunchKernelGGL((rescore_kernel<DT, false>), grid, block, lds, st, q64, d, cat, ld,      \
                        gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps, out_s, \
-                       out_r, certified);
+                       out_r, certified, ovf_cnt, ovf_cap);
   switch (dtype) {
     case EBT_F32: EBT_RS(EBT_F32) break;
     case EBT_BF16: EBT_RS(EBT_BF16) break;

@@ -18,6 +18,8 @@
 // Block order: XCD-bijective remap (blocks sharing an XCD get a contiguous logical range), then
 // groups of 8 catalog tiles walked query-tile-major, so a catalog tile is fetched from HBM once
 // per XCD and re-read from L2 by the 32 query tiles that use it.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace ebt {
@@ -64,12 +66,72 @@ __device__ __forceinline__ f32x4_t mfma16(const u16x8_t& a, const u16x8_t& b, f3
   }
 }
 
-template <bool BF16>
+// Epilogue destinations. Store mode: the float32 score matrix S[q][i]. Filter mode (the fused
+// screen): only scores >= thr[q] leave the kernel, appended to the query's candidate list
+// (cand_v / cand_i [q*ld_cand + cand_off + slot], slot from an atomic counter cnt[q]; slots past
+// `cap` are dropped and counted, so cnt[q] > cap flags an overflow). thr[q] is a lower bound of
+// the query's k'-th best approx score, so no candidate of the true top-k' is ever filtered.
+struct EpiArgs {
+  float* S;
+  int64_t ld_s;
+  const float* thr;
+  int* cnt;
+  float* cand_v;
+  int64_t* cand_i;
+  int64_t ld_cand;
+  int64_t cand_off;
+  int cap;
+  int64_t idx_base;
+};
+
+template <bool FILTER>
+__device__ __forceinline__ void epilogue4(const EpiArgs& e, int64_t q, int64_t i0,
+                                          int64_t n_rows, const f32x4_t& acc, float qs,
+                                          float th, const float* __restrict__ cscale) {
+  if constexpr (!FILTER) {
+    float* srow = e.S + q * e.ld_s;
+    if (i0 + 3 < n_rows) {
+      float4 cs = cscale ? *(const float4*)(cscale + i0) : make_float4(1.f, 1.f, 1.f, 1.f);
+      float4 v;
+      v.x = acc[0] * qs * cs.x;
+      v.y = acc[1] * qs * cs.y;
+      v.z = acc[2] * qs * cs.z;
+      v.w = acc[3] * qs * cs.w;
+      *(float4*)(srow + i0) = v;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (i0 + r < n_rows) {
+          const float cs = cscale ? cscale[i0 + r] : 1.f;
+          srow[i0 + r] = acc[r] * qs * cs;
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t i = i0 + r;
+      if (i < n_rows) {
+        const float cs = cscale ? cscale[i] : 1.f;
+        const float v = acc[r] * qs * cs;
+        if (v >= th) {
+          const int p = atomicAdd(e.cnt + q, 1);
+          if (p < e.cap) {
+            const int64_t o = q * e.ld_cand + e.cand_off + p;
+            e.cand_v[o] = v;
+            e.cand_i[o] = e.idx_base + i;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <bool BF16, bool FILTER>
 __global__ __launch_bounds__(GTHREADS, 2) void screen_gemm_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ C, int64_t ld_img,
     int64_t n_rows, int n_qtiles, int64_t n_ctiles, int ksteps,
-    const float* __restrict__ qscale, const float* __restrict__ cscale,
-    float* __restrict__ S, int64_t ld_s) {
+    const float* __restrict__ qscale, const float* __restrict__ cscale, EpiArgs e) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -146,66 +208,715 @@ __global__ __launch_bounds__(GTHREADS, 2) void screen_gemm_kernel(
   for (int b = 0; b < 4; ++b) {
     const int64_t q = q0 + wj * 64 + b * 16 + (lane & 15);
     const float qs = qscale[q];
-    float* srow = S + q * ld_s;
+    const float th = FILTER ? e.thr[q] : 0.f;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int64_t i0 = c0 + wi * 64 + a * 16 + 4 * (lane >> 4);
-      if (i0 + 3 < n_rows) {
-        float4 cs = cscale ? *(const float4*)(cscale + i0) : make_float4(1.f, 1.f, 1.f, 1.f);
-        float4 v;
-        v.x = acc[a][b][0] * qs * cs.x;
-        v.y = acc[a][b][1] * qs * cs.y;
-        v.z = acc[a][b][2] * qs * cs.z;
-        v.w = acc[a][b][3] * qs * cs.w;
-        *(float4*)(srow + i0) = v;
-      } else {
+      epilogue4<FILTER>(e, q, i0, n_rows, acc[a][b], qs, th, cscale);
+    }
+  }
+}
+
+// =============================================================================================
+// 256 x 256 tile, 8 waves, 4-slot LDS ring of 32-deep k slices (the large-batch kernel).
+//
+// Wave (wm, wn) in a 2 x 4 grid owns catalog rows wm*128..+127 and queries wn*64..+63 of the
+// tile: 8 x 4 tiles of v_mfma_f32_16x16x32 (128 accumulator VGPRs). A k slice is 256 rows x 32 k
+// of each operand (16 KiB + 16 KiB); slot t&3 of the ring holds slice t. Per slice a wave issues
+// 4 global_load_lds_dwordx4 (2 per operand, 16 rows x 64 B each) for slice t+3, reads 12
+// fragments (ds_read_b128) of slice t and runs 32 MFMAs. One s_barrier per slice; the counted
+// `s_waitcnt vmcnt(8)` before it leaves slices t+1 and t+2 in flight, so ~64 KiB per CU is
+// always being fetched while the MFMAs run.
+// LDS image of a slice operand: row-major 64-byte rows with the 16-byte chunk c stored at slot
+// c ^ (((row >> 3) & 1) << 1); for the 16x16x32 operand map (lane l reads row l&15, chunk l>>4)
+// this puts the 16 lanes of every ds_read_b128 lane group on 16 distinct bank slots.
+// =============================================================================================
+constexpr int HBM_ = 256;             // catalog rows per block
+constexpr int HBN_ = 256;             // queries per block
+constexpr int HBK_ = 32;              // k per slice
+constexpr int HTHREADS = 512;
+constexpr int HOP_BYTES = 256 * 64;   // one operand slice: 16 KiB
+constexpr int HSLOT_BYTES = 2 * HOP_BYTES;
+constexpr int HLDS_BYTES = 4 * HSLOT_BYTES;  // 128 KiB
+constexpr int HGROUP_C = 2;
+
+__device__ __forceinline__ void stage_slice(const uint16_t* __restrict__ X, int64_t ldx,
+                                            int64_t row0, int64_t last_row, int k0,
+                                            char* op_lds, int wave, int lane) {
+  const int sub = lane >> 2;   // row inside the 16-row piece
+  const int slot = lane & 3;   // 16-byte slot inside the 64-byte LDS row
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (i0 + r < n_rows) {
-            const float cs = cscale ? cscale[i0 + r] : 1.f;
-            srow[i0 + r] = acc[a][b][r] * qs * cs;
-          }
-        }
+  for (int j = 0; j < 2; ++j) {
+    const int piece = wave * 2 + j;  // 16 pieces of 16 rows = 256 rows
+    const int rr = piece * 16 + sub;
+    int64_t grow = row0 + rr;
+    grow = grow > last_row ? last_row : grow;
+    const int chunk = slot ^ (((rr >> 3) & 1) << 1);
+    const uint16_t* src = X + grow * ldx + k0 + chunk * 8;
+    __builtin_amdgcn_global_load_lds((gbl_cvoid*)src, (lds_void*)(op_lds + piece * 1024), 16, 0,
+                                     0);
+  }
+}
+
+template <bool BF16, bool FILTER>
+__global__ __launch_bounds__(HTHREADS, 2) void screen_gemm256_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ C, int64_t ld_img,
+    int64_t n_rows, int n_qtiles, int64_t n_ctiles, int nslices,
+    const float* __restrict__ qscale, const float* __restrict__ cscale, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int64_t nwg = (int64_t)n_qtiles * n_ctiles;
+  const int64_t bid = blockIdx.x;
+  const int64_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int64_t L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int64_t per_group = (int64_t)HGROUP_C * n_qtiles;
+  const int64_t g = L / per_group, w = L - g * per_group;
+  const int64_t gc_rem = n_ctiles - g * HGROUP_C;
+  const int64_t gc = gc_rem < HGROUP_C ? gc_rem : HGROUP_C;
+  const int64_t ct = g * HGROUP_C + w % gc;
+  const int64_t qt = w / gc;
+  const int64_t c0 = ct * HBM_;
+  const int64_t q0 = qt * HBN_;
+
+  const int wm = wave >> 2;  // catalog half (128 rows)
+  const int wn = wave & 3;   // query quarter (64 queries)
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // fragment byte offsets inside an operand slice (row tile base is a multiple of 16)
+  const int fr = lane & 15, fc = lane >> 4;
+  const int frag_off = fr * 64 + ((fc ^ (((fr >> 3) & 1) << 1)) << 4);
+  const int a_base = wm * 128 * 64 + frag_off;
+  const int b_base = HOP_BYTES + wn * 64 * 64 + frag_off;
+
+  const int64_t last_c = n_rows - 1;
+  const int64_t last_q = (int64_t)n_qtiles * HBN_ - 1;
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    if (t < nslices) {
+      char* sl = smem + t * HSLOT_BYTES;
+      stage_slice(C, ld_img, c0, last_c, t * HBK_, sl, wave, lane);
+      stage_slice(Q, ld_img, q0, last_q, t * HBK_, sl + HOP_BYTES, wave, lane);
+    }
+  }
+
+  for (int t = 0; t < nslices; ++t) {
+    // slice t landed for this wave: leave the later slices' loads in flight
+    const int ahead = nslices - 1 - t;
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 3 < nslices) {
+      char* sl = smem + ((t + 3) & 3) * HSLOT_BYTES;
+      stage_slice(C, ld_img, c0, last_c, (t + 3) * HBK_, sl, wave, lane);
+      stage_slice(Q, ld_img, q0, last_q, (t + 3) * HBK_, sl + HOP_BYTES, wave, lane);
+    }
+    const char* sl = smem + (t & 3) * HSLOT_BYTES;
+    u16x8_t bf[4], af[8];
+    // all B fragments and the first half of A up front; the second half of A is read while
+    // the first 16 MFMAs run (hipcc would otherwise serialise read -> wait -> 4 MFMAs).
+#pragma unroll
+    for (int b = 0; b < 4; ++b) bf[b] = *(const u16x8_t*)(sl + b_base + b * 16 * 64);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) af[a] = *(const u16x8_t*)(sl + a_base + a * 16 * 64);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int a = 4; a < 8; ++a) af[a] = *(const u16x8_t*)(sl + a_base + a * 16 * 64);
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = mfma16<BF16>(af[a], bf[b], acc[a][b]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+  }
+
+  // ---- epilogue ----
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int64_t q = q0 + wn * 64 + b * 16 + (lane & 15);
+    const float qs = qscale[q];
+    const float th = FILTER ? e.thr[q] : 0.f;
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      const int64_t i0 = c0 + wm * 128 + a * 16 + 4 * (lane >> 4);
+      epilogue4<FILTER>(e, q, i0, n_rows, acc[a][b], qs, th, cscale);
+    }
+  }
+}
+
+// =============================================================================================
+// 256 x 256 tile, 8 waves, BK = 64, "quadrant phases" (the default large-batch kernel).
+//
+// The LDS holds two K-tiles (buffer = tile & 1), each as four 16 KiB half-tiles: A0/A1 = catalog
+// rows 0-127 / 128-255, B0/B1 = queries 0-127 / 128-255 (128 rows x 128 B, chunk c of row r at
+// slot c ^ (r & 7): conflict-free ds_read_b128 for the 16x16x32 operand map). A K-tile is
+// computed in four phases, one output QUADRANT each -- Q1 (A0,B0), Q2 (A0,B1), Q3 (A1,B1),
+// Q4 (A1,B0) -- with all 8 waves on the same quadrant (2 x 4 waves of 64 x 32 outputs: 16
+// MFMAs per wave per phase). So every half-tile dies early (A0 after Q2, B1 after Q3, A1 and B0
+// after Q4) and its region is restaged for tile t+2 one phase later: each phase issues exactly
+// one half-tile (2 global_load_lds_dwordx4 per lane), keeping 3-4 half-tiles in flight; the
+// counted `s_waitcnt vmcnt` in Q2 and Q4 retires only the half the NEXT phase reads. Phase:
+// ds_read this phase's fragments -> issue one half-tile -> [vmcnt] -> s_barrier -> 16 MFMAs at
+// s_setprio 1 -> s_barrier. Accumulators: 4 quadrants x 4 x 2 tiles (128 VGPRs).
+// =============================================================================================
+constexpr int QP_THREADS = 512;
+constexpr int QP_HALF = 128 * 128;            // 16 KiB: 128 rows x 64 k x 2 B
+constexpr int QP_BUF = 4 * QP_HALF;           // one K-tile
+constexpr int QP_LDS = 2 * QP_BUF;            // 128 KiB
+constexpr int QP_GROUP_C = 4;
+// half-tile order of the issue sequence: idx = 4*tile + type
+enum { H_A0 = 0, H_B1 = 1, H_B0 = 2, H_A1 = 3 };
+__device__ __forceinline__ constexpr int half_off(int type) {
+  return type == H_A0 ? 0 : type == H_A1 ? QP_HALF : type == H_B0 ? 2 * QP_HALF : 3 * QP_HALF;
+}
+
+// One wave stages 2 x 1 KiB pieces (16 rows x 128 B) of a 128-row half-tile.
+__device__ __forceinline__ void qp_stage(const uint16_t* __restrict__ X, int64_t ldx, int64_t row0,
+                                         int64_t last_row, int k0, char* half_lds, int wave,
+                                         int lane) {
+  const int slot = lane & 7;
+  const int sub = lane >> 3;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int piece = wave * 2 + j;
+    const int rr = piece * 8 + sub;
+    int64_t grow = row0 + rr;
+    grow = grow > last_row ? last_row : grow;
+    const int chunk = slot ^ sub;
+    const uint16_t* src = X + grow * ldx + k0 + chunk * 8;
+    __builtin_amdgcn_global_load_lds((gbl_cvoid*)src, (lds_void*)(half_lds + piece * 1024), 16, 0,
+                                     0);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+// s_waitcnt with an immediate chosen at run time (near the last tiles fewer loads follow).
+__device__ __forceinline__ void wait_vm_halves(int halves_after) {
+  if (halves_after >= 4) wait_vm<8>();
+  else if (halves_after == 3) wait_vm<6>();
+  else if (halves_after == 2) wait_vm<4>();
+  else if (halves_after == 1) wait_vm<2>();
+  else wait_vm<0>();
+}
+
+__device__ __forceinline__ void qp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool BF16, bool FILTER>
+__global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ C, int64_t ld_img,
+    int64_t n_rows, int n_qtiles, int64_t n_ctiles, int ktiles,
+    const float* __restrict__ qscale, const float* __restrict__ cscale, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int64_t nwg = (int64_t)n_qtiles * n_ctiles;
+  const int64_t bid = blockIdx.x;
+  const int64_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int64_t L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int64_t per_group = (int64_t)QP_GROUP_C * n_qtiles;
+  const int64_t g = L / per_group, w = L - g * per_group;
+  const int64_t gc_rem = n_ctiles - g * QP_GROUP_C;
+  const int64_t gc = gc_rem < QP_GROUP_C ? gc_rem : QP_GROUP_C;
+  const int64_t ct = g * QP_GROUP_C + w % gc;
+  const int64_t qt = w / gc;
+  const int64_t c0 = ct * 256;
+  const int64_t q0 = qt * 256;
+  const int64_t last_c = n_rows - 1;
+  const int64_t last_q = (int64_t)n_qtiles * 256 - 1;
+
+  const int wa = wave >> 2;  // 64-row slab of the quadrant's catalog half
+  const int wb = wave & 3;   // 32-query slab of the quadrant's query half
+  const int fr = lane & 15;
+  // fragment byte offsets inside a half-tile for k-step ks (0, 1): row r, chunk ks*4 + lane>>4
+  int a_off[4][2], b_off[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int c = ks * 4 + (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = wa * 64 + i * 16 + fr;
+      a_off[i][ks] = r * 128 + ((c ^ (r & 7)) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = wb * 32 + j * 16 + fr;
+      b_off[j][ks] = r * 128 + ((c ^ (r & 7)) << 4);
+    }
+  }
+
+  f32x4_t acc[4][4][2];  // [quadrant][i][j]
+#pragma unroll
+  for (int qd = 0; qd < 4; ++qd)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[qd][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int total = 4 * ktiles;
+  auto issue = [&](int idx) {
+    if (idx < total) {
+      const int tile = idx >> 2, type = idx & 3;
+      char* dst = smem + (tile & 1) * QP_BUF + half_off(type);
+      const int k0 = tile * 64;
+      if (type == H_A0) qp_stage(C, ld_img, c0, last_c, k0, dst, wave, lane);
+      else if (type == H_A1) qp_stage(C, ld_img, c0 + 128, last_c, k0, dst, wave, lane);
+      else if (type == H_B0) qp_stage(Q, ld_img, q0, last_q, k0, dst, wave, lane);
+      else qp_stage(Q, ld_img, q0 + 128, last_q, k0, dst, wave, lane);
+    }
+  };
+  auto halves_after = [&](int needed, int last_issued) {
+    const int last = last_issued < total - 1 ? last_issued : total - 1;
+    const int n = last - needed;
+    return n > 0 ? n : 0;
+  };
+
+  // prologue: tile 0 (idx 0..3) and A0/B1 of tile 1 (idx 4, 5); retire what Q1/Q2 of tile 0 read
+#pragma unroll
+  for (int idx = 0; idx < 6; ++idx) issue(idx);
+  wait_vm_halves(halves_after(2, 5));
+  qp_barrier();
+
+  u16x8_t af[4][2], bfr[2][2];
+  for (int t = 0; t < ktiles; ++t) {
+    const char* buf = smem + (t & 1) * QP_BUF;
+    // ---- Q1: (A0, B0); reads A0 + B0, issues B0(t+1) ----
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j][ks] = *(const u16x8_t*)(buf + 2 * QP_HALF + b_off[j][ks]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i][ks] = *(const u16x8_t*)(buf + a_off[i][ks]);
+    }
+    issue(4 * t + 6);
+    qp_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[0][i][j] = mfma16<BF16>(af[i][ks], bfr[j][ks], acc[0][i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    qp_barrier();
+    // ---- Q2: (A0, B1); reads B1, issues A1(t+1), retires A1(t) for Q3 ----
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j][ks] = *(const u16x8_t*)(buf + 3 * QP_HALF + b_off[j][ks]);
+    issue(4 * t + 7);
+    wait_vm_halves(halves_after(4 * t + 3, 4 * t + 7));
+    qp_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[1][i][j] = mfma16<BF16>(af[i][ks], bfr[j][ks], acc[1][i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    qp_barrier();
+    // ---- Q3: (A1, B1); reads A1, issues A0(t+2) into A0(t)'s dead region ----
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i][ks] = *(const u16x8_t*)(buf + QP_HALF + a_off[i][ks]);
+    issue(4 * t + 8);
+    qp_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[2][i][j] = mfma16<BF16>(af[i][ks], bfr[j][ks], acc[2][i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    qp_barrier();
+    // ---- Q4: (A1, B0); reads B0, issues B1(t+2), retires B0(t+1) for Q1 of the next tile ----
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j][ks] = *(const u16x8_t*)(buf + 2 * QP_HALF + b_off[j][ks]);
+    issue(4 * t + 9);
+    wait_vm_halves(halves_after(4 * t + 6, 4 * t + 9));
+    qp_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[3][i][j] = mfma16<BF16>(af[i][ks], bfr[j][ks], acc[3][i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    qp_barrier();
+  }
+
+  // ---- epilogue: quadrant (ah, bh): catalog half ah, query half bh ----
+#pragma unroll
+  for (int qd = 0; qd < 4; ++qd) {
+    const int ah = (qd == 0 || qd == 1) ? 0 : 1;
+    const int bh = (qd == 0 || qd == 3) ? 0 : 1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t q = q0 + bh * 128 + wb * 32 + j * 16 + fr;
+      const float qs = qscale[q];
+      const float th = FILTER ? e.thr[q] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t i0 = c0 + ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
+        epilogue4<FILTER>(e, q, i0, n_rows, acc[qd][i][j], qs, th, cscale);
       }
     }
   }
 }
 
-int screen_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows, int32_t d_pad,
-                int32_t ld_img, int img_dtype, const float* qscale, const float* cscale,
-                float* scores, int64_t ld_scores, hipStream_t stream) {
-  if (!qimg || !cimg || !qscale || !scores) {
-    set_error("ebt_screen_scores: null pointer");
+// =============================================================================================
+// Pipelined quadrant phases (qp2): the same 256 x 256 x 64 tiling, LDS image and quadrant order
+// as qp, but ONE barrier per phase and the fragments of the NEXT phase are read while the
+// current phase's 16 MFMAs run (interleaved by sched_group_barrier), so LDS reads and barriers
+// no longer sit between MFMA clusters. Register sets: A0 / A1 fragments (32 VGPRs each) and two
+// B sets whose roles swap every K-tile (B0(t) is read in Q4(t-1) and kept until Q4(t), B1(t) is
+// read in Q1(t)), 224 VGPRs with the accumulators.
+// Half-tile schedule (phase P = 4t + quadrant issues sequence index P + 7, index = 4u + type
+// with type A0, B0, B1, A1): a region is restaged >= 2 phases after its last ds_read issue and
+// `s_waitcnt vmcnt(8)` before the barrier of every phase that reads retires exactly the half
+// that phase reads (A0/B0 of t+1 in Q4(t), B1(t) in Q1(t), A1(t) in Q2(t)).
+// =============================================================================================
+enum { P_A0 = 0, P_B0 = 1, P_B1 = 2, P_A1 = 3 };
+__device__ __forceinline__ constexpr int p_half_off(int type) {
+  return type == P_A0 ? 0 : type == P_A1 ? QP_HALF : type == P_B0 ? 2 * QP_HALF : 3 * QP_HALF;
+}
+
+template <bool BF16>
+__device__ __forceinline__ void qp2_mma(f32x4_t (&acc)[4][2], const u16x8_t (&a)[4][2],
+                                        const u16x8_t (&b)[2][2]) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma16<BF16>(a[i][ks], b[j][ks], acc[i][j]);
+}
+
+template <bool BF16, bool FILTER>
+__global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ C, int64_t ld_img,
+    int64_t n_rows, int n_qtiles, int64_t n_ctiles, int ktiles,
+    const float* __restrict__ qscale, const float* __restrict__ cscale, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int64_t nwg = (int64_t)n_qtiles * n_ctiles;
+  const int64_t bid = blockIdx.x;
+  const int64_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int64_t L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int64_t per_group = (int64_t)QP_GROUP_C * n_qtiles;
+  const int64_t g = L / per_group, w = L - g * per_group;
+  const int64_t gc_rem = n_ctiles - g * QP_GROUP_C;
+  const int64_t gc = gc_rem < QP_GROUP_C ? gc_rem : QP_GROUP_C;
+  const int64_t ct = g * QP_GROUP_C + w % gc;
+  const int64_t qt = w / gc;
+  const int64_t c0 = ct * 256;
+  const int64_t q0 = qt * 256;
+  const int64_t last_c = n_rows - 1;
+  const int64_t last_q = (int64_t)n_qtiles * 256 - 1;
+
+  const int wa = wave >> 2;
+  const int wb = wave & 3;
+  const int fr = lane & 15;
+  int a_off[4][2], b_off[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int c = ks * 4 + (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = wa * 64 + i * 16 + fr;
+      a_off[i][ks] = r * 128 + ((c ^ (r & 7)) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = wb * 32 + j * 16 + fr;
+      b_off[j][ks] = r * 128 + ((c ^ (r & 7)) << 4);
+    }
+  }
+
+  f32x4_t acc0[4][2], acc1[4][2], acc2[4][2], acc3[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      acc0[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      acc1[i][j] = acc0[i][j];
+      acc2[i][j] = acc0[i][j];
+      acc3[i][j] = acc0[i][j];
+    }
+
+  // LDS-DMA through buffer descriptors (T8): one 32-bit per-lane offset serves every half-tile;
+  // rows past the end of the catalog fall outside num_records and read as 0 (never stored).
+  const int64_t row_bytes = ld_img * 2;
+  const int64_t c_rem = (n_rows - c0) * row_bytes;
+  const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(C + c0 * ld_img), 0, (int)(c_rem < 0x7fffffffLL ? c_rem : 0x7fffffffLL), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsQ = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(Q + q0 * ld_img), 0, (int)(256 * row_bytes), 0x00020000);
+  // lane: row (wave*16 + (lane>>3)) of the half, 16-byte chunk (lane&7)^(lane>>3)
+  const int voff = (int)((wave * 16 + (lane >> 3)) * row_bytes) + (((lane & 7) ^ (lane >> 3)) << 4);
+  const int piece_step = (int)(8 * row_bytes);
+  const int half_step = (int)(128 * row_bytes);
+  const int total = 4 * ktiles;
+  auto issue = [&](int idx) {
+    if (idx < total) {
+      const int tile = idx >> 2, type = idx & 3;
+      char* dst = smem + (tile & 1) * QP_BUF + p_half_off(type) + wave * 2048;
+      const int soff = tile * 128 + ((type == P_A1 || type == P_B1) ? half_step : 0);
+      const __amdgpu_buffer_rsrc_t rs = (type == P_A0 || type == P_A1) ? rsC : rsQ;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)dst, 16, voff, soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + 1024), 16, voff,
+                                               soff + piece_step, 0, 0);
+    }
+  };
+  auto wait_for = [&](int needed, int last_issued) {
+    const int last = last_issued < total - 1 ? last_issued : total - 1;
+    const int n = last - needed;
+    wait_vm_halves(n > 0 ? n : 0);
+  };
+  auto read_a = [&](u16x8_t (&a)[4][2], const char* half) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i][ks] = *(const u16x8_t*)(half + a_off[i][ks]);
+  };
+  auto read_b = [&](u16x8_t (&b)[2][2], const char* half) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j][ks] = *(const u16x8_t*)(half + b_off[j][ks]);
+  };
+
+  u16x8_t fa0[4][2], fa1[4][2], fbx[2][2], fby[2][2];
+  // prologue: sequence indices 0..6; A0(0), B0(0) into the A0 / X sets
+#pragma unroll
+  for (int idx = 0; idx < 7; ++idx) issue(idx);
+  wait_for(1, 6);
+  qp_barrier();
+  read_a(fa0, smem + p_half_off(P_A0));
+  read_b(fbx, smem + p_half_off(P_B0));
+  wait_for(2, 6);  // B1(0), read in Q1(0)
+
+  // One tile of four phases. B0(t) lives in `s0`, B1(t) in `s1`; Q4 reads B0(t+1) into s1.
+#define QP2_TILE(T, s0, s1)                                                                       \
+  {                                                                                              \
+    const int t_ = (T);                                                                          \
+    const char* buf = smem + (t_ & 1) * QP_BUF;                                                  \
+    const char* nbuf = smem + ((t_ + 1) & 1) * QP_BUF;                                           \
+    /* Q1 (A0, B0): read B1(t) */                                                                \
+    qp_barrier();                                                                                \
+    issue(4 * t_ + 7);                                                                           \
+    qp2_mma<BF16>(acc0, fa0, s0);                                                                \
+    read_b(s1, buf + p_half_off(P_B1));                                                          \
+    _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_) {                                           \
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
+    }                                                                                            \
+    wait_for(4 * t_ + 3, 4 * t_ + 7); /* A1(t) for Q2 */                                         \
+    /* Q2 (A0, B1): read A1(t) */                                                                \
+    qp_barrier();                                                                                \
+    issue(4 * t_ + 8);                                                                           \
+    qp2_mma<BF16>(acc1, fa0, s1);                                                                \
+    read_a(fa1, buf + p_half_off(P_A1));                                                         \
+    _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                           \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
+    }                                                                                            \
+    /* Q3 (A1, B1): no reads */                                                                  \
+    qp_barrier();                                                                                \
+    issue(4 * t_ + 9);                                                                           \
+    qp2_mma<BF16>(acc2, fa1, s1);                                                                \
+    wait_for(4 * t_ + 5, 4 * t_ + 9); /* A0(t+1), B0(t+1) for Q4 */                              \
+    /* Q4 (A1, B0): read A0(t+1), B0(t+1) */                                                     \
+    qp_barrier();                                                                                \
+    issue(4 * t_ + 10);                                                                          \
+    qp2_mma<BF16>(acc3, fa1, s0);                                                                \
+    if (t_ + 1 < ktiles) {                                                                       \
+      read_a(fa0, nbuf + p_half_off(P_A0));                                                      \
+      read_b(s1, nbuf + p_half_off(P_B0));                                                       \
+    }                                                                                            \
+    _Pragma("unroll") for (int i_ = 0; i_ < 12; ++i_) {                                          \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
+    }                                                                                            \
+    wait_for(4 * t_ + 6, 4 * t_ + 10); /* B1(t+1) for Q1(t+1) */                                 \
+  }
+
+  int t = 0;
+  for (; t + 1 < ktiles; t += 2) {
+    QP2_TILE(t, fbx, fby);
+    QP2_TILE(t + 1, fby, fbx);
+  }
+  if (t < ktiles) QP2_TILE(t, fbx, fby);
+#undef QP2_TILE
+
+  // ---- epilogue: quadrant qd = (ah, bh) as in qp ----
+  auto store_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t q = q0 + bh * 128 + wb * 32 + j * 16 + fr;
+      const float qs = qscale[q];
+      const float th = FILTER ? e.thr[q] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t i0 = c0 + ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
+        epilogue4<FILTER>(e, q, i0, n_rows, acc[i][j], qs, th, cscale);
+      }
+    }
+  };
+  store_quadrant(acc0, 0, 0);
+  store_quadrant(acc1, 0, 1);
+  store_quadrant(acc2, 1, 1);
+  store_quadrant(acc3, 1, 0);
+}
+
+template <bool FILTER>
+static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
+                       int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
+                       const float* cscale, const EpiArgs& e, hipStream_t stream) {
+  static const int force_tile = [] {
+    const char* v = getenv("EBT_GEMM_TILE");
+    return v ? atoi(v) : 0;
+  }();
+  const bool big = B_pad % HBN_ == 0 && force_tile != 128;
+  const int n_qtiles = (int)(B_pad / (big ? HBN_ : GBN));
+  const int64_t n_ctiles = ceil_div(n_rows, big ? HBM_ : GBM);
+  const int64_t nwg = n_ctiles * n_qtiles;
+  if (nwg > 0x7fffffffLL) {
+    set_error("screen gemm: grid too large");
+    return EBT_EINVAL;
+  }
+  const uint16_t* Q = (const uint16_t*)qimg;
+  const uint16_t* C = (const uint16_t*)cimg;
+  if (big && force_tile == 0) {  // default: pipelined quadrant-phase kernel
+    dim3 grid((unsigned)nwg), block(QP_THREADS);
+    auto k = img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, FILTER>
+                                   : screen_gemm_qp2_kernel<false, FILTER>;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, QP_LDS);
+    hipLaunchKernelGGL(k, grid, block, QP_LDS, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
+                       n_ctiles, d_pad / 64, qscale, cscale, e);
+    return launch_check("screen_gemm_qp2_kernel");
+  }
+  if (big && force_tile == 1) {  // quadrant phases, two barriers per phase
+    dim3 grid((unsigned)nwg), block(QP_THREADS);
+    auto k = img_dtype == EBT_BF16 ? screen_gemm_qp_kernel<true, FILTER>
+                                   : screen_gemm_qp_kernel<false, FILTER>;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, QP_LDS);
+    hipLaunchKernelGGL(k, grid, block, QP_LDS, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
+                       n_ctiles, d_pad / 64, qscale, cscale, e);
+    return launch_check("screen_gemm_qp_kernel");
+  }
+  if (big) {
+    dim3 grid((unsigned)nwg), block(HTHREADS);
+    auto k = img_dtype == EBT_BF16 ? screen_gemm256_kernel<true, FILTER>
+                                   : screen_gemm256_kernel<false, FILTER>;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              HLDS_BYTES);
+    hipLaunchKernelGGL(k, grid, block, HLDS_BYTES, stream, Q, C, (int64_t)ld_img, n_rows,
+                       n_qtiles, n_ctiles, d_pad / HBK_, qscale, cscale, e);
+    return launch_check("screen_gemm256_kernel");
+  }
+  dim3 grid((unsigned)nwg), block(GTHREADS);
+  auto k = img_dtype == EBT_BF16 ? screen_gemm_kernel<true, FILTER>
+                                 : screen_gemm_kernel<false, FILTER>;
+  hipLaunchKernelGGL(k, grid, block, GLDS_BYTES, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
+                     n_ctiles, d_pad / GBK, qscale, cscale, e);
+  return launch_check("screen_gemm_kernel");
+}
+
+static int check_gemm_args(const char* who, const void* qimg, int64_t B_pad, const void* cimg,
+                           int64_t n_rows, int32_t d_pad, int32_t ld_img, int img_dtype,
+                           const float* qscale, const float* cscale) {
+  if (!qimg || !cimg || !qscale) {
+    set_error("%s: null pointer", who);
     return EBT_EINVAL;
   }
   if (B_pad <= 0 || B_pad % GBN != 0 || n_rows <= 0 || d_pad <= 0 || d_pad % GBK != 0 ||
-      ld_img < d_pad || ld_img % 64 != 0 || ld_scores < n_rows || ld_scores % 4 != 0 ||
-      (img_dtype != EBT_F16 && img_dtype != EBT_BF16)) {
-    set_error("ebt_screen_scores: bad shape (B_pad=%lld n=%lld d_pad=%d ld_img=%d ld_s=%lld)",
-              (long long)B_pad, (long long)n_rows, d_pad, ld_img, (long long)ld_scores);
+      ld_img < d_pad || ld_img % 64 != 0 || (img_dtype != EBT_F16 && img_dtype != EBT_BF16)) {
+    set_error("%s: bad shape (B_pad=%lld n=%lld d_pad=%d ld_img=%d)", who, (long long)B_pad,
+              (long long)n_rows, d_pad, ld_img);
     return EBT_EINVAL;
   }
   if (cscale && ((uintptr_t)cscale & 15)) {
-    set_error("ebt_screen_scores: cscale must be 16-byte aligned");
+    set_error("%s: cscale must be 16-byte aligned", who);
     return EBT_EINVAL;
   }
-  const int n_qtiles = (int)(B_pad / GBN);
-  const int64_t n_ctiles = ceil_div(n_rows, GBM);
-  const int64_t nwg = n_ctiles * n_qtiles;
-  if (nwg > 0x7fffffffLL) {
-    set_error("ebt_screen_scores: grid too large");
+  return EBT_OK;
+}
+
+int screen_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows, int32_t d_pad,
+                int32_t ld_img, int img_dtype, const float* qscale, const float* cscale,
+                float* scores, int64_t ld_scores, hipStream_t stream) {
+  int rc = check_gemm_args("ebt_screen_scores", qimg, B_pad, cimg, n_rows, d_pad, ld_img,
+                           img_dtype, qscale, cscale);
+  if (rc) return rc;
+  if (!scores || ld_scores < n_rows || ld_scores % 4 != 0) {
+    set_error("ebt_screen_scores: bad score buffer (ld_s=%lld)", (long long)ld_scores);
     return EBT_EINVAL;
   }
-  dim3 grid((unsigned)nwg), block(GTHREADS);
-  if (img_dtype == EBT_BF16)
-    hipLaunchKernelGGL(screen_gemm_kernel<true>, grid, block, GLDS_BYTES, stream,
-                       (const uint16_t*)qimg, (const uint16_t*)cimg, (int64_t)ld_img, n_rows,
-                       n_qtiles, n_ctiles, d_pad / GBK, qscale, cscale, scores, ld_scores);
-  else
-    hipLaunchKernelGGL(screen_gemm_kernel<false>, grid, block, GLDS_BYTES, stream,
-                       (const uint16_t*)qimg, (const uint16_t*)cimg, (int64_t)ld_img, n_rows,
-                       n_qtiles, n_ctiles, d_pad / GBK, qscale, cscale, scores, ld_scores);
-  return launch_check("screen_gemm_kernel");
+  EpiArgs e{};
+  e.S = scores;
+  e.ld_s = ld_scores;
+  return launch_gemm<false>(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale, cscale,
+                            e, stream);
+}
+
+int screen_gemm_filter(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
+                       int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
+                       const float* cscale, const float* thr, int* cnt, float* cand_v,
+                       int64_t* cand_i, int64_t ld_cand, int64_t cand_off, int cap,
+                       int64_t idx_base, hipStream_t stream) {
+  int rc = check_gemm_args("screen_gemm_filter", qimg, B_pad, cimg, n_rows, d_pad, ld_img,
+                           img_dtype, qscale, cscale);
+  if (rc) return rc;
+  if (!thr || !cnt || !cand_v || !cand_i || cap < 1 || ld_cand < cand_off + cap) {
+    set_error("screen_gemm_filter: bad candidate buffer");
+    return EBT_EINVAL;
+  }
+  EpiArgs e{};
+  e.thr = thr;
+  e.cnt = cnt;
+  e.cand_v = cand_v;
+  e.cand_i = cand_i;
+  e.ld_cand = ld_cand;
+  e.cand_off = cand_off;
+  e.cap = cap;
+  e.idx_base = idx_base;
+  return launch_gemm<true>(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale, cscale,
+                           e, stream);
 }
 
 }  // namespace ebt

@@ -211,7 +211,8 @@ template <bool HAS_IDX, bool VEC>
 __global__ __launch_bounds__(STHREADS, 2) void select_topk_kernel(
     const float* __restrict__ vals, const int64_t* __restrict__ idxs, int64_t ld, int64_t n,
     int64_t seg_len, int64_t idx_base, int kprime, float* __restrict__ out_vals,
-    int64_t* __restrict__ out_idx, int64_t ld_out) {
+    int64_t* __restrict__ out_idx, int64_t ld_out, const int* __restrict__ row_cnt,
+    int64_t n_head, int cap) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const SelLayout Lo = sel_layout(kprime);
   uint32_t* bkey = (uint32_t*)(smem + Lo.off_key);
@@ -222,11 +223,16 @@ __global__ __launch_bounds__(STHREADS, 2) void select_topk_kernel(
   uint32_t* misc = (uint32_t*)(smem + Lo.off_misc + 64);
 
   const int tid = threadIdx.x, lane = tid & 63;
-  const int64_t row = blockIdx.y;
-  const int seg = blockIdx.x;
+  const int64_t row = blockIdx.x;
+  const int seg = blockIdx.y;
   const int64_t s0 = (int64_t)seg * seg_len;
   int64_t s1 = s0 + seg_len;
   s1 = s1 < n ? s1 : n;
+  if (row_cnt) {  // candidate lists: a fixed head plus a counted (capped) tail per row
+    const int c = row_cnt[row];
+    const int64_t nr = n_head + (c < cap ? c : cap);
+    s1 = s1 < nr ? s1 : nr;
+  }
   const float* vrow = vals + row * ld;
   const int64_t* irow = HAS_IDX ? idxs + row * ld : nullptr;
 
@@ -347,11 +353,13 @@ __global__ __launch_bounds__(STHREADS, 2) void select_topk_kernel(
 
 size_t select_lds_bytes(int kprime) { return sel_layout(kprime).bytes; }
 
-int select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B, int64_t n,
-                int64_t idx_base, int32_t kprime, int32_t segs, float* out_vals,
-                int64_t* out_idx, int64_t ld_out, hipStream_t stream) {
+static int select_launch(const float* vals, const int64_t* idx, int64_t ld, int64_t B,
+                         int64_t n, int64_t idx_base, int32_t kprime, int32_t segs,
+                         float* out_vals, int64_t* out_idx, int64_t ld_out, const int* row_cnt,
+                         int64_t n_head, int cap, hipStream_t stream) {
   if (!vals || !out_vals || !out_idx || B < 0 || n < 0 || ld < n || segs < 1 || kprime < 1 ||
-      kprime > KPRIME_MAX || ld_out < (int64_t)segs * kprime || n >= 0x7fffffffLL) {
+      kprime > KPRIME_MAX || ld_out < (int64_t)segs * kprime || n >= 0x7fffffffLL ||
+      segs > 65535 || B > 0x7fffffffLL) {
     set_error("ebt_select_topk: bad arguments (B=%lld n=%lld ld=%lld kprime=%d segs=%d)",
               (long long)B, (long long)n, (long long)ld, kprime, segs);
     return EBT_EINVAL;
@@ -362,12 +370,13 @@ int select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B, in
   const bool vec = (ld % 4 == 0) && (((uintptr_t)vals & 15) == 0) &&
                    (!idx || ((uintptr_t)idx & 15) == 0);
   const size_t lds = select_lds_bytes(kprime);
-  dim3 grid((unsigned)segs, (unsigned)B), block(STHREADS);
+  dim3 grid((unsigned)B, (unsigned)segs), block(STHREADS);
 #define EBT_SEL_LAUNCH(H, V)                                                                  \
   (void)hipFuncSetAttribute((const void*)select_topk_kernel<H, V>,                            \
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
   hipLaunchKernelGGL((select_topk_kernel<H, V>), grid, block, lds, stream, vals, idx, ld, n, \
-                     seg_len, idx_base, (int)kprime, out_vals, out_idx, ld_out)
+                     seg_len, idx_base, (int)kprime, out_vals, out_idx, ld_out, row_cnt,     \
+                     n_head, cap)
   if (idx) {
     if (vec) { EBT_SEL_LAUNCH(true, true); }
     else { EBT_SEL_LAUNCH(true, false); }
@@ -377,6 +386,72 @@ int select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B, in
   }
 #undef EBT_SEL_LAUNCH
   return launch_check("select_topk_kernel");
+}
+
+int select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B, int64_t n,
+                int64_t idx_base, int32_t kprime, int32_t segs, float* out_vals,
+                int64_t* out_idx, int64_t ld_out, hipStream_t stream) {
+  return select_launch(vals, idx, ld, B, n, idx_base, kprime, segs, out_vals, out_idx, ld_out,
+                       nullptr, 0, 0, stream);
+}
+
+// Candidate-list select over rows made of a fixed head of n_head entries followed by a tail
+// whose valid length is min(row_cnt[b], cap) (the fused screen's appended candidates).
+int select_topk_counted(const float* vals, const int64_t* idx, int64_t ld, int64_t B,
+                        int64_t n_head, const int* row_cnt, int cap, int32_t kprime,
+                        float* out_vals, int64_t* out_idx, int64_t ld_out, hipStream_t stream) {
+  return select_launch(vals, idx, ld, B, n_head + cap, 0, kprime, 1, out_vals, out_idx, ld_out,
+                       row_cnt, n_head, cap, stream);
+}
+
+// ------------------------------------------------------------- fused-screen helpers -------
+// thr[b] = vals[b*ld + kprime-1]: the k'-th best approx score of the head chunk, a lower bound
+// of the query's global k'-th best (-inf when the head had fewer than k' valid rows).
+__global__ void kth_threshold_kernel(const float* __restrict__ vals, int64_t ld, int64_t B,
+                                     int64_t B_pad, int kprime, float* __restrict__ thr) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) thr[b] = vals[b * ld + kprime - 1];
+  else if (b < B_pad) thr[b] = __builtin_inff();  // padding queries append nothing
+}
+
+int kth_threshold(const float* vals, int64_t ld, int64_t B, int64_t B_pad, int kprime,
+                  float* thr, hipStream_t st) {
+  hipLaunchKernelGGL(kth_threshold_kernel, dim3((unsigned)ceil_div(B_pad, 256)), dim3(256), 0,
+                     st, vals, ld, B, B_pad, kprime, thr);
+  return launch_check("kth_threshold_kernel");
+}
+
+// Excluded rows among appended candidates (lib.py:48,55): binary search of each candidate's
+// GLOBAL row in the query's exclusion list (sorted ascending); hits become -inf.
+__global__ __launch_bounds__(256) void mask_candidates_kernel(
+    float* __restrict__ cand_v, const int64_t* __restrict__ cand_i, int64_t ld, int64_t off,
+    const int* __restrict__ cnt, int cap, int64_t row_offset, const int64_t* __restrict__ eo,
+    const int64_t* __restrict__ er) {
+  const int64_t b = blockIdx.x;
+  const int64_t lo0 = eo[b], hi0 = eo[b + 1];
+  if (hi0 <= lo0) return;
+  int c = cnt[b];
+  c = c < cap ? c : cap;
+  for (int j = threadIdx.x; j < c; j += blockDim.x) {
+    const int64_t o = b * ld + off + j;
+    const int64_t g = cand_i[o] + row_offset;
+    int64_t lo = lo0, hi = hi0;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (er[mid] < g) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo < hi0 && er[lo] == g) cand_v[o] = -__builtin_inff();
+  }
+}
+
+int mask_candidates(float* cand_v, const int64_t* cand_i, int64_t ld, int64_t off, int64_t B,
+                    const int* cnt, int cap, int64_t row_offset, const int64_t* eo,
+                    const int64_t* er, hipStream_t st) {
+  if (B == 0) return EBT_OK;
+  hipLaunchKernelGGL(mask_candidates_kernel, dim3((unsigned)B), dim3(256), 0, st, cand_v, cand_i,
+                     ld, off, cnt, cap, row_offset, eo, er);
+  return launch_check("mask_candidates_kernel");
 }
 
 }  // namespace ebt

@@ -36,6 +36,13 @@ def _round_up(v: int, m: int) -> int:
     return (v + m - 1) // m * m
 
 
+def pad_batch(B: int) -> int:
+    """Query rows of the MFMA image: the 256x256-tile GEMM serves batches above 128 queries,
+    the 128x128-tile one smaller batches (ebt_screen_scores picks by B_pad % 256)."""
+    B = max(B, 1)
+    return _round_up(B, 128) if B <= 128 else _round_up(B, 256)
+
+
 @dataclass
 class QueryBatch:
     """Device-side prepared queries (ebt_query_* outputs)."""
@@ -51,7 +58,7 @@ class QueryBatch:
 
     def subset(self, idx: torch.Tensor) -> "QueryBatch":
         n = int(idx.numel())
-        B_pad = _round_up(max(n, 1), 128)
+        B_pad = pad_batch(n)
         qimg = torch.zeros((B_pad, self.qimg.shape[1]), dtype=self.qimg.dtype, device=self.qimg.device)
         qimg[:n] = self.qimg.index_select(0, idx)
         qscale = torch.ones(B_pad, dtype=torch.float32, device=self.qimg.device)
@@ -66,7 +73,7 @@ def csr_from_lists(lists: Sequence[Sequence[int]], device) -> Tuple[torch.Tensor
     off = [0]
     flat = []
     for l in lists:
-        flat.extend(int(v) for v in l)
+        flat.extend(sorted(int(v) for v in l))  # sorted: ebt_cosine_topk binary-searches them
         off.append(len(flat))
     o = torch.tensor(off, dtype=torch.int64, device=device)
     r = torch.tensor(flat if flat else [0], dtype=torch.int64, device=device)
@@ -134,7 +141,7 @@ def prepare_queries(catalog: Catalog, queries: Optional[torch.Tensor] = None,
                 "by check_pairwise_arrays.")
         scale = (1.0 / counts.to(torch.float64)).contiguous()
         call("ebt_scale_rows_f64", ptr(q64), B, d, ptr(scale), st)
-    B_pad = _round_up(max(B, 1), 128)
+    B_pad = pad_batch(B)
     qimg = torch.empty((B_pad, catalog.ld_img), dtype=catalog.img_torch_dtype, device=dev)
     qscale = torch.empty(B_pad, dtype=torch.float32, device=dev)
     eps = torch.empty(B_pad, dtype=torch.float32, device=dev)
@@ -160,13 +167,14 @@ def _chunk_rows(catalog: Catalog, B_pad: int, budget: int) -> int:
 def run_pipeline(catalog: Catalog, qb: QueryBatch, k: int, kprime: int,
                  exclude: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
                  chunk_rows: Optional[int] = None, timer: Optional[_lib.Timer] = None,
-                 workspace: Optional[torch.Tensor] = None):
-    """One ebt_cosine_topk call. Returns (scores f64 [B,k], rows i64 [B,k], certified i32 [B])."""
+                 workspace: Optional[torch.Tensor] = None, flags: int = 0):
+    """One ebt_cosine_topk call. Returns (scores f64 [B,k], rows i64 [B,k], certified i32 [B]);
+    certified is 1 (exact), 0 (widen k') or -1 (fused candidate list overflowed: run unfused)."""
     dev = catalog.device
     st = stream_of(dev)
     B, B_pad = qb.B, qb.B_pad
     chunk = chunk_rows or _chunk_rows(catalog, B_pad, DEFAULT_SCORE_BUDGET)
-    need = _lib.load().ebt_cosine_topk_workspace(B, B_pad, catalog.n, kprime, chunk)
+    need = _lib.load().ebt_cosine_topk_workspace(B, B_pad, catalog.n, kprime, chunk, flags)
     if need == 0:
         raise EbertError("invalid workspace request")
     if workspace is None or workspace.numel() < need:
@@ -178,7 +186,7 @@ def run_pipeline(catalog: Catalog, qb: QueryBatch, k: int, kprime: int,
     call("ebt_cosine_topk", ptr(qb.q64), ptr(qb.qimg), ptr(qb.qscale), ptr(qb.eps), B, B_pad,
          ptr(catalog.data), catalog.dtype_code, catalog.ld, ptr(catalog.gnorm), ptr(catalog.image),
          ptr(catalog.cscale), catalog.img_dtype, catalog.ld_img, catalog.n, catalog.d,
-         catalog.d_pad, catalog.row_offset, ptr(eo), ptr(er), k, kprime, chunk, ptr(workspace),
+         catalog.d_pad, catalog.row_offset, ptr(eo), ptr(er), k, kprime, chunk, flags, ptr(workspace),
          int(workspace.numel()), ptr(out_s), ptr(out_r), ptr(cert),
          timer.handle if timer is not None else None, st)
     return out_s, out_r, cert
@@ -189,7 +197,7 @@ def score_topk(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
                exclude: Optional[Union[Tuple[torch.Tensor, torch.Tensor], Sequence[Sequence[int]]]] = None,
                kprime: Optional[int] = None, chunk_rows: Optional[int] = None,
                timer: Optional[_lib.Timer] = None, liked_counts: Optional[torch.Tensor] = None,
-               liked_sum_hook=None) -> Tuple[torch.Tensor, torch.Tensor]:
+               liked_sum_hook=None, fuse: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
     """Top-k by cosine (mean cosine over liked rows) with exclusions.
 
     Returns (scores float64 [B, k], rows int64 [B, k]) on the catalog's device, ordered by
@@ -211,18 +219,29 @@ def score_topk(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
         raise EbertError(f"k={k} > {KPRIME_MAX} over a {catalog.n}-row catalog is not supported")
     kp = kprime or default_kprime(catalog, k_eff)
     kp = max(_round_up(k_eff, 4), min(_round_up(kp, 4), n_cap, KPRIME_MAX))
-    s, r, cert = run_pipeline(catalog, qb, k_eff, kp, exclude, chunk_rows, timer)
-    # certification retry: only queries whose candidate set is not provably complete
+    flags = 0 if fuse else _lib.EBT_FLAG_NO_FUSE
+    s, r, cert = run_pipeline(catalog, qb, k_eff, kp, exclude, chunk_rows, timer, flags=flags)
+    # retries, only for the queries that need one: a fused candidate list that overflowed
+    # (cert -1: rerun unfused) or a candidate set that is not provably complete (cert 0: widen k')
     while True:
-        bad = torch.nonzero(cert == 0).flatten()
-        if bad.numel() == 0:
+        flat = cert.cpu()
+        over = torch.nonzero(flat < 0).flatten().to(dev)
+        bad = torch.nonzero(flat == 0).flatten().to(dev)
+        if over.numel() == 0 and bad.numel() == 0:
             break
+        if over.numel():
+            sub_ex = csr_subset(exclude[0], exclude[1], over) if exclude is not None else None
+            s2, r2, c2 = run_pipeline(catalog, qb.subset(over), k_eff, kp, sub_ex, chunk_rows,
+                                      timer, flags=_lib.EBT_FLAG_NO_FUSE)
+            s[over], r[over], cert[over] = s2, r2, c2
+            continue
         if kp >= min(n_cap, KPRIME_MAX):
             raise EbertError(f"{bad.numel()} queries could not be certified at k'={kp} "
                              "(a tie cluster wider than k' at the k-th score)")
         kp = min(kp * 4, n_cap, KPRIME_MAX)
         sub_ex = csr_subset(exclude[0], exclude[1], bad) if exclude is not None else None
-        s2, r2, c2 = run_pipeline(catalog, qb.subset(bad), k_eff, kp, sub_ex, chunk_rows, timer)
+        s2, r2, c2 = run_pipeline(catalog, qb.subset(bad), k_eff, kp, sub_ex, chunk_rows, timer,
+                                  flags=flags)
         s[bad], r[bad], cert[bad] = s2, r2, c2
     if k_eff < k:
         pad_s = torch.full((qb.B, k - k_eff), float("nan"), dtype=torch.float64, device=dev)

@@ -34,18 +34,20 @@ def test_invalid_args_return_einval_without_gpu():
     lib = _lib.load()
     assert lib.ebt_select_topk(None, None, 0, 1, 0, 0, 0, 1, None, None, 0, None) == -1
     assert b"ebt_select_topk" in lib.ebt_last_error()
-    assert lib.ebt_cosine_topk_workspace(10, 5, 100, 8, 128) == 0  # B_pad < B
-    assert lib.ebt_cosine_topk_workspace(10, 128, 1000, 104, 512) > 0
+    assert lib.ebt_cosine_topk_workspace(10, 5, 100, 8, 128, 0) == 0  # B_pad < B
+    assert lib.ebt_cosine_topk_workspace(10, 128, 1000, 104, 512, 0) > 0
     assert lib.ebt_merge_topk(None, None, 0, 1, 1, None, None, None) == -1
 
 
 def test_workspace_grows_with_chunks():
     from robot_ebert_amd import _lib
     lib = _lib.load()
-    one = lib.ebt_cosine_topk_workspace(4096, 4096, 1_000_000, 200, 1_000_064)
-    many = lib.ebt_cosine_topk_workspace(4096, 4096, 1_000_000, 200, 262_144)
+    one = lib.ebt_cosine_topk_workspace(4096, 4096, 1_000_000, 200, 1_000_064, 1)
+    many = lib.ebt_cosine_topk_workspace(4096, 4096, 1_000_000, 200, 262_144, 1)
+    fused = lib.ebt_cosine_topk_workspace(4096, 4096, 1_000_000, 200, 262_144, 0)
     assert one > 4096 * 1_000_000 * 4
     assert many < one
+    assert fused < many  # the fused screen materialises only the head rows' scores
 
 
 def test_no_cpu_fallback_on_cpu_tensors():

@@ -237,6 +237,44 @@ def test_chunked_catalog_equals_single_chunk(cuda_device):
     assert_topk_equal(s1, r1, s_ref, r_ref)
 
 
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_fused_screen_equals_unfused_and_oracle(cuda_device, dt):
+    """n >= 2H takes the fused screen (head threshold + GEMM epilogue filter)."""
+    ebt, L = _ebt()
+    n, d, B, k = 300_000, 256, 300, 40
+    c = gaussian(1, n, d, dt)
+    q = gaussian(2, B, d, dt)
+    rng = np.random.default_rng(3)
+    excl = [np.sort(rng.choice(n, 200, replace=False)) for _ in range(B)]
+    excl[0] = np.arange(0, n, 3)  # a third of the catalog excluded for query 0
+    cat = ebt.Catalog(_t(c, dt, cuda_device))
+    qt = _t(q, dt, cuda_device)
+    timer = ebt.Timer()
+    s1, r1 = ebt.score_topk(cat, k, queries=qt, exclude=[list(e) for e in excl], timer=timer)
+    assert timer.query("gemm_filter")[1] >= 1, "fused path not taken"
+    s2, r2 = ebt.score_topk(cat, k, queries=qt, exclude=[list(e) for e in excl], fuse=False)
+    assert torch.equal(r1, r2)
+    torch.testing.assert_close(s1, s2, rtol=0, atol=0)
+    sample = list(range(0, B, 25))
+    s_ref, r_ref = R.cosine_topk(q[sample], c, k, [excl[i] for i in sample])
+    assert_topk_equal(s1[sample], r1[sample], s_ref, r_ref)
+
+
+def test_fused_overflow_falls_back(cuda_device):
+    """Scores that grow with the row index make the head threshold useless: every tail row
+    passes, the candidate list overflows, and the query must be redone unfused -- exactly."""
+    ebt, L = _ebt()
+    n, d, k = 200_000, 64, 16
+    rng = np.random.default_rng(9)
+    q = rng.standard_normal((2, d))
+    t = (np.arange(n) / n)[:, None]
+    c = q[0][None, :] * t + rng.standard_normal((n, d)) * (1.0 - t) * 0.5
+    cat = ebt.Catalog(_t(c, "f64", cuda_device))
+    s, r = ebt.score_topk(cat, k, queries=_t(q, "f64", cuda_device))
+    s_ref, r_ref = R.cosine_topk(q, c, k)
+    assert_topk_equal(s, r, s_ref, r_ref)
+
+
 # ----------------------------------------------------------- the reference call surface ----
 def _collab_setup(cuda_device):
     ebt, L = _ebt()

@@ -1,0 +1,85 @@
+"""Per-kernel microbenchmarks (GPU): screening GEMM TFLOP/s and streaming select GB/s.
+
+    python tools/kernel_bench.py [--gemm] [--select] [--rescore]
+
+Timed with torch.cuda.Event on the current stream, which is the stream libebert launches on.
+Random (Gaussian) operands: zero-filled data runs faster on this chip (DVFS), see the guide.
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from robot_ebert_amd import _lib as L  # noqa: E402
+
+
+def timeit(fn, iters=10, warm=3):
+    for _ in range(warm):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def bench_gemm(dev, B, N, d, dt):
+    g = torch.Generator(device=dev).manual_seed(0)
+    q = torch.randn((B, d), generator=g, device=dev).to(dt)
+    c = torch.randn((N, d), generator=g, device=dev).to(dt)
+    qs = torch.ones(B, device=dev)
+    S = torch.empty((B, N), device=dev)
+    st = L.stream_of(dev)
+    code = L.DTYPE_CODE[dt]
+    ms = timeit(lambda: L.call("ebt_screen_scores", L.ptr(q), B, L.ptr(c), N, d, d, code,
+                               L.ptr(qs), None, L.ptr(S), N, st))
+    tf = 2.0 * B * N * d / (ms * 1e-3) / 1e12
+    return {"kernel": "screen_gemm", "B": B, "N": N, "d": d, "dtype": str(dt), "ms": round(ms, 4),
+            "tflops": round(tf, 1), "frac_2500": round(tf / 2500, 4),
+            "tile": os.environ.get("EBT_GEMM_TILE", "auto")}
+
+
+def bench_select(dev, B, n, kp):
+    g = torch.Generator(device=dev).manual_seed(0)
+    v = torch.randn((B, n), generator=g, device=dev) * 0.0255
+    ov = torch.empty((B, kp), device=dev)
+    oi = torch.empty((B, kp), dtype=torch.int64, device=dev)
+    st = L.stream_of(dev)
+    ms = timeit(lambda: L.call("ebt_select_topk", L.ptr(v), None, n, B, n, 0, kp, 1, L.ptr(ov),
+                               L.ptr(oi), kp, st))
+    gbs = 4.0 * B * n / (ms * 1e-3) / 1e9
+    return {"kernel": "select_topk", "B": B, "n": n, "kprime": kp, "ms": round(ms, 4),
+            "GBps": round(gbs, 1), "frac_8000": round(gbs / 8000, 4)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gemm", action="store_true")
+    ap.add_argument("--select", action="store_true")
+    ap.add_argument("--one", action="store_true", help="single C3-chunk GEMM config (profiling)")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    L.load()
+    res = []
+    if args.one:
+        print(json.dumps(bench_gemm(dev, 4096, 262144, 1536, torch.float16)), flush=True)
+        return
+    if args.gemm or not args.select:
+        for (B, N, d, dt) in [(4096, 262144, 1536, torch.float16), (4096, 262144, 1536, torch.bfloat16),
+                              (1024, 100000, 768, torch.bfloat16), (4096, 65536, 1536, torch.float16)]:
+            res.append(bench_gemm(dev, B, N, d, dt))
+            print(json.dumps(res[-1]), flush=True)
+    if args.select or not args.gemm:
+        for (B, n, kp) in [(4096, 262144, 200), (4096, 262144, 104), (1024, 100000, 120)]:
+            res.append(bench_select(dev, B, n, kp))
+            print(json.dumps(res[-1]), flush=True)
+
+
+if __name__ == "__main__":
+    main()
