@@ -112,6 +112,18 @@ def cpu_baseline_and_parity(cfg, cat_gpu: torch.Tensor, q_gpu: torch.Tensor, s_g
     return base, parity
 
 
+def pmc_traffic(config: str, world: int):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
+    (profiles/pmc_<config>.json, FETCH_SIZE*2 + WRITE_SIZE, gfx950 correction applied when it
+    was written by tools/pmc_summary.py); null when no summary exists for this config."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}_n{world}.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -184,14 +196,26 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    gemm_ms, gemm_n = timer.query("gemm")
-    sel_ms, sel_n = timer.query("select")
-    msel_ms, msel_n = timer.query("merge_select")
-    res_ms, res_n = timer.query("rescore")
+    from robot_ebert_amd.search import plan
+    pl = plan(cat, cfg["b"], k)
+    st = {name: timer.query(name) for name in ("gemm", "gemm_filter", "mask", "select",
+                                               "merge_select", "rescore")}
     n_local = end - begin
-    flops = 2.0 * cfg["b"] * n_local * cfg["d"] * args.steps
-    achieved = flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else None
-    sel_bytes = 4.0 * cfg["b"] * n_local * args.steps
+    B, d = cfg["b"], cfg["d"]
+    head = pl["head_rows"]
+    tail = n_local - head if pl["fused"] else 0
+    # dominant kernel: the fused screening GEMM over the tail rows (else the score-writing GEMM)
+    if pl["fused"]:
+        dom_name, (dom_ms, dom_n) = "screen_gemm_qp2_kernel<filter>", st["gemm_filter"]
+        dom_flops = 2.0 * B * tail * d * args.steps
+    else:
+        dom_name, (dom_ms, dom_n) = "screen_gemm_qp2_kernel<store>", st["gemm"]
+        dom_flops = 2.0 * B * n_local * d * args.steps
+    achieved = dom_flops / (dom_ms * 1e-3) / 1e12 if dom_ms > 0 else None
+    all_gemm_ms = st["gemm"][0] + st["gemm_filter"][0]
+    all_tf = 2.0 * B * n_local * d * args.steps / (all_gemm_ms * 1e-3) / 1e12 if all_gemm_ms else None
+    sel_ms, sel_n = st["select"]
+    sel_bytes = 4.0 * B * (head if pl["fused"] else n_local) * args.steps  # f32 scores read
     sel_gbs = sel_bytes / (sel_ms * 1e-3) / 1e9 if sel_ms > 0 else None
     value = cfg["b"] * args.steps / elapsed
 
@@ -219,25 +243,25 @@ def main() -> None:
                 "arith": "f16/bf16 MFMA screen (f32 acc) + exact f64 rescore of certified candidates",
             },
             "roofline": {
-                "bound": "mfma", "kernel": "screen_gemm_kernel",
+                "bound": "mfma", "kernel": dom_name,
                 "achieved": round(achieved, 2) if achieved else None,
                 "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_F16_TFLOPS, 4) if achieved else None,
-                "traffic": None,
-                "per_launch": {"launches": gemm_n, "avg_ms": round(gemm_ms / max(gemm_n, 1), 3),
-                               "flops": flops / max(gemm_n, 1)},
+                "traffic": pmc_traffic(args.config, world),
+                "per_launch": {"launches": dom_n, "avg_ms": round(dom_ms / max(dom_n, 1), 4),
+                               "flops": dom_flops / max(dom_n, 1),
+                               "flops_formula": "2*B*rows*d (rows = tail rows of the fused screen)"},
+                "all_gemm_tflops": round(all_tf, 2) if all_tf else None,
             },
             "topk_roofline": {
-                "bound": "hbm", "kernel": "select_topk_kernel",
+                "bound": "hbm", "kernel": "select_topk_kernel (head rows)",
                 "achieved": round(sel_gbs, 1) if sel_gbs else None, "peak": PEAK_HBM_GBS,
                 "unit": "GB/s", "frac": round(sel_gbs / PEAK_HBM_GBS, 4) if sel_gbs else None,
-                "per_launch": {"launches": sel_n, "avg_ms": round(sel_ms / max(sel_n, 1), 3)},
+                "per_launch": {"launches": sel_n, "avg_ms": round(sel_ms / max(sel_n, 1), 4),
+                               "bytes_formula": "4*B*rows (f32 scores read once)"},
             },
-            "stage_ms_per_step": {
-                "gemm": round(gemm_ms / args.steps, 3), "select": round(sel_ms / args.steps, 3),
-                "merge_select": round(msel_ms / args.steps, 3),
-                "rescore": round(res_ms / args.steps, 3),
-            },
+            "plan": pl,
+            "stage_ms_per_step": {name: round(v[0] / args.steps, 4) for name, v in st.items()},
         }
         if world == 1 and not args.no_cpu_baseline:
             base, parity = cpu_baseline_and_parity(cfg, emb, q, s, r, args.cpu_budget)

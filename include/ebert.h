@@ -107,6 +107,16 @@ int ebt_screen_scores(const void* qimg, int64_t B_pad, const void* cimg, int64_t
                       int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
                       const float* cscale, float* scores, int64_t ld_scores, void* stream);
 
+/* The fused screen's GEMM: the same product, but only scores >= thr[b] leave the kernel, appended
+ * to query b's candidate list: slot p = atomicAdd(&cnt[b], 1); if p < cap,
+ * cand_v/cand_i[b*ld_cand + cand_off + p] = (score, idx_base + i). cnt[b] > cap afterwards means
+ * the list overflowed. thr has B_pad entries (use +inf for padding rows). */
+int ebt_screen_filter(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
+                      int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
+                      const float* cscale, const float* thr, int32_t* cnt, float* cand_v,
+                      int64_t* cand_i, int64_t ld_cand, int64_t cand_off, int32_t cap,
+                      int64_t idx_base, void* stream);
+
 /* Excluded rows (lib.py:48,55: rated movies are not candidates): for every b < B and every
  * GLOBAL row g in excl_rows[excl_off[b] .. excl_off[b+1]) with col_begin <= g < col_end,
  * scores[b][g - col_begin] = -inf. */
@@ -144,6 +154,11 @@ int ebt_merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t
 /* ---- the whole pipeline -------------------------------------------------------------------
  * flags: EBT_FLAG_NO_FUSE disables the fused screen (every score row is materialised). */
 #define EBT_FLAG_NO_FUSE 1
+/* How ebt_cosine_topk will run these sizes (host pointers out): head rows screened unfused,
+ * fused-candidate capacity per query (0 = not fused), score chunk rows, fused flag. */
+int ebt_cosine_topk_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
+                         int64_t chunk_rows, int flags, int64_t* head_rows, int64_t* cap,
+                         int64_t* chunk, int32_t* fused);
 /* Workspace bytes needed by ebt_cosine_topk for these sizes. */
 size_t ebt_cosine_topk_workspace(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
                                  int64_t chunk_rows, int flags);

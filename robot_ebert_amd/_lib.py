@@ -42,6 +42,8 @@ _SIGNATURES = {
                          _VP], _INT),
     "ebt_screen_scores": ([_VP, _I64, _VP, _I64, _I32, _I32, _INT, _VP, _VP, _VP, _I64, _VP],
                           _INT),
+    "ebt_screen_filter": ([_VP, _I64, _VP, _I64, _I32, _I32, _INT, _VP, _VP, _VP, _VP, _VP, _VP,
+                           _I64, _I64, _I32, _I64, _VP], _INT),
     "ebt_mask_excluded": ([_VP, _I64, _I64, _I64, _I64, _VP, _VP, _VP], _INT),
     "ebt_select_topk": ([_VP, _VP, _I64, _I64, _I64, _I64, _I32, _I32, _VP, _VP, _I64, _VP],
                         _INT),
@@ -49,6 +51,9 @@ _SIGNATURES = {
                      _VP, _VP, _VP, _VP], _INT),
     "ebt_merge_topk": ([_VP, _VP, _I32, _I64, _I32, _VP, _VP, _VP], _INT),
     "ebt_cosine_topk_workspace": ([_I64, _I64, _I64, _I32, _I64, _INT], _SZ),
+    "ebt_cosine_topk_plan": ([_I64, _I64, _I64, _I32, _I64, _INT, ctypes.POINTER(_I64),
+                              ctypes.POINTER(_I64), ctypes.POINTER(_I64),
+                              ctypes.POINTER(ctypes.c_int32)], _INT),
     "ebt_cosine_topk": ([_VP, _VP, _VP, _VP, _I64, _I64, _VP, _INT, _I64, _VP, _VP, _VP, _INT,
                          _I32, _I64, _I32, _I32, _I64, _VP, _VP, _I32, _I32, _I64, _INT, _VP, _SZ,
                          _VP, _VP, _VP, _VP, _VP], _INT),

@@ -283,6 +283,16 @@ int ebt_screen_scores(const void* qimg, int64_t B_pad, const void* cimg, int64_t
                      ld_scores, (hipStream_t)stream);
 }
 
+int ebt_screen_filter(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
+                      int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
+                      const float* cscale, const float* thr, int32_t* cnt, float* cand_v,
+                      int64_t* cand_i, int64_t ld_cand, int64_t cand_off, int32_t cap,
+                      int64_t idx_base, void* stream) {
+  return screen_gemm_filter(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale, cscale,
+                            thr, cnt, cand_v, cand_i, ld_cand, cand_off, cap, idx_base,
+                            (hipStream_t)stream);
+}
+
 int ebt_mask_excluded(float* scores, int64_t ld_scores, int64_t B, int64_t col_begin,
                       int64_t col_end, const int64_t* excl_off, const int64_t* excl_rows,
                       void* stream) {
@@ -314,6 +324,22 @@ size_t ebt_cosine_topk_workspace(int64_t B, int64_t B_pad, int64_t n_rows, int32
                                  int64_t chunk_rows, int flags) {
   if (B < 0 || B_pad < B || n_rows < 1 || kprime < 1 || chunk_rows < 1) return 0;
   return ws_layout(B, B_pad, n_rows, kprime, chunk_rows, flags).bytes;
+}
+
+int ebt_cosine_topk_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
+                         int64_t chunk_rows, int flags, int64_t* head_rows, int64_t* cap,
+                         int64_t* chunk, int32_t* fused) {
+  if (B < 0 || B_pad < B || n_rows < 1 || kprime < 1 || chunk_rows < 1 || !head_rows || !cap ||
+      !chunk || !fused) {
+    set_error("ebt_cosine_topk_plan: bad arguments");
+    return EBT_EINVAL;
+  }
+  const WsLayout L = ws_layout(B, B_pad, n_rows, kprime, chunk_rows, flags);
+  *head_rows = L.head;
+  *cap = L.fused ? L.cap : 0;
+  *chunk = L.chunk;
+  *fused = L.fused ? 1 : 0;
+  return EBT_OK;
 }
 
 int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, const float* eps,

@@ -623,7 +623,7 @@ __device__ __forceinline__ void qp2_mma(f32x4_t (&acc)[4][2], const u16x8_t (&a)
       for (int j = 0; j < 2; ++j) acc[i][j] = mfma16<BF16>(a[i][ks], b[j][ks], acc[i][j]);
 }
 
-template <bool BF16, bool FILTER>
+template <bool BF16, bool FILTER, int VAR = 0>
 __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ C, int64_t ld_img,
     int64_t n_rows, int n_qtiles, int64_t n_ctiles, int ktiles,
@@ -705,7 +705,7 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
   auto wait_for = [&](int needed, int last_issued) {
     const int last = last_issued < total - 1 ? last_issued : total - 1;
     const int n = last - needed;
-    wait_vm_halves(n > 0 ? n : 0);
+    if constexpr (!(VAR & 1)) wait_vm_halves(n > 0 ? n : 0);  // VAR&1: timing-only, racy
   };
   auto read_a = [&](u16x8_t (&a)[4][2], const char* half) {
 #pragma unroll
@@ -775,6 +775,9 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     wait_for(4 * t_ + 6, 4 * t_ + 10); /* B1(t+1) for Q1(t+1) */                                 \
   }
 
+  if constexpr (VAR & 2) {  // static priority for the younger half (MI355X_MICROARCH item 4)
+    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
   int t = 0;
   for (; t + 1 < ktiles; t += 2) {
     QP2_TILE(t, fbx, fby);
@@ -823,8 +826,18 @@ static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_
   const uint16_t* C = (const uint16_t*)cimg;
   if (big && force_tile == 0) {  // default: pipelined quadrant-phase kernel
     dim3 grid((unsigned)nwg), block(QP_THREADS);
+    static const int var = [] {
+      const char* v = getenv("EBT_GEMM_VAR");
+      return v ? atoi(v) : 0;
+    }();
     auto k = img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, FILTER>
                                    : screen_gemm_qp2_kernel<false, FILTER>;
+    if (var == 1)
+      k = img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, FILTER, 1>
+                                : screen_gemm_qp2_kernel<false, FILTER, 1>;
+    else if (var == 2)
+      k = img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, FILTER, 2>
+                                : screen_gemm_qp2_kernel<false, FILTER, 2>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, QP_LDS);
     hipLaunchKernelGGL(k, grid, block, QP_LDS, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
                        n_ctiles, d_pad / 64, qscale, cscale, e);

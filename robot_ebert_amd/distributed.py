@@ -31,11 +31,14 @@ def gather_partials(scores: torch.Tensor, rows: torch.Tensor,
                     group: Optional[dist.ProcessGroup] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """All-gather the [B, k] partial results of every rank -> [R, B, k] (rank order)."""
     world = dist.get_world_size(group)
-    gs = torch.empty((world,) + tuple(scores.shape), dtype=scores.dtype, device=scores.device)
-    gr = torch.empty((world,) + tuple(rows.shape), dtype=rows.dtype, device=rows.device)
+    B = scores.shape[0]
+    # concatenated along dim 0 (the layout every backend accepts), viewed as [R, B, k]
+    gs = torch.empty((world * B,) + tuple(scores.shape[1:]), dtype=scores.dtype,
+                     device=scores.device)
+    gr = torch.empty((world * B,) + tuple(rows.shape[1:]), dtype=rows.dtype, device=rows.device)
     dist.all_gather_into_tensor(gs, scores.contiguous(), group=group)
     dist.all_gather_into_tensor(gr, rows.contiguous(), group=group)
-    return gs, gr
+    return gs.view((world,) + tuple(scores.shape)), gr.view((world,) + tuple(rows.shape))
 
 
 def split_liked(liked: Sequence[Sequence[int]], begin: int, end: int):

@@ -164,6 +164,25 @@ def _chunk_rows(catalog: Catalog, B_pad: int, budget: int) -> int:
     return min(rows, _round_up(catalog.n, 128))
 
 
+def plan(catalog: Catalog, B: int, k: int, kprime: Optional[int] = None,
+         chunk_rows: Optional[int] = None, fuse: bool = True) -> dict:
+    """How score_topk will run a batch of B queries (ebt_cosine_topk_plan): k', fused or not,
+    head rows (screened through the materialised-score path), candidate capacity, chunk rows."""
+    import ctypes
+    B_pad = pad_batch(B)
+    k_eff = min(k, catalog.n)
+    kp = kprime or default_kprime(catalog, k_eff)
+    kp = max(_round_up(k_eff, 4), min(_round_up(kp, 4), _round_up(catalog.n, 4), KPRIME_MAX))
+    chunk = chunk_rows or _chunk_rows(catalog, B_pad, DEFAULT_SCORE_BUDGET)
+    h, c, ch = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    f = ctypes.c_int32()
+    call("ebt_cosine_topk_plan", B, B_pad, catalog.n, kp, chunk,
+         0 if fuse else _lib.EBT_FLAG_NO_FUSE, ctypes.byref(h), ctypes.byref(c), ctypes.byref(ch),
+         ctypes.byref(f))
+    return {"kprime": kp, "B_pad": B_pad, "fused": bool(f.value), "head_rows": h.value,
+            "cap": c.value, "chunk_rows": ch.value}
+
+
 def run_pipeline(catalog: Catalog, qb: QueryBatch, k: int, kprime: int,
                  exclude: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
                  chunk_rows: Optional[int] = None, timer: Optional[_lib.Timer] = None,

@@ -40,9 +40,26 @@ def bench_gemm(dev, B, N, d, dt):
     ms = timeit(lambda: L.call("ebt_screen_scores", L.ptr(q), B, L.ptr(c), N, d, d, code,
                                L.ptr(qs), None, L.ptr(S), N, st))
     tf = 2.0 * B * N * d / (ms * 1e-3) / 1e12
+    # fused-screen (filter) epilogue: threshold high enough that ~0.3% of scores are appended
+    thr = torch.full((B,), 0.0, device=dev)
+    thr[:] = 3.0 * (d ** 0.5)  # raw (unnormalised) Gaussian dot products: ~3 sigma
+    cap = 8192
+    cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+    cv = torch.empty((B, cap), device=dev)
+    ci = torch.empty((B, cap), dtype=torch.int64, device=dev)
+
+    def run_filter():
+        cnt.zero_()
+        L.call("ebt_screen_filter", L.ptr(q), B, L.ptr(c), N, d, d, code, L.ptr(qs), None,
+               L.ptr(thr), L.ptr(cnt), L.ptr(cv), L.ptr(ci), cap, 0, cap, 0, st)
+    ms_f = timeit(run_filter)
+    tf_f = 2.0 * B * N * d / (ms_f * 1e-3) / 1e12
     return {"kernel": "screen_gemm", "B": B, "N": N, "d": d, "dtype": str(dt), "ms": round(ms, 4),
             "tflops": round(tf, 1), "frac_2500": round(tf / 2500, 4),
-            "tile": os.environ.get("EBT_GEMM_TILE", "auto")}
+            "filter_ms": round(ms_f, 4), "filter_tflops": round(tf_f, 1),
+            "mean_appended": round(float(cnt.float().mean()), 1),
+            "tile": os.environ.get("EBT_GEMM_TILE", "auto"),
+            "var": os.environ.get("EBT_GEMM_VAR", "0")}
 
 
 def bench_select(dev, B, n, kp):
