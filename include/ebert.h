@@ -151,9 +151,21 @@ int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dt
 int ebt_merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, int32_t k,
                    double* out_scores, int64_t* out_rows, void* stream);
 
+/* Exact screen: scores[b*ld_scores + j] = (float)((q64_b . c_j) / gnorm64_j) in float64
+ * arithmetic for every row j < n_rows (no replacement in the reference: the fallback screen of
+ * EBT_FLAG_EXACT, whose only error is the final f32 rounding). */
+int ebt_screen_exact(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
+                     int64_t ld, const double* gnorm64, int64_t n_rows, float* scores,
+                     int64_t ld_scores, void* stream);
+
 /* ---- the whole pipeline -------------------------------------------------------------------
- * flags: EBT_FLAG_NO_FUSE disables the fused screen (every score row is materialised). */
+ * flags: EBT_FLAG_NO_FUSE disables the fused screen (every score row is materialised).
+ * EBT_FLAG_EXACT screens with ebt_screen_exact instead of the MFMA image (unfused; qimg,
+ * qscale, eps and cimg may be NULL): the last resort for a query that cannot be certified at
+ * kprime = 4096, certified with eps = EBT_EXACT_EPS (|q64| <= 1 as the ebt_query_* make it). */
 #define EBT_FLAG_NO_FUSE 1
+#define EBT_FLAG_EXACT 2
+#define EBT_EXACT_EPS 1.1920928955078125e-07f /* 2^-23 >= f32 rounding of |s| <= 1 + f64 error */
 /* How ebt_cosine_topk will run these sizes (host pointers out): head rows screened unfused,
  * fused-candidate capacity per query (0 = not fused), score chunk rows, fused flag. */
 int ebt_cosine_topk_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,

@@ -21,6 +21,7 @@ DTYPE_CODE = {torch.float32: EBT_F32, torch.bfloat16: EBT_BF16, torch.float16: E
               torch.float64: EBT_F64}
 STAGES = {"gemm": 0, "mask": 1, "select": 2, "merge_select": 3, "rescore": 4, "gemm_filter": 5}
 EBT_FLAG_NO_FUSE = 1
+EBT_FLAG_EXACT = 2
 
 
 class EbertError(RuntimeError):
@@ -50,6 +51,7 @@ _SIGNATURES = {
     "ebt_rescore": ([_VP, _I64, _I32, _VP, _INT, _I64, _VP, _I64, _VP, _VP, _I32, _I32, _I64, _VP,
                      _VP, _VP, _VP, _VP], _INT),
     "ebt_merge_topk": ([_VP, _VP, _I32, _I64, _I32, _VP, _VP, _VP], _INT),
+    "ebt_screen_exact": ([_VP, _I64, _I32, _VP, _INT, _I64, _VP, _I64, _VP, _I64, _VP], _INT),
     "ebt_cosine_topk_workspace": ([_I64, _I64, _I64, _I32, _I64, _INT], _SZ),
     "ebt_cosine_topk_plan": ([_I64, _I64, _I64, _I32, _I64, _INT, ctypes.POINTER(_I64),
                               ctypes.POINTER(_I64), ctypes.POINTER(_I64),

@@ -56,6 +56,18 @@ int mask_candidates(float*, const int64_t*, int64_t, int64_t, int64_t, const int
                     const int64_t*, const int64_t*, hipStream_t);
 int merge_topk(const double*, const int64_t*, int32_t, int64_t, int32_t, double*, int64_t*,
                hipStream_t);
+int screen_exact(const double*, int64_t, int32_t, const void*, int, int64_t, const double*, int64_t,
+                 float*, int64_t, hipStream_t);
+
+// EBT_FLAG_EXACT screening operands (the float64 catalog path), null for the MFMA screen
+struct ExactScreen {
+  const double* q64;
+  int32_t d;
+  const void* cat;
+  int dtype;
+  int64_t ld;
+  const double* gnorm;
+};
 
 // ------------------------------------------------------------------------------ timer ------
 struct Timer {
@@ -113,7 +125,7 @@ struct WsLayout {
   int segs;
   bool fused;
   size_t off_s, off_segv, off_segi, off_chv, off_chi, off_fv, off_fi, off_cv, off_ci, off_cnt,
-      off_thr, bytes;
+      off_thr, off_eps, bytes;
 };
 
 static size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -126,7 +138,7 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
   int64_t H = 256LL * kprime;
   H = H < 65536 ? 65536 : H;
   H = (H + 255) / 256 * 256;
-  L.fused = !(flags & EBT_FLAG_NO_FUSE) && n_rows >= 2 * H;
+  L.fused = !(flags & (EBT_FLAG_NO_FUSE | EBT_FLAG_EXACT)) && n_rows >= 2 * H;
   L.head = L.fused ? H : n_rows;
   if (L.fused) {
     int64_t expect = (int64_t)kprime * (n_rows - H) / H;
@@ -171,6 +183,8 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
     L.off_thr = o;
     o = align_up(o + (size_t)B_pad * 4);
   }
+  L.off_eps = o;
+  if (flags & EBT_FLAG_EXACT) o = align_up(o + (size_t)B_pad * 4);
   L.bytes = o;
   return L;
 }
@@ -182,7 +196,7 @@ static int head_topk(const WsLayout& L, char* ws, const void* qimg, const float*
                      int img_dtype, int32_t ld_img, int64_t r0, int64_t nrows, int32_t d_pad,
                      int64_t row_offset, const int64_t* excl_off, const int64_t* excl_rows,
                      int32_t kprime, float* dv_final, int64_t* di_final, int64_t ld_final,
-                     void* timer, hipStream_t st) {
+                     void* timer, hipStream_t st, const ExactScreen* ex = nullptr) {
   float* S = (float*)(ws + L.off_s);
   float* segv = (float*)(ws + L.off_segv);
   int64_t* segi = (int64_t*)(ws + L.off_segi);
@@ -195,8 +209,14 @@ static int head_topk(const WsLayout& L, char* ws, const void* qimg, const float*
     const int64_t nc = (r0 + nrows - c0) < L.chunk ? (r0 + nrows - c0) : L.chunk;
     {
       StageScope s(timer, EBT_STAGE_GEMM, st);
-      rc = screen_gemm(qimg, B_pad, (const char*)cimg + c0 * ld_img * 2, nc, d_pad, ld_img,
-                       img_dtype, qscale, cscale ? cscale + c0 : nullptr, S, L.ld_s, st);
+      if (ex) {
+        const int es = ex->dtype == EBT_F64 ? 8 : (ex->dtype == EBT_F32 ? 4 : 2);
+        rc = screen_exact(ex->q64, B, ex->d, (const char*)ex->cat + c0 * ex->ld * es, ex->dtype,
+                          ex->ld, ex->gnorm + c0, nc, S, L.ld_s, st);
+      } else {
+        rc = screen_gemm(qimg, B_pad, (const char*)cimg + c0 * ld_img * 2, nc, d_pad, ld_img,
+                         img_dtype, qscale, cscale ? cscale + c0 : nullptr, S, L.ld_s, st);
+      }
     }
     if (rc) return rc;
     if (excl_off) {
@@ -315,6 +335,13 @@ int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dt
                  eps, out_scores, out_rows, certified, (hipStream_t)stream, nullptr, 0);
 }
 
+int ebt_screen_exact(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
+                     int64_t ld, const double* gnorm64, int64_t n_rows, float* scores,
+                     int64_t ld_scores, void* stream) {
+  return screen_exact(q64, B, d, cat, dtype, ld, gnorm64, n_rows, scores, ld_scores,
+                      (hipStream_t)stream);
+}
+
 int ebt_merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, int32_t k,
                    double* out_scores, int64_t* out_rows, void* stream) {
   return merge_topk(scores, rows, R, B, k, out_scores, out_rows, (hipStream_t)stream);
@@ -351,7 +378,8 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
                     double* out_scores, int64_t* out_rows, int32_t* certified, void* timer,
                     void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (!q64 || !qimg || !qscale || !eps || !cat || !gnorm64 || !cimg || !workspace ||
+  const bool exact = flags & EBT_FLAG_EXACT;
+  if (!q64 || (!exact && (!qimg || !qscale || !eps || !cimg)) || !cat || !gnorm64 || !workspace ||
       !out_scores || !out_rows || !certified) {
     set_error("ebt_cosine_topk: null pointer");
     return EBT_EINVAL;
@@ -374,6 +402,23 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
   float* fv = (float*)(ws + L.off_fv);
   int64_t* fi = (int64_t*)(ws + L.off_fi);
   int rc;
+  if (exact) {  // float64 screen; its bound replaces the caller's eps
+    const ExactScreen ex{q64, d, cat, dtype, ld, gnorm64};
+    float* xeps = (float*)(ws + L.off_eps);
+    const float e = EBT_EXACT_EPS;
+    uint32_t bits;
+    memcpy(&bits, &e, 4);
+    rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)xeps, (int)bits, (size_t)B, st),
+                   "hipMemsetD32Async");
+    if (rc) return rc;
+    rc = head_topk(L, ws, nullptr, nullptr, B, B_pad, nullptr, nullptr, img_dtype, ld_img, 0,
+                   n_rows, d_pad, row_offset, excl_off, excl_rows, kprime, fv, fi, kprime, timer,
+                   st, &ex);
+    if (rc) return rc;
+    StageScope s(timer, EBT_STAGE_RESCORE, st);
+    return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, fv, fi, kprime, k, n_rows, xeps,
+                   out_scores, out_rows, certified, st, nullptr, 0);
+  }
   if (!L.fused) {
     rc = head_topk(L, ws, qimg, qscale, B, B_pad, cimg, cscale, img_dtype, ld_img, 0, n_rows,
                    d_pad, row_offset, excl_off, excl_rows, kprime, fv, fi, kprime, timer, st);

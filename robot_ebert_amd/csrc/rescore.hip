@@ -242,4 +242,96 @@ int merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, 
   return launch_check("merge_topk_kernel");
 }
 
+// ---------------------------------------------------------------------------------------------
+// Exact screen (EBT_FLAG_EXACT): S[b][j] = (float)((q64_b . c_j) / gnorm64_j), the rescore's own
+// float64 arithmetic rounded once to f32, for every row of a chunk. This is the last-resort
+// screen for a query whose f16/bf16 screen cannot be certified even at k' = 4096 (a cluster of
+// more than k' rows within the f16 error bound of the k-th score): its only error is the f32
+// rounding (|score| <= 1, so <= 2^-25) plus float64 round-off, so EXACT_EPS certifies anything
+// short of true f32-level ties. Plain FMA tiling (64 queries x 64 rows per workgroup, 4 x 4 per
+// thread): it runs for a handful of queries, never on the hot path.
+// ---------------------------------------------------------------------------------------------
+constexpr int XT = 64, XK = 16;
+
+template <int DT>
+__global__ __launch_bounds__(256) void screen_exact_kernel(
+    const double* __restrict__ q64, int64_t B, int d, const void* __restrict__ cat, int64_t ld,
+    const double* __restrict__ gnorm, int64_t n_rows, float* __restrict__ S, int64_t ld_s) {
+  __shared__ double qs[XK][XT + 1], cs[XK][XT + 1];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int64_t r0 = (int64_t)blockIdx.x * XT, b0 = (int64_t)blockIdx.y * XT;
+  double acc[4][4] = {};
+  for (int k0 = 0; k0 < d; k0 += XK) {
+    for (int e = tid; e < XT * XK; e += 256) {
+      const int rr = e / XK, kk = e % XK;
+      const int64_t row = r0 + rr, qb = b0 + rr;
+      const bool kin = k0 + kk < d;
+      cs[kk][rr] = (kin && row < n_rows) ? load_as_f64<DT>(cat, row * ld + k0 + kk) : 0.0;
+      qs[kk][rr] = (kin && qb < B) ? q64[qb * d + k0 + kk] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < XK; ++kk) {
+      double a[4], c[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[i] = qs[kk][ty * 4 + i];
+        c[i] = cs[kk][tx * 4 + i];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_fma(a[i], c[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t qb = b0 + ty * 4 + i;
+    if (qb >= B) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t row = r0 + tx * 4 + j;
+      if (row < n_rows) {
+        const double v = acc[i][j] / gnorm[row];
+        S[qb * ld_s + row] = (v == v) ? (float)v : -__builtin_inff();
+      }
+    }
+  }
+}
+
+int screen_exact(const double* q64, int64_t B, int32_t d, const void* cat, int dtype, int64_t ld,
+                 const double* gnorm, int64_t n_rows, float* S, int64_t ld_s, hipStream_t st) {
+  if (!q64 || !cat || !gnorm || !S || B < 0 || d < 1 || ld < d || n_rows < 0 || ld_s < n_rows ||
+      dtype < 0 || dtype > 3) {
+    set_error("ebt_screen_exact: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (B == 0 || n_rows == 0) return EBT_OK;
+  if (ceil_div(B, XT) > 65535) {
+    set_error("ebt_screen_exact: batch too large");
+    return EBT_EINVAL;
+  }
+  dim3 grid((unsigned)ceil_div(n_rows, XT), (unsigned)ceil_div(B, XT)), block(256);
+  switch (dtype) {
+    case EBT_F32:
+      hipLaunchKernelGGL(screen_exact_kernel<EBT_F32>, grid, block, 0, st, q64, B, d, cat, ld,
+                         gnorm, n_rows, S, ld_s);
+      break;
+    case EBT_BF16:
+      hipLaunchKernelGGL(screen_exact_kernel<EBT_BF16>, grid, block, 0, st, q64, B, d, cat, ld,
+                         gnorm, n_rows, S, ld_s);
+      break;
+    case EBT_F16:
+      hipLaunchKernelGGL(screen_exact_kernel<EBT_F16>, grid, block, 0, st, q64, B, d, cat, ld,
+                         gnorm, n_rows, S, ld_s);
+      break;
+    default:
+      hipLaunchKernelGGL(screen_exact_kernel<EBT_F64>, grid, block, 0, st, q64, B, d, cat, ld,
+                         gnorm, n_rows, S, ld_s);
+      break;
+  }
+  return launch_check("screen_exact_kernel");
+}
+
 }  // namespace ebt

@@ -108,17 +108,32 @@ __device__ __forceinline__ void epilogue4(const EpiArgs& e, int64_t q, int64_t i
       }
     }
   } else {
+    // one vector load of the row scales and a cheap all-miss test first: the append path is
+    // taken for ~k'/H of the values, and keeping it cold keeps the accumulators in registers
+    float4 cs = make_float4(1.f, 1.f, 1.f, 1.f);
+    if (cscale) {
+      if (i0 + 3 < n_rows) {
+        cs = *(const float4*)(cscale + i0);
+      } else {
+        cs.x = i0 + 0 < n_rows ? cscale[i0 + 0] : 1.f;
+        cs.y = i0 + 1 < n_rows ? cscale[i0 + 1] : 1.f;
+        cs.z = i0 + 2 < n_rows ? cscale[i0 + 2] : 1.f;
+        cs.w = i0 + 3 < n_rows ? cscale[i0 + 3] : 1.f;
+      }
+    }
+    const float v[4] = {acc[0] * qs * cs.x, acc[1] * qs * cs.y, acc[2] * qs * cs.z,
+                        acc[3] * qs * cs.w};
+    const bool any = (v[0] >= th && i0 < n_rows) || (v[1] >= th && i0 + 1 < n_rows) ||
+                     (v[2] >= th && i0 + 2 < n_rows) || (v[3] >= th && i0 + 3 < n_rows);
+    if (__builtin_expect(any, 0)) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t i = i0 + r;
-      if (i < n_rows) {
-        const float cs = cscale ? cscale[i] : 1.f;
-        const float v = acc[r] * qs * cs;
-        if (v >= th) {
+      for (int r = 0; r < 4; ++r) {
+        const int64_t i = i0 + r;
+        if (i < n_rows && v[r] >= th) {
           const int p = atomicAdd(e.cnt + q, 1);
           if (p < e.cap) {
             const int64_t o = q * e.ld_cand + e.cand_off + p;
-            e.cand_v[o] = v;
+            e.cand_v[o] = v[r];
             e.cand_i[o] = e.idx_base + i;
           }
         }
@@ -645,8 +660,6 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
   const int64_t qt = w / gc;
   const int64_t c0 = ct * 256;
   const int64_t q0 = qt * 256;
-  const int64_t last_c = n_rows - 1;
-  const int64_t last_q = (int64_t)n_qtiles * 256 - 1;
 
   const int wa = wave >> 2;
   const int wb = wave & 3;
@@ -806,6 +819,229 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
   store_quadrant(acc3, 1, 0);
 }
 
+// =============================================================================================
+// Persistent pipelined quadrant phases (pq, the default): qp2's tile, LDS image and phase
+// schedule, but one workgroup per CU walks a sequence of output tiles and the half-tile stream
+// runs straight across tile boundaries -- the next tile's first K-tiles are already in flight
+// (and its first fragments already read) while the current tile's last phases and epilogue run.
+// At d = 1536 the per-tile prologue latency and epilogue of a one-tile-per-workgroup launch
+// cost ~22 % (measured: 1050 TF at K = 1536 vs 1305 TF at K = 12288).
+// Tile order: virtual block vb = iter * G + wg goes through the same XCD-bijective remap and
+// 4-catalog-tile grouping as qp2 (G % 8 == 0, so vb and wg share the XCD label).
+// =============================================================================================
+// Tile origins are forced uniform (readfirstlane) and the buffer descriptors are rebuilt from
+// them at each issue: a descriptor carried through the tile loop in a struct ended up in VGPRs,
+// which turns every buffer_load ... lds into a readfirstlane waterfall loop.
+struct PqTile {
+  int c0, q0;
+};
+
+__device__ __forceinline__ PqTile pq_tile(int64_t vb, int64_t nwg, int n_qtiles, int64_t n_ctiles) {
+  PqTile T;
+  const int64_t vbc = vb < nwg ? vb : nwg - 1;  // past the end: a valid tile, never stored
+  const int64_t xcd = vbc & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int64_t L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (vbc >> 3);
+  const int64_t per_group = (int64_t)QP_GROUP_C * n_qtiles;
+  const int64_t g = L / per_group, w = L - g * per_group;
+  const int64_t gc_rem = n_ctiles - g * QP_GROUP_C;
+  const int64_t gc = gc_rem < QP_GROUP_C ? gc_rem : QP_GROUP_C;
+  T.c0 = __builtin_amdgcn_readfirstlane((int)((g * QP_GROUP_C + w % gc) * 256));
+  T.q0 = __builtin_amdgcn_readfirstlane((int)((w / gc) * 256));
+  return T;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const uint16_t* base, int64_t off,
+                                                               int64_t bytes) {
+  const uint64_t a = (uint64_t)(base + off);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
+}
+
+template <bool BF16, bool FILTER>
+__global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_pq_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ C, int64_t ld_img,
+    int64_t n_rows, int n_qtiles, int64_t n_ctiles, int nk,
+    const float* __restrict__ qscale, const float* __restrict__ cscale, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t G = gridDim.x, wg = blockIdx.x;
+  const int64_t nwg = (int64_t)n_qtiles * n_ctiles;
+  const int my_tiles = (int)((nwg - wg + G - 1) / G);
+  const int total_kt = my_tiles * nk;
+  const int total = 4 * total_kt;
+
+  const int wa = wave >> 2;
+  const int wb = wave & 3;
+  const int fr = lane & 15;
+  // row r = base + 16*i + fr has (r & 7) == (fr & 7): one swizzled column per k-step, rows are
+  // immediate offsets (i * 2048 bytes)
+  int a_off0[2], b_off0[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int c = ks * 4 + (lane >> 4);
+    a_off0[ks] = (wa * 64 + fr) * 128 + ((c ^ (fr & 7)) << 4);
+    b_off0[ks] = (wb * 32 + fr) * 128 + ((c ^ (fr & 7)) << 4);
+  }
+  const int64_t row_bytes = ld_img * 2;
+  const int voff = (int)((wave * 16 + (lane >> 3)) * row_bytes) + (((lane & 7) ^ (lane >> 3)) << 4);
+  const int piece_step = (int)(8 * row_bytes);
+  const int half_step = (int)(128 * row_bytes);
+
+  int iter = 0;  // output tile being computed
+  PqTile cur = pq_tile(wg, nwg, n_qtiles, n_ctiles);
+  PqTile nxt = pq_tile(wg + G, nwg, n_qtiles, n_ctiles);
+
+  // sequence index idx = 4 * (global K-tile) + type; a global K-tile kt belongs to output tile
+  // kt / nk, which is `iter` or `iter + 1` (the stream runs at most 2 K-tiles ahead, nk >= 2).
+  auto issue = [&](int idx) __attribute__((always_inline)) {
+    if (idx < total) {
+      const int tk = idx >> 2, type = idx & 3;
+      const bool next = tk >= (iter + 1) * nk;
+      const int t = tk - (next ? iter + 1 : iter) * nk;
+      char* dst = smem + (tk & 1) * QP_BUF + p_half_off(type) + wave * 2048;
+      const int soff = t * 128 + ((type == P_A1 || type == P_B1) ? half_step : 0);
+      const bool is_c = type == P_A0 || type == P_A1;
+      const int tc0 = next ? nxt.c0 : cur.c0, tq0 = next ? nxt.q0 : cur.q0;
+      int64_t c_rem = ((int64_t)n_rows - tc0) * row_bytes;
+      c_rem = c_rem < 256 * row_bytes ? c_rem : 256 * row_bytes;
+      const __amdgpu_buffer_rsrc_t rs = is_c ? uniform_rsrc(C, (int64_t)tc0 * ld_img, c_rem)
+                                             : uniform_rsrc(Q, (int64_t)tq0 * ld_img,
+                                                            256 * row_bytes);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)dst, 16, voff, soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + 1024), 16, voff,
+                                               soff + piece_step, 0, 0);
+    }
+  };
+  auto wait_for = [&](int needed, int last_issued) __attribute__((always_inline)) {
+    const int last = last_issued < total - 1 ? last_issued : total - 1;
+    const int n = last - needed;
+    wait_vm_halves(n > 0 ? n : 0);
+  };
+  auto read_a = [&](u16x8_t (&a)[4][2], const char* half) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i][ks] = *(const u16x8_t*)(half + a_off0[ks] + i * 2048);
+  };
+  auto read_b = [&](u16x8_t (&b)[2][2], const char* half) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j][ks] = *(const u16x8_t*)(half + b_off0[ks] + j * 2048);
+  };
+
+  f32x4_t acc0[4][2], acc1[4][2], acc2[4][2], acc3[4][2];
+  auto zero_acc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        acc0[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        acc1[i][j] = acc0[i][j];
+        acc2[i][j] = acc0[i][j];
+        acc3[i][j] = acc0[i][j];
+      }
+  };
+  auto store_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t q = cur.q0 + bh * 128 + wb * 32 + j * 16 + fr;
+      const float qs = qscale[q];
+      const float th = FILTER ? e.thr[q] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t i0 = cur.c0 + ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
+        epilogue4<FILTER>(e, q, i0, n_rows, acc[i][j], qs, th, cscale);
+      }
+    }
+  };
+  // end of an output tile: write it, advance the tile descriptors
+  auto finish_tile = [&]() __attribute__((always_inline)) {
+    store_quadrant(acc0, 0, 0);
+    store_quadrant(acc1, 0, 1);
+    store_quadrant(acc2, 1, 1);
+    store_quadrant(acc3, 1, 0);
+    zero_acc();
+    ++iter;
+    cur = nxt;
+    nxt = pq_tile(wg + (int64_t)(iter + 1) * G, nwg, n_qtiles, n_ctiles);
+  };
+
+  zero_acc();
+  u16x8_t fa0[4][2], fa1[4][2], fbx[2][2], fby[2][2];
+#pragma unroll
+  for (int idx = 0; idx < 7; ++idx) issue(idx);
+  wait_for(1, 6);
+  qp_barrier();
+  read_a(fa0, smem + p_half_off(P_A0));
+  read_b(fbx, smem + p_half_off(P_B0));
+  wait_for(2, 6);
+
+  // one K-tile (global index KT) of four phases, exactly as qp2
+#define PQ_KTILE(KT, s0, s1, MORE)                                                               \
+  {                                                                                             \
+    const int t_ = (KT);                                                                        \
+    const char* buf = smem + (t_ & 1) * QP_BUF;                                                 \
+    const char* nbuf = smem + ((t_ + 1) & 1) * QP_BUF;                                          \
+    qp_barrier();                                                                               \
+    issue(4 * t_ + 7);                                                                          \
+    qp2_mma<BF16>(acc0, fa0, s0);                                                               \
+    read_b(s1, buf + p_half_off(P_B1));                                                         \
+    _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_) {                                          \
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                        \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                        \
+    }                                                                                           \
+    wait_for(4 * t_ + 3, 4 * t_ + 7);                                                           \
+    qp_barrier();                                                                               \
+    issue(4 * t_ + 8);                                                                          \
+    qp2_mma<BF16>(acc1, fa0, s1);                                                               \
+    read_a(fa1, buf + p_half_off(P_A1));                                                        \
+    _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                          \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                        \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                        \
+    }                                                                                           \
+    qp_barrier();                                                                               \
+    issue(4 * t_ + 9);                                                                          \
+    qp2_mma<BF16>(acc2, fa1, s1);                                                               \
+    wait_for(4 * t_ + 5, 4 * t_ + 9);                                                           \
+    qp_barrier();                                                                               \
+    issue(4 * t_ + 10);                                                                         \
+    qp2_mma<BF16>(acc3, fa1, s0);                                                               \
+    if (MORE) {                                                                                 \
+      read_a(fa0, nbuf + p_half_off(P_A0));                                                     \
+      read_b(s1, nbuf + p_half_off(P_B0));                                                      \
+    }                                                                                           \
+    _Pragma("unroll") for (int i_ = 0; i_ < 12; ++i_) {                                         \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                        \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                        \
+    }                                                                                           \
+    wait_for(4 * t_ + 6, 4 * t_ + 10);                                                          \
+  }
+
+  // nk is even (host guarantees), so every output tile starts with B0 in the X set
+  for (int it = 0; it < my_tiles; ++it) {
+    for (int tt = 0; tt < nk; tt += 2) {
+      const int kt = it * nk + tt;
+      PQ_KTILE(kt, fbx, fby, true);
+      PQ_KTILE(kt + 1, fby, fbx, tt + 2 < nk);
+    }
+    // the next tile's first fragments are read after the epilogue, not during the last phase:
+    // keeps them out of the registers the epilogue needs (its A0/B0 halves have landed and
+    // passed the last phase's barrier; nothing is issued until the next barrier)
+    finish_tile();
+    if (it + 1 < my_tiles) {
+      const char* nb = smem + ((it + 1) * nk & 1) * QP_BUF;
+      read_a(fa0, nb + p_half_off(P_A0));
+      read_b(fbx, nb + p_half_off(P_B0));
+    }
+  }
+#undef PQ_KTILE
+}
+
 template <bool FILTER>
 static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
                        int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
@@ -824,7 +1060,23 @@ static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_
   }
   const uint16_t* Q = (const uint16_t*)qimg;
   const uint16_t* C = (const uint16_t*)cimg;
-  if (big && force_tile == 0) {  // default: pipelined quadrant-phase kernel
+  if (big && force_tile == 3 && d_pad % 128 == 0) {  // persistent variant (measured slower)
+    static const int n_cu = [] {
+      int dev = 0, cus = 256;
+      if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      return cus > 0 ? cus : 256;
+    }();
+    const int64_t G = nwg < n_cu ? nwg : n_cu;  // one 128 KiB-LDS workgroup per CU
+    dim3 grid((unsigned)G), block(QP_THREADS);
+    auto k = img_dtype == EBT_BF16 ? screen_gemm_pq_kernel<true, FILTER>
+                                   : screen_gemm_pq_kernel<false, FILTER>;
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, QP_LDS);
+    hipLaunchKernelGGL(k, grid, block, QP_LDS, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
+                       n_ctiles, d_pad / 64, qscale, cscale, e);
+    return launch_check("screen_gemm_pq_kernel");
+  }
+  if (big && (force_tile == 0 || force_tile == 2)) {  // pipelined quadrant phases, 1 tile/WG
     dim3 grid((unsigned)nwg), block(QP_THREADS);
     static const int var = [] {
       const char* v = getenv("EBT_GEMM_VAR");

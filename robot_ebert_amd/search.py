@@ -254,10 +254,19 @@ def score_topk(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
                                       timer, flags=_lib.EBT_FLAG_NO_FUSE)
             s[over], r[over], cert[over] = s2, r2, c2
             continue
-        if kp >= min(n_cap, KPRIME_MAX):
+        widen = kp < min(n_cap, KPRIME_MAX)
+        if not widen and flags & _lib.EBT_FLAG_EXACT:
             raise EbertError(f"{bad.numel()} queries could not be certified at k'={kp} "
-                             "(a tie cluster wider than k' at the k-th score)")
-        kp = min(kp * 4, n_cap, KPRIME_MAX)
+                             "(more than k' rows tie with the k-th score at f32 precision)")
+        if widen:
+            kp = min(kp * 4, n_cap, KPRIME_MAX)
+        else:
+            # the f16/bf16 screen's error bound spans more than k' = 4096 rows around the
+            # k-th score: screen these queries again in float64 (EBT_FLAG_EXACT), from the
+            # default k' up
+            flags = _lib.EBT_FLAG_EXACT
+            kp = max(_round_up(k_eff, 4), min(_round_up(default_kprime(catalog, k_eff), 4),
+                                              n_cap, KPRIME_MAX))
         sub_ex = csr_subset(exclude[0], exclude[1], bad) if exclude is not None else None
         s2, r2, c2 = run_pipeline(catalog, qb.subset(bad), k_eff, kp, sub_ex, chunk_rows, timer,
                                   flags=flags)

@@ -92,6 +92,46 @@ def test_screen_gemm_vs_torch_fp32(cuda_device, img, shape):
     torch.testing.assert_close(S2[:m, :N], c2.float().T[:m], rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("dt", ["f32", "f64", "bf16"])
+def test_screen_exact_vs_oracle(cuda_device, dt):
+    """ebt_screen_exact: float64 cosine rounded once to f32, against the oracle's float64 cosine
+    (f32 rounding of |s| <= 1 is <= 2^-25; ragged B/N/d exercise the tile edges)."""
+    ebt, L = _ebt()
+    B, N, d = 70, 1333, 77
+    c = gaussian(21, N, d, dt)
+    c[5] = 0.0
+    qv = gaussian(22, B, d, "f64")
+    ct = _t(c, dt, cuda_device)
+    g = torch.empty(N, dtype=torch.float64, device=cuda_device)
+    L.call("ebt_row_norms", L.ptr(ct), L.DTYPE_CODE[ct.dtype], N, d, d, L.ptr(g), None,
+           L.stream_of(cuda_device))
+    q64 = torch.from_numpy(R.normalize_rows(qv)).to(cuda_device)
+    ld_s = N + 3
+    S = torch.full((B, ld_s), float("nan"), device=cuda_device)
+    L.call("ebt_screen_exact", L.ptr(q64), B, d, L.ptr(ct), L.DTYPE_CODE[ct.dtype], d, L.ptr(g), N,
+           L.ptr(S), ld_s, L.stream_of(cuda_device))
+    ref = R.cosine_similarity(qv, c.astype(np.float64))
+    got = S[:, :N].double().cpu().numpy()
+    np.testing.assert_allclose(got, ref, rtol=0, atol=2.0 ** -24)
+    assert torch.isnan(S[:, N:]).all()
+
+
+def test_exact_screen_fallback_near_ties(cuda_device):
+    """A cluster of 10000 rows within ~1e-4 of the top score: the f16 screen cannot certify it
+    even at k' = 4096, so the query is screened again in float64 -- and must match the oracle."""
+    ebt, L = _ebt()
+    n, d, k = 60_000, 64, 50
+    rng = np.random.default_rng(4)
+    q = rng.standard_normal((1, d))
+    c = rng.standard_normal((n, d))
+    idx = rng.choice(n, 10_000, replace=False)
+    c[idx] = q[0] + rng.standard_normal((idx.size, d)) * 1e-2
+    cat = ebt.Catalog(_t(c, "f64", cuda_device))
+    s, r = ebt.score_topk(cat, k, queries=_t(q, "f64", cuda_device))
+    s_ref, r_ref = R.cosine_topk(q, c, k)
+    assert_topk_equal(s, r, s_ref, r_ref)
+
+
 def _select_ref(v, k):
     n = v.shape[0]
     keys = np.where(np.isnan(v) | (v == -np.inf), -np.inf, v)

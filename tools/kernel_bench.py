@@ -80,12 +80,14 @@ def main():
     ap.add_argument("--gemm", action="store_true")
     ap.add_argument("--select", action="store_true")
     ap.add_argument("--one", action="store_true", help="single C3-chunk GEMM config (profiling)")
+    ap.add_argument("--shape", default="4096,262144,1536", help="B,N,d for --one")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     L.load()
     res = []
     if args.one:
-        print(json.dumps(bench_gemm(dev, 4096, 262144, 1536, torch.float16)), flush=True)
+        B, N, d = (int(x) for x in args.shape.split(","))
+        print(json.dumps(bench_gemm(dev, B, N, d, torch.float16)), flush=True)
         return
     if args.gemm or not args.select:
         for (B, N, d, dt) in [(4096, 262144, 1536, torch.float16), (4096, 262144, 1536, torch.bfloat16),
