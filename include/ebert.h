@@ -181,11 +181,13 @@ size_t ebt_cosine_topk_workspace(int64_t B, int64_t B_pad, int64_t n_rows, int32
  *   rescore.
  *   fused (default when n_rows >= 2*H, H = max(65536, 256*kprime)): the head rows [0, H) go
  *   through the unfused path; the k'-th best head score of each query is a lower bound of its
- *   global k'-th best, and the GEMM over the tail rows [H, n) appends only scores >= that bound
- *   to a per-query candidate list (epilogue filter: no score matrix in HBM); exclusions are
- *   removed from the list (excl_rows must be sorted ascending per query), the k' best of head +
- *   tail are selected and rescored. certified[b] = -1 reports a candidate-list overflow (rerun
- *   the query with EBT_FLAG_NO_FUSE).
+ *   global k'-th best. The tail rows [H, n) are screened in doubling segments (each as large as
+ *   all rows before it): the GEMM appends only scores >= the query's current bound to its
+ *   candidate list (epilogue filter: no score matrix in HBM), exclusions are removed from the
+ *   list (excl_rows must be sorted ascending per query), the k' best are kept and the bound is
+ *   raised to their k'-th score before the next segment -- about k' appends per query per
+ *   segment. The final k' are rescored. certified[b] = -1 reports a segment whose appends
+ *   exceeded the capacity (rerun the query with EBT_FLAG_NO_FUSE).
  * Inputs: the query batch prepared by ebt_query_* (q64, qimg, qscale, eps; B real rows, B_pad
  * image rows), the catalog (cat/dtype/ld with gnorm64; its screening image cimg with cscale or
  * NULL, ld_img, d_pad), exclusions as CSR of GLOBAL rows (NULL = none), k <= kprime.

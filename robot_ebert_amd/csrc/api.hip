@@ -51,7 +51,8 @@ int screen_gemm_filter(const void*, int64_t, const void*, int64_t, int32_t, int3
                        int64_t, int, int64_t, hipStream_t);
 int select_topk_counted(const float*, const int64_t*, int64_t, int64_t, int64_t, const int*, int,
                         int32_t, float*, int64_t*, int64_t, hipStream_t);
-int kth_threshold(const float*, int64_t, int64_t, int64_t, int, float*, hipStream_t);
+int kth_threshold(const float*, int64_t, int64_t, int64_t, int, float*, const int*, int*,
+                  hipStream_t);
 int mask_candidates(float*, const int64_t*, int64_t, int64_t, int64_t, const int*, int, int64_t,
                     const int64_t*, const int64_t*, hipStream_t);
 int merge_topk(const double*, const int64_t*, int32_t, int64_t, int32_t, double*, int64_t*,
@@ -125,7 +126,7 @@ struct WsLayout {
   int segs;
   bool fused;
   size_t off_s, off_segv, off_segi, off_chv, off_chi, off_fv, off_fi, off_cv, off_ci, off_cnt,
-      off_thr, off_eps, bytes;
+      off_thr, off_ovf, off_eps, bytes;
 };
 
 static size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -141,9 +142,9 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
   L.fused = !(flags & (EBT_FLAG_NO_FUSE | EBT_FLAG_EXACT)) && n_rows >= 2 * H;
   L.head = L.fused ? H : n_rows;
   if (L.fused) {
-    int64_t expect = (int64_t)kprime * (n_rows - H) / H;
-    int64_t cap = 4 * expect + 2048;
-    cap = cap > (1LL << 22) ? (1LL << 22) : cap;
+    // the tail is screened in doubling segments (each as large as all rows before it), so a
+    // segment appends ~k' candidates per query whatever n is
+    int64_t cap = 4 * (int64_t)kprime + 2048;
     L.cap = (cap + 255) / 256 * 256;
     L.ld_cand = (kprime + L.cap + 3) / 4 * 4;
   }
@@ -181,6 +182,8 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
     L.off_cnt = o;
     o = align_up(o + (size_t)B_pad * 4);
     L.off_thr = o;
+    o = align_up(o + (size_t)B_pad * 4);
+    L.off_ovf = o;
     o = align_up(o + (size_t)B_pad * 4);
   }
   L.off_eps = o;
@@ -436,35 +439,57 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
                  row_offset, excl_off, excl_rows, kprime, cv, ci, L.ld_cand, timer, st);
   if (rc) return rc;
   // 2. per-query threshold = the head's k'-th best approx score
-  rc = kth_threshold(cv, L.ld_cand, B, B_pad, kprime, thr, st);
+  int* ovf = (int*)(ws + L.off_ovf);
+  rc = hip_check(hipMemsetAsync(ovf, 0, (size_t)B_pad * 4, st), "hipMemsetAsync");
   if (rc) return rc;
-  rc = hip_check(hipMemsetAsync(cnt, 0, (size_t)B_pad * 4, st), "hipMemsetAsync");
+  rc = kth_threshold(cv, L.ld_cand, B, B_pad, kprime, thr, nullptr, nullptr, st);
   if (rc) return rc;
-  // 3. tail rows [H, n): GEMM with the threshold filter in the epilogue
-  {
-    StageScope s(timer, EBT_STAGE_GEMM_FILTER, st);
-    rc = screen_gemm_filter(qimg, B_pad, (const char*)cimg + L.head * ld_img * 2,
-                            n_rows - L.head, d_pad, ld_img, img_dtype, qscale,
-                            cscale ? cscale + L.head : nullptr, thr, cnt, cv, ci, L.ld_cand,
-                            kprime, (int)L.cap, L.head, st);
-  }
-  if (rc) return rc;
-  // 4. exclusions among the appended candidates, then the k' best of head + tail
-  if (excl_off) {
-    StageScope s(timer, EBT_STAGE_MASK, st);
-    rc = mask_candidates(cv, ci, L.ld_cand, kprime, B, cnt, (int)L.cap, row_offset, excl_off,
-                         excl_rows, st);
+  // 3. tail rows [H, n) in doubling segments: GEMM with the threshold filter in the epilogue,
+  //    exclusions dropped from the appended candidates, the k' best of list + appended kept,
+  //    and the threshold raised to the new k'-th best before the next segment
+  int64_t r0 = L.head;
+  while (r0 < n_rows) {
+    int64_t seg = n_rows - r0 < r0 ? n_rows - r0 : r0;
+    if (n_rows - (r0 + seg) < seg / 2) seg = n_rows - r0;  // no small last segment
+    const bool last = r0 + seg >= n_rows;
+    rc = hip_check(hipMemsetAsync(cnt, 0, (size_t)B_pad * 4, st), "hipMemsetAsync");
     if (rc) return rc;
+    {
+      StageScope s(timer, EBT_STAGE_GEMM_FILTER, st);
+      rc = screen_gemm_filter(qimg, B_pad, (const char*)cimg + r0 * ld_img * 2, seg, d_pad,
+                              ld_img, img_dtype, qscale, cscale ? cscale + r0 : nullptr, thr,
+                              cnt, cv, ci, L.ld_cand, kprime, (int)L.cap, r0, st);
+    }
+    if (rc) return rc;
+    if (excl_off) {
+      StageScope s(timer, EBT_STAGE_MASK, st);
+      rc = mask_candidates(cv, ci, L.ld_cand, kprime, B, cnt, (int)L.cap, row_offset, excl_off,
+                           excl_rows, st);
+      if (rc) return rc;
+    }
+    {
+      StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
+      rc = select_topk_counted(cv, ci, L.ld_cand, B, kprime, cnt, (int)L.cap, kprime, fv, fi,
+                               kprime, st);
+      if (rc) return rc;
+      if (!last) {  // the list so far back into the candidate rows' first k' slots
+        rc = hip_check(hipMemcpy2DAsync(cv, (size_t)L.ld_cand * 4, fv, (size_t)kprime * 4,
+                                        (size_t)kprime * 4, (size_t)B, hipMemcpyDeviceToDevice,
+                                        st), "hipMemcpy2DAsync");
+        if (!rc)
+          rc = hip_check(hipMemcpy2DAsync(ci, (size_t)L.ld_cand * 8, fi, (size_t)kprime * 8,
+                                          (size_t)kprime * 8, (size_t)B,
+                                          hipMemcpyDeviceToDevice, st), "hipMemcpy2DAsync");
+      }
+      if (!rc)
+        rc = kth_threshold(cv, L.ld_cand, B, B_pad, kprime, last ? nullptr : thr, cnt, ovf, st);
+    }
+    if (rc) return rc;
+    r0 += seg;
   }
-  {
-    StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
-    rc = select_topk_counted(cv, ci, L.ld_cand, B, kprime, cnt, (int)L.cap, kprime, fv, fi,
-                             kprime, st);
-  }
-  if (rc) return rc;
   StageScope s(timer, EBT_STAGE_RESCORE, st);
   return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, fv, fi, kprime, k, n_rows, eps,
-                 out_scores, out_rows, certified, st, cnt, (int)L.cap);
+                 out_scores, out_rows, certified, st, ovf, (int)L.cap);
 }
 
 void* ebt_timer_create(void) { return new (std::nothrow) Timer(); }

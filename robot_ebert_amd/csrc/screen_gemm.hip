@@ -7,17 +7,19 @@
 //
 // Shape: "NT" GEMM -- both operands are row-major with k contiguous (catalog [N][d_pad],
 // queries [B_pad][d_pad]), so both MFMA fragments are contiguous 16-byte LDS reads.
-// Tile: 128 catalog rows x 128 queries x 64 k per stage, 256 threads = 4 waves (2 x 2), each
-// wave 64 x 64 = 4 x 4 tiles of v_mfma_f32_16x16x32_{f16,bf16}. The catalog tile is the MFMA A
-// operand so each lane ends up owning 4 CONSECUTIVE catalog rows of one query: the epilogue
-// stores one float4 per accumulator into the query's score row.
+// Two kernels: the 256 x 256 "quadrant phase" kernel for batches padded to 256 (below), and a
+// 128 x 128 one (128 catalog rows x 128 queries x 64 k per stage, 4 waves of 64 x 64) for
+// B_pad = 128. Both use v_mfma_f32_16x16x32_{f16,bf16} with the catalog tile as the MFMA A
+// operand, so each lane ends up owning 4 CONSECUTIVE catalog rows of one query: the epilogue
+// stores one float4 per accumulator into the query's score row (or, in the fused screen, appends
+// the values >= the query's threshold to its candidate list).
 // Staging: global_load_lds_dwordx4 (16 B/lane, 1 KiB per wave-instruction = 8 rows x 128 B)
 // into a double-buffered 64 KiB LDS ring; the XOR swizzle slot = chunk ^ (row & 7) is applied to
 // the per-lane SOURCE address (LDS-DMA writes lane-linearly), and the same XOR on the read side
 // makes every ds_read_b128 lane group conflict-free.
 // Block order: XCD-bijective remap (blocks sharing an XCD get a contiguous logical range), then
-// groups of 8 catalog tiles walked query-tile-major, so a catalog tile is fetched from HBM once
-// per XCD and re-read from L2 by the 32 query tiles that use it.
+// groups of 8 (128-kernel) / 4 (256-kernel) catalog tiles walked query-tile-major, so a catalog
+// tile is fetched from HBM about once per XCD and re-read from L2 by the query tiles that use it.
 #include <cstdlib>
 
 #include "common.h"
@@ -233,146 +235,6 @@ __global__ __launch_bounds__(GTHREADS, 2) void screen_gemm_kernel(
 }
 
 // =============================================================================================
-// 256 x 256 tile, 8 waves, 4-slot LDS ring of 32-deep k slices (the large-batch kernel).
-//
-// Wave (wm, wn) in a 2 x 4 grid owns catalog rows wm*128..+127 and queries wn*64..+63 of the
-// tile: 8 x 4 tiles of v_mfma_f32_16x16x32 (128 accumulator VGPRs). A k slice is 256 rows x 32 k
-// of each operand (16 KiB + 16 KiB); slot t&3 of the ring holds slice t. Per slice a wave issues
-// 4 global_load_lds_dwordx4 (2 per operand, 16 rows x 64 B each) for slice t+3, reads 12
-// fragments (ds_read_b128) of slice t and runs 32 MFMAs. One s_barrier per slice; the counted
-// `s_waitcnt vmcnt(8)` before it leaves slices t+1 and t+2 in flight, so ~64 KiB per CU is
-// always being fetched while the MFMAs run.
-// LDS image of a slice operand: row-major 64-byte rows with the 16-byte chunk c stored at slot
-// c ^ (((row >> 3) & 1) << 1); for the 16x16x32 operand map (lane l reads row l&15, chunk l>>4)
-// this puts the 16 lanes of every ds_read_b128 lane group on 16 distinct bank slots.
-// =============================================================================================
-constexpr int HBM_ = 256;             // catalog rows per block
-constexpr int HBN_ = 256;             // queries per block
-constexpr int HBK_ = 32;              // k per slice
-constexpr int HTHREADS = 512;
-constexpr int HOP_BYTES = 256 * 64;   // one operand slice: 16 KiB
-constexpr int HSLOT_BYTES = 2 * HOP_BYTES;
-constexpr int HLDS_BYTES = 4 * HSLOT_BYTES;  // 128 KiB
-constexpr int HGROUP_C = 2;
-
-__device__ __forceinline__ void stage_slice(const uint16_t* __restrict__ X, int64_t ldx,
-                                            int64_t row0, int64_t last_row, int k0,
-                                            char* op_lds, int wave, int lane) {
-  const int sub = lane >> 2;   // row inside the 16-row piece
-  const int slot = lane & 3;   // 16-byte slot inside the 64-byte LDS row
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int piece = wave * 2 + j;  // 16 pieces of 16 rows = 256 rows
-    const int rr = piece * 16 + sub;
-    int64_t grow = row0 + rr;
-    grow = grow > last_row ? last_row : grow;
-    const int chunk = slot ^ (((rr >> 3) & 1) << 1);
-    const uint16_t* src = X + grow * ldx + k0 + chunk * 8;
-    __builtin_amdgcn_global_load_lds((gbl_cvoid*)src, (lds_void*)(op_lds + piece * 1024), 16, 0,
-                                     0);
-  }
-}
-
-template <bool BF16, bool FILTER>
-__global__ __launch_bounds__(HTHREADS, 2) void screen_gemm256_kernel(
-    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ C, int64_t ld_img,
-    int64_t n_rows, int n_qtiles, int64_t n_ctiles, int nslices,
-    const float* __restrict__ qscale, const float* __restrict__ cscale, EpiArgs e) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-
-  const int64_t nwg = (int64_t)n_qtiles * n_ctiles;
-  const int64_t bid = blockIdx.x;
-  const int64_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int64_t L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int64_t per_group = (int64_t)HGROUP_C * n_qtiles;
-  const int64_t g = L / per_group, w = L - g * per_group;
-  const int64_t gc_rem = n_ctiles - g * HGROUP_C;
-  const int64_t gc = gc_rem < HGROUP_C ? gc_rem : HGROUP_C;
-  const int64_t ct = g * HGROUP_C + w % gc;
-  const int64_t qt = w / gc;
-  const int64_t c0 = ct * HBM_;
-  const int64_t q0 = qt * HBN_;
-
-  const int wm = wave >> 2;  // catalog half (128 rows)
-  const int wn = wave & 3;   // query quarter (64 queries)
-
-  f32x4_t acc[8][4];
-#pragma unroll
-  for (int a = 0; a < 8; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  // fragment byte offsets inside an operand slice (row tile base is a multiple of 16)
-  const int fr = lane & 15, fc = lane >> 4;
-  const int frag_off = fr * 64 + ((fc ^ (((fr >> 3) & 1) << 1)) << 4);
-  const int a_base = wm * 128 * 64 + frag_off;
-  const int b_base = HOP_BYTES + wn * 64 * 64 + frag_off;
-
-  const int64_t last_c = n_rows - 1;
-  const int64_t last_q = (int64_t)n_qtiles * HBN_ - 1;
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    if (t < nslices) {
-      char* sl = smem + t * HSLOT_BYTES;
-      stage_slice(C, ld_img, c0, last_c, t * HBK_, sl, wave, lane);
-      stage_slice(Q, ld_img, q0, last_q, t * HBK_, sl + HOP_BYTES, wave, lane);
-    }
-  }
-
-  for (int t = 0; t < nslices; ++t) {
-    // slice t landed for this wave: leave the later slices' loads in flight
-    const int ahead = nslices - 1 - t;
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + 3 < nslices) {
-      char* sl = smem + ((t + 3) & 3) * HSLOT_BYTES;
-      stage_slice(C, ld_img, c0, last_c, (t + 3) * HBK_, sl, wave, lane);
-      stage_slice(Q, ld_img, q0, last_q, (t + 3) * HBK_, sl + HOP_BYTES, wave, lane);
-    }
-    const char* sl = smem + (t & 3) * HSLOT_BYTES;
-    u16x8_t bf[4], af[8];
-    // all B fragments and the first half of A up front; the second half of A is read while
-    // the first 16 MFMAs run (hipcc would otherwise serialise read -> wait -> 4 MFMAs).
-#pragma unroll
-    for (int b = 0; b < 4; ++b) bf[b] = *(const u16x8_t*)(sl + b_base + b * 16 * 64);
-#pragma unroll
-    for (int a = 0; a < 4; ++a) af[a] = *(const u16x8_t*)(sl + a_base + a * 16 * 64);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int a = 4; a < 8; ++a) af[a] = *(const u16x8_t*)(sl + a_base + a * 16 * 64);
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] = mfma16<BF16>(af[a], bf[b], acc[a][b]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
-  }
-
-  // ---- epilogue ----
-#pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    const int64_t q = q0 + wn * 64 + b * 16 + (lane & 15);
-    const float qs = qscale[q];
-    const float th = FILTER ? e.thr[q] : 0.f;
-#pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      const int64_t i0 = c0 + wm * 128 + a * 16 + 4 * (lane >> 4);
-      epilogue4<FILTER>(e, q, i0, n_rows, acc[a][b], qs, th, cscale);
-    }
-  }
-}
-
-// =============================================================================================
 // 256 x 256 tile, 8 waves, BK = 64, "quadrant phases" (the default large-batch kernel).
 //
 // The LDS holds two K-tiles (buffer = tile & 1), each as four 16 KiB half-tiles: A0/A1 = catalog
@@ -382,48 +244,22 @@ __global__ __launch_bounds__(HTHREADS, 2) void screen_gemm256_kernel(
 // Q4 (A1,B0) -- with all 8 waves on the same quadrant (2 x 4 waves of 64 x 32 outputs: 16
 // MFMAs per wave per phase). So every half-tile dies early (A0 after Q2, B1 after Q3, A1 and B0
 // after Q4) and its region is restaged for tile t+2 one phase later: each phase issues exactly
-// one half-tile (2 global_load_lds_dwordx4 per lane), keeping 3-4 half-tiles in flight; the
-// counted `s_waitcnt vmcnt` in Q2 and Q4 retires only the half the NEXT phase reads. Phase:
-// ds_read this phase's fragments -> issue one half-tile -> [vmcnt] -> s_barrier -> 16 MFMAs at
-// s_setprio 1 -> s_barrier. Accumulators: 4 quadrants x 4 x 2 tiles (128 VGPRs).
+// one half-tile (2 LDS-DMA pieces per lane), keeping 3-4 half-tiles in flight.
+// Accumulators: 4 quadrants x 4 x 2 tiles (128 VGPRs).
 // =============================================================================================
 constexpr int QP_THREADS = 512;
 constexpr int QP_HALF = 128 * 128;            // 16 KiB: 128 rows x 64 k x 2 B
 constexpr int QP_BUF = 4 * QP_HALF;           // one K-tile
 constexpr int QP_LDS = 2 * QP_BUF;            // 128 KiB
 constexpr int QP_GROUP_C = 4;
-// half-tile order of the issue sequence: idx = 4*tile + type
-enum { H_A0 = 0, H_B1 = 1, H_B0 = 2, H_A1 = 3 };
-__device__ __forceinline__ constexpr int half_off(int type) {
-  return type == H_A0 ? 0 : type == H_A1 ? QP_HALF : type == H_B0 ? 2 * QP_HALF : 3 * QP_HALF;
-}
-
-// One wave stages 2 x 1 KiB pieces (16 rows x 128 B) of a 128-row half-tile.
-__device__ __forceinline__ void qp_stage(const uint16_t* __restrict__ X, int64_t ldx, int64_t row0,
-                                         int64_t last_row, int k0, char* half_lds, int wave,
-                                         int lane) {
-  const int slot = lane & 7;
-  const int sub = lane >> 3;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int piece = wave * 2 + j;
-    const int rr = piece * 8 + sub;
-    int64_t grow = row0 + rr;
-    grow = grow > last_row ? last_row : grow;
-    const int chunk = slot ^ sub;
-    const uint16_t* src = X + grow * ldx + k0 + chunk * 8;
-    __builtin_amdgcn_global_load_lds((gbl_cvoid*)src, (lds_void*)(half_lds + piece * 1024), 16, 0,
-                                     0);
-  }
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N == 0, "unsupported vmcnt");
 }
 // s_waitcnt with an immediate chosen at run time (near the last tiles fewer loads follow).
 __device__ __forceinline__ void wait_vm_halves(int halves_after) {
@@ -434,187 +270,21 @@ __device__ __forceinline__ void wait_vm_halves(int halves_after) {
   else wait_vm<0>();
 }
 
+// s_barrier is a no-memory intrinsic to LLVM: the empty asm with a memory clobber keeps LDS
+// reads from being hoisted above it at IR level; sched_barrier(0) does the same for the
+// machine scheduler.
 __device__ __forceinline__ void qp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-}
-
-template <bool BF16, bool FILTER>
-__global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp_kernel(
-    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ C, int64_t ld_img,
-    int64_t n_rows, int n_qtiles, int64_t n_ctiles, int ktiles,
-    const float* __restrict__ qscale, const float* __restrict__ cscale, EpiArgs e) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-
-  const int64_t nwg = (int64_t)n_qtiles * n_ctiles;
-  const int64_t bid = blockIdx.x;
-  const int64_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int64_t L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int64_t per_group = (int64_t)QP_GROUP_C * n_qtiles;
-  const int64_t g = L / per_group, w = L - g * per_group;
-  const int64_t gc_rem = n_ctiles - g * QP_GROUP_C;
-  const int64_t gc = gc_rem < QP_GROUP_C ? gc_rem : QP_GROUP_C;
-  const int64_t ct = g * QP_GROUP_C + w % gc;
-  const int64_t qt = w / gc;
-  const int64_t c0 = ct * 256;
-  const int64_t q0 = qt * 256;
-  const int64_t last_c = n_rows - 1;
-  const int64_t last_q = (int64_t)n_qtiles * 256 - 1;
-
-  const int wa = wave >> 2;  // 64-row slab of the quadrant's catalog half
-  const int wb = wave & 3;   // 32-query slab of the quadrant's query half
-  const int fr = lane & 15;
-  // fragment byte offsets inside a half-tile for k-step ks (0, 1): row r, chunk ks*4 + lane>>4
-  int a_off[4][2], b_off[2][2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const int c = ks * 4 + (lane >> 4);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = wa * 64 + i * 16 + fr;
-      a_off[i][ks] = r * 128 + ((c ^ (r & 7)) << 4);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r = wb * 32 + j * 16 + fr;
-      b_off[j][ks] = r * 128 + ((c ^ (r & 7)) << 4);
-    }
-  }
-
-  f32x4_t acc[4][4][2];  // [quadrant][i][j]
-#pragma unroll
-  for (int qd = 0; qd < 4; ++qd)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[qd][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int total = 4 * ktiles;
-  auto issue = [&](int idx) {
-    if (idx < total) {
-      const int tile = idx >> 2, type = idx & 3;
-      char* dst = smem + (tile & 1) * QP_BUF + half_off(type);
-      const int k0 = tile * 64;
-      if (type == H_A0) qp_stage(C, ld_img, c0, last_c, k0, dst, wave, lane);
-      else if (type == H_A1) qp_stage(C, ld_img, c0 + 128, last_c, k0, dst, wave, lane);
-      else if (type == H_B0) qp_stage(Q, ld_img, q0, last_q, k0, dst, wave, lane);
-      else qp_stage(Q, ld_img, q0 + 128, last_q, k0, dst, wave, lane);
-    }
-  };
-  auto halves_after = [&](int needed, int last_issued) {
-    const int last = last_issued < total - 1 ? last_issued : total - 1;
-    const int n = last - needed;
-    return n > 0 ? n : 0;
-  };
-
-  // prologue: tile 0 (idx 0..3) and A0/B1 of tile 1 (idx 4, 5); retire what Q1/Q2 of tile 0 read
-#pragma unroll
-  for (int idx = 0; idx < 6; ++idx) issue(idx);
-  wait_vm_halves(halves_after(2, 5));
-  qp_barrier();
-
-  u16x8_t af[4][2], bfr[2][2];
-  for (int t = 0; t < ktiles; ++t) {
-    const char* buf = smem + (t & 1) * QP_BUF;
-    // ---- Q1: (A0, B0); reads A0 + B0, issues B0(t+1) ----
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j][ks] = *(const u16x8_t*)(buf + 2 * QP_HALF + b_off[j][ks]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i][ks] = *(const u16x8_t*)(buf + a_off[i][ks]);
-    }
-    issue(4 * t + 6);
-    qp_barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[0][i][j] = mfma16<BF16>(af[i][ks], bfr[j][ks], acc[0][i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    qp_barrier();
-    // ---- Q2: (A0, B1); reads B1, issues A1(t+1), retires A1(t) for Q3 ----
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j][ks] = *(const u16x8_t*)(buf + 3 * QP_HALF + b_off[j][ks]);
-    issue(4 * t + 7);
-    wait_vm_halves(halves_after(4 * t + 3, 4 * t + 7));
-    qp_barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[1][i][j] = mfma16<BF16>(af[i][ks], bfr[j][ks], acc[1][i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    qp_barrier();
-    // ---- Q3: (A1, B1); reads A1, issues A0(t+2) into A0(t)'s dead region ----
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i][ks] = *(const u16x8_t*)(buf + QP_HALF + a_off[i][ks]);
-    issue(4 * t + 8);
-    qp_barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[2][i][j] = mfma16<BF16>(af[i][ks], bfr[j][ks], acc[2][i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    qp_barrier();
-    // ---- Q4: (A1, B0); reads B0, issues B1(t+2), retires B0(t+1) for Q1 of the next tile ----
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j][ks] = *(const u16x8_t*)(buf + 2 * QP_HALF + b_off[j][ks]);
-    issue(4 * t + 9);
-    wait_vm_halves(halves_after(4 * t + 6, 4 * t + 9));
-    qp_barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[3][i][j] = mfma16<BF16>(af[i][ks], bfr[j][ks], acc[3][i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    qp_barrier();
-  }
-
-  // ---- epilogue: quadrant (ah, bh): catalog half ah, query half bh ----
-#pragma unroll
-  for (int qd = 0; qd < 4; ++qd) {
-    const int ah = (qd == 0 || qd == 1) ? 0 : 1;
-    const int bh = (qd == 0 || qd == 3) ? 0 : 1;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t q = q0 + bh * 128 + wb * 32 + j * 16 + fr;
-      const float qs = qscale[q];
-      const float th = FILTER ? e.thr[q] : 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t i0 = c0 + ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
-        epilogue4<FILTER>(e, q, i0, n_rows, acc[qd][i][j], qs, th, cscale);
-      }
-    }
-  }
 }
 
 // =============================================================================================
-// Pipelined quadrant phases (qp2): the same 256 x 256 x 64 tiling, LDS image and quadrant order
-// as qp, but ONE barrier per phase and the fragments of the NEXT phase are read while the
-// current phase's 16 MFMAs run (interleaved by sched_group_barrier), so LDS reads and barriers
-// no longer sit between MFMA clusters. Register sets: A0 / A1 fragments (32 VGPRs each) and two
+// Pipelined quadrant phases (qp2): ONE barrier per phase, and the fragments of the NEXT phase
+// are read while the current phase's 16 MFMAs run (interleaved by sched_group_barrier), so LDS
+// reads and barriers do not sit between MFMA clusters. Register sets: A0 / A1 fragments (32 VGPRs each) and two
 // B sets whose roles swap every K-tile (B0(t) is read in Q4(t-1) and kept until Q4(t), B1(t) is
 // read in Q1(t)), 224 VGPRs with the accumulators.
 // Half-tile schedule (phase P = 4t + quadrant issues sequence index P + 7, index = 4u + type
@@ -638,7 +308,7 @@ __device__ __forceinline__ void qp2_mma(f32x4_t (&acc)[4][2], const u16x8_t (&a)
       for (int j = 0; j < 2; ++j) acc[i][j] = mfma16<BF16>(a[i][ks], b[j][ks], acc[i][j]);
 }
 
-template <bool BF16, bool FILTER, int VAR = 0>
+template <bool BF16, bool FILTER>
 __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ C, int64_t ld_img,
     int64_t n_rows, int n_qtiles, int64_t n_ctiles, int ktiles,
@@ -718,7 +388,7 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
   auto wait_for = [&](int needed, int last_issued) {
     const int last = last_issued < total - 1 ? last_issued : total - 1;
     const int n = last - needed;
-    if constexpr (!(VAR & 1)) wait_vm_halves(n > 0 ? n : 0);  // VAR&1: timing-only, racy
+    wait_vm_halves(n > 0 ? n : 0);
   };
   auto read_a = [&](u16x8_t (&a)[4][2], const char* half) {
 #pragma unroll
@@ -788,9 +458,6 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     wait_for(4 * t_ + 6, 4 * t_ + 10); /* B1(t+1) for Q1(t+1) */                                 \
   }
 
-  if constexpr (VAR & 2) {  // static priority for the younger half (MI355X_MICROARCH item 4)
-    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-  }
   int t = 0;
   for (; t + 1 < ktiles; t += 2) {
     QP2_TILE(t, fbx, fby);
@@ -799,7 +466,7 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
   if (t < ktiles) QP2_TILE(t, fbx, fby);
 #undef QP2_TILE
 
-  // ---- epilogue: quadrant qd = (ah, bh) as in qp ----
+  // ---- epilogue: quadrant (ah, bh) = catalog half ah x query half bh ----
   auto store_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -819,240 +486,20 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
   store_quadrant(acc3, 1, 0);
 }
 
-// =============================================================================================
-// Persistent pipelined quadrant phases (pq, the default): qp2's tile, LDS image and phase
-// schedule, but one workgroup per CU walks a sequence of output tiles and the half-tile stream
-// runs straight across tile boundaries -- the next tile's first K-tiles are already in flight
-// (and its first fragments already read) while the current tile's last phases and epilogue run.
-// At d = 1536 the per-tile prologue latency and epilogue of a one-tile-per-workgroup launch
-// cost ~22 % (measured: 1050 TF at K = 1536 vs 1305 TF at K = 12288).
-// Tile order: virtual block vb = iter * G + wg goes through the same XCD-bijective remap and
-// 4-catalog-tile grouping as qp2 (G % 8 == 0, so vb and wg share the XCD label).
-// =============================================================================================
-// Tile origins are forced uniform (readfirstlane) and the buffer descriptors are rebuilt from
-// them at each issue: a descriptor carried through the tile loop in a struct ended up in VGPRs,
-// which turns every buffer_load ... lds into a readfirstlane waterfall loop.
-struct PqTile {
-  int c0, q0;
-};
-
-__device__ __forceinline__ PqTile pq_tile(int64_t vb, int64_t nwg, int n_qtiles, int64_t n_ctiles) {
-  PqTile T;
-  const int64_t vbc = vb < nwg ? vb : nwg - 1;  // past the end: a valid tile, never stored
-  const int64_t xcd = vbc & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int64_t L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (vbc >> 3);
-  const int64_t per_group = (int64_t)QP_GROUP_C * n_qtiles;
-  const int64_t g = L / per_group, w = L - g * per_group;
-  const int64_t gc_rem = n_ctiles - g * QP_GROUP_C;
-  const int64_t gc = gc_rem < QP_GROUP_C ? gc_rem : QP_GROUP_C;
-  T.c0 = __builtin_amdgcn_readfirstlane((int)((g * QP_GROUP_C + w % gc) * 256));
-  T.q0 = __builtin_amdgcn_readfirstlane((int)((w / gc) * 256));
-  return T;
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const uint16_t* base, int64_t off,
-                                                               int64_t bytes) {
-  const uint64_t a = (uint64_t)(base + off);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
-}
-
-template <bool BF16, bool FILTER>
-__global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_pq_kernel(
-    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ C, int64_t ld_img,
-    int64_t n_rows, int n_qtiles, int64_t n_ctiles, int nk,
-    const float* __restrict__ qscale, const float* __restrict__ cscale, EpiArgs e) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t G = gridDim.x, wg = blockIdx.x;
-  const int64_t nwg = (int64_t)n_qtiles * n_ctiles;
-  const int my_tiles = (int)((nwg - wg + G - 1) / G);
-  const int total_kt = my_tiles * nk;
-  const int total = 4 * total_kt;
-
-  const int wa = wave >> 2;
-  const int wb = wave & 3;
-  const int fr = lane & 15;
-  // row r = base + 16*i + fr has (r & 7) == (fr & 7): one swizzled column per k-step, rows are
-  // immediate offsets (i * 2048 bytes)
-  int a_off0[2], b_off0[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const int c = ks * 4 + (lane >> 4);
-    a_off0[ks] = (wa * 64 + fr) * 128 + ((c ^ (fr & 7)) << 4);
-    b_off0[ks] = (wb * 32 + fr) * 128 + ((c ^ (fr & 7)) << 4);
-  }
-  const int64_t row_bytes = ld_img * 2;
-  const int voff = (int)((wave * 16 + (lane >> 3)) * row_bytes) + (((lane & 7) ^ (lane >> 3)) << 4);
-  const int piece_step = (int)(8 * row_bytes);
-  const int half_step = (int)(128 * row_bytes);
-
-  int iter = 0;  // output tile being computed
-  PqTile cur = pq_tile(wg, nwg, n_qtiles, n_ctiles);
-  PqTile nxt = pq_tile(wg + G, nwg, n_qtiles, n_ctiles);
-
-  // sequence index idx = 4 * (global K-tile) + type; a global K-tile kt belongs to output tile
-  // kt / nk, which is `iter` or `iter + 1` (the stream runs at most 2 K-tiles ahead, nk >= 2).
-  auto issue = [&](int idx) __attribute__((always_inline)) {
-    if (idx < total) {
-      const int tk = idx >> 2, type = idx & 3;
-      const bool next = tk >= (iter + 1) * nk;
-      const int t = tk - (next ? iter + 1 : iter) * nk;
-      char* dst = smem + (tk & 1) * QP_BUF + p_half_off(type) + wave * 2048;
-      const int soff = t * 128 + ((type == P_A1 || type == P_B1) ? half_step : 0);
-      const bool is_c = type == P_A0 || type == P_A1;
-      const int tc0 = next ? nxt.c0 : cur.c0, tq0 = next ? nxt.q0 : cur.q0;
-      int64_t c_rem = ((int64_t)n_rows - tc0) * row_bytes;
-      c_rem = c_rem < 256 * row_bytes ? c_rem : 256 * row_bytes;
-      const __amdgpu_buffer_rsrc_t rs = is_c ? uniform_rsrc(C, (int64_t)tc0 * ld_img, c_rem)
-                                             : uniform_rsrc(Q, (int64_t)tq0 * ld_img,
-                                                            256 * row_bytes);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)dst, 16, voff, soff, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + 1024), 16, voff,
-                                               soff + piece_step, 0, 0);
-    }
-  };
-  auto wait_for = [&](int needed, int last_issued) __attribute__((always_inline)) {
-    const int last = last_issued < total - 1 ? last_issued : total - 1;
-    const int n = last - needed;
-    wait_vm_halves(n > 0 ? n : 0);
-  };
-  auto read_a = [&](u16x8_t (&a)[4][2], const char* half) __attribute__((always_inline)) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i][ks] = *(const u16x8_t*)(half + a_off0[ks] + i * 2048);
-  };
-  auto read_b = [&](u16x8_t (&b)[2][2], const char* half) __attribute__((always_inline)) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) b[j][ks] = *(const u16x8_t*)(half + b_off0[ks] + j * 2048);
-  };
-
-  f32x4_t acc0[4][2], acc1[4][2], acc2[4][2], acc3[4][2];
-  auto zero_acc = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        acc0[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        acc1[i][j] = acc0[i][j];
-        acc2[i][j] = acc0[i][j];
-        acc3[i][j] = acc0[i][j];
-      }
-  };
-  auto store_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t q = cur.q0 + bh * 128 + wb * 32 + j * 16 + fr;
-      const float qs = qscale[q];
-      const float th = FILTER ? e.thr[q] : 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t i0 = cur.c0 + ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
-        epilogue4<FILTER>(e, q, i0, n_rows, acc[i][j], qs, th, cscale);
-      }
-    }
-  };
-  // end of an output tile: write it, advance the tile descriptors
-  auto finish_tile = [&]() __attribute__((always_inline)) {
-    store_quadrant(acc0, 0, 0);
-    store_quadrant(acc1, 0, 1);
-    store_quadrant(acc2, 1, 1);
-    store_quadrant(acc3, 1, 0);
-    zero_acc();
-    ++iter;
-    cur = nxt;
-    nxt = pq_tile(wg + (int64_t)(iter + 1) * G, nwg, n_qtiles, n_ctiles);
-  };
-
-  zero_acc();
-  u16x8_t fa0[4][2], fa1[4][2], fbx[2][2], fby[2][2];
-#pragma unroll
-  for (int idx = 0; idx < 7; ++idx) issue(idx);
-  wait_for(1, 6);
-  qp_barrier();
-  read_a(fa0, smem + p_half_off(P_A0));
-  read_b(fbx, smem + p_half_off(P_B0));
-  wait_for(2, 6);
-
-  // one K-tile (global index KT) of four phases, exactly as qp2
-#define PQ_KTILE(KT, s0, s1, MORE)                                                               \
-  {                                                                                             \
-    const int t_ = (KT);                                                                        \
-    const char* buf = smem + (t_ & 1) * QP_BUF;                                                 \
-    const char* nbuf = smem + ((t_ + 1) & 1) * QP_BUF;                                          \
-    qp_barrier();                                                                               \
-    issue(4 * t_ + 7);                                                                          \
-    qp2_mma<BF16>(acc0, fa0, s0);                                                               \
-    read_b(s1, buf + p_half_off(P_B1));                                                         \
-    _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_) {                                          \
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                        \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                        \
-    }                                                                                           \
-    wait_for(4 * t_ + 3, 4 * t_ + 7);                                                           \
-    qp_barrier();                                                                               \
-    issue(4 * t_ + 8);                                                                          \
-    qp2_mma<BF16>(acc1, fa0, s1);                                                               \
-    read_a(fa1, buf + p_half_off(P_A1));                                                        \
-    _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                          \
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                        \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                        \
-    }                                                                                           \
-    qp_barrier();                                                                               \
-    issue(4 * t_ + 9);                                                                          \
-    qp2_mma<BF16>(acc2, fa1, s1);                                                               \
-    wait_for(4 * t_ + 5, 4 * t_ + 9);                                                           \
-    qp_barrier();                                                                               \
-    issue(4 * t_ + 10);                                                                         \
-    qp2_mma<BF16>(acc3, fa1, s0);                                                               \
-    if (MORE) {                                                                                 \
-      read_a(fa0, nbuf + p_half_off(P_A0));                                                     \
-      read_b(s1, nbuf + p_half_off(P_B0));                                                      \
-    }                                                                                           \
-    _Pragma("unroll") for (int i_ = 0; i_ < 12; ++i_) {                                         \
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                        \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                        \
-    }                                                                                           \
-    wait_for(4 * t_ + 6, 4 * t_ + 10);                                                          \
-  }
-
-  // nk is even (host guarantees), so every output tile starts with B0 in the X set
-  for (int it = 0; it < my_tiles; ++it) {
-    for (int tt = 0; tt < nk; tt += 2) {
-      const int kt = it * nk + tt;
-      PQ_KTILE(kt, fbx, fby, true);
-      PQ_KTILE(kt + 1, fby, fbx, tt + 2 < nk);
-    }
-    // the next tile's first fragments are read after the epilogue, not during the last phase:
-    // keeps them out of the registers the epilogue needs (its A0/B0 halves have landed and
-    // passed the last phase's barrier; nothing is issued until the next barrier)
-    finish_tile();
-    if (it + 1 < my_tiles) {
-      const char* nb = smem + ((it + 1) * nk & 1) * QP_BUF;
-      read_a(fa0, nb + p_half_off(P_A0));
-      read_b(fbx, nb + p_half_off(P_B0));
-    }
-  }
-#undef PQ_KTILE
-}
+// Kernel choice: batches padded to a multiple of 256 queries take the 256 x 256 quadrant-phase
+// kernel; smaller batches (B_pad = 128) the 128 x 128 one. Measured alternatives that lost on
+// MI355X ("screening GEMM"): a 4-slot ring with k32 slices, one barrier per phase
+// with two barriers (qp), a persistent one-workgroup-per-CU walk of the same tiles, and a
+// 4-wave 128 x 128-per-wave tile (LDS-DMA issue cost with one wave per SIMD).
+constexpr int QP_TILE = 256;
 
 template <bool FILTER>
 static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
                        int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
                        const float* cscale, const EpiArgs& e, hipStream_t stream) {
-  static const int force_tile = [] {
-    const char* v = getenv("EBT_GEMM_TILE");
-    return v ? atoi(v) : 0;
-  }();
-  const bool big = B_pad % HBN_ == 0 && force_tile != 128;
-  const int n_qtiles = (int)(B_pad / (big ? HBN_ : GBN));
-  const int64_t n_ctiles = ceil_div(n_rows, big ? HBM_ : GBM);
+  const bool big = B_pad % QP_TILE == 0;
+  const int n_qtiles = (int)(B_pad / (big ? QP_TILE : GBN));
+  const int64_t n_ctiles = ceil_div(n_rows, big ? QP_TILE : GBM);
   const int64_t nwg = n_ctiles * n_qtiles;
   if (nwg > 0x7fffffffLL) {
     set_error("screen gemm: grid too large");
@@ -1060,59 +507,14 @@ static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_
   }
   const uint16_t* Q = (const uint16_t*)qimg;
   const uint16_t* C = (const uint16_t*)cimg;
-  if (big && force_tile == 3 && d_pad % 128 == 0) {  // persistent variant (measured slower)
-    static const int n_cu = [] {
-      int dev = 0, cus = 256;
-      if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      return cus > 0 ? cus : 256;
-    }();
-    const int64_t G = nwg < n_cu ? nwg : n_cu;  // one 128 KiB-LDS workgroup per CU
-    dim3 grid((unsigned)G), block(QP_THREADS);
-    auto k = img_dtype == EBT_BF16 ? screen_gemm_pq_kernel<true, FILTER>
-                                   : screen_gemm_pq_kernel<false, FILTER>;
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, QP_LDS);
-    hipLaunchKernelGGL(k, grid, block, QP_LDS, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
-                       n_ctiles, d_pad / 64, qscale, cscale, e);
-    return launch_check("screen_gemm_pq_kernel");
-  }
-  if (big && (force_tile == 0 || force_tile == 2)) {  // pipelined quadrant phases, 1 tile/WG
+  if (big) {
     dim3 grid((unsigned)nwg), block(QP_THREADS);
-    static const int var = [] {
-      const char* v = getenv("EBT_GEMM_VAR");
-      return v ? atoi(v) : 0;
-    }();
     auto k = img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, FILTER>
                                    : screen_gemm_qp2_kernel<false, FILTER>;
-    if (var == 1)
-      k = img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, FILTER, 1>
-                                : screen_gemm_qp2_kernel<false, FILTER, 1>;
-    else if (var == 2)
-      k = img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, FILTER, 2>
-                                : screen_gemm_qp2_kernel<false, FILTER, 2>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, QP_LDS);
     hipLaunchKernelGGL(k, grid, block, QP_LDS, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
                        n_ctiles, d_pad / 64, qscale, cscale, e);
     return launch_check("screen_gemm_qp2_kernel");
-  }
-  if (big && force_tile == 1) {  // quadrant phases, two barriers per phase
-    dim3 grid((unsigned)nwg), block(QP_THREADS);
-    auto k = img_dtype == EBT_BF16 ? screen_gemm_qp_kernel<true, FILTER>
-                                   : screen_gemm_qp_kernel<false, FILTER>;
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, QP_LDS);
-    hipLaunchKernelGGL(k, grid, block, QP_LDS, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
-                       n_ctiles, d_pad / 64, qscale, cscale, e);
-    return launch_check("screen_gemm_qp_kernel");
-  }
-  if (big) {
-    dim3 grid((unsigned)nwg), block(HTHREADS);
-    auto k = img_dtype == EBT_BF16 ? screen_gemm256_kernel<true, FILTER>
-                                   : screen_gemm256_kernel<false, FILTER>;
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              HLDS_BYTES);
-    hipLaunchKernelGGL(k, grid, block, HLDS_BYTES, stream, Q, C, (int64_t)ld_img, n_rows,
-                       n_qtiles, n_ctiles, d_pad / HBK_, qscale, cscale, e);
-    return launch_check("screen_gemm256_kernel");
   }
   dim3 grid((unsigned)nwg), block(GTHREADS);
   auto k = img_dtype == EBT_BF16 ? screen_gemm_kernel<true, FILTER>

@@ -407,17 +407,24 @@ int select_topk_counted(const float* vals, const int64_t* idx, int64_t ld, int64
 // ------------------------------------------------------------- fused-screen helpers -------
 // thr[b] = vals[b*ld + kprime-1]: the k'-th best approx score of the head chunk, a lower bound
 // of the query's global k'-th best (-inf when the head had fewer than k' valid rows).
+// Fused-screen bookkeeping between segments: thr[b] = the k'-th best approx score of the
+// candidate list so far (a lower bound of the global k'-th: the list is the top-k' of a subset of
+// the rows), padding queries +inf (they append nothing); ovf_max[b] = max count seen (a segment
+// whose count exceeded the capacity dropped candidates -> certified -1).
 __global__ void kth_threshold_kernel(const float* __restrict__ vals, int64_t ld, int64_t B,
-                                     int64_t B_pad, int kprime, float* __restrict__ thr) {
+                                     int64_t B_pad, int kprime, float* __restrict__ thr,
+                                     const int* __restrict__ cnt, int* __restrict__ ovf_max) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < B) thr[b] = vals[b * ld + kprime - 1];
-  else if (b < B_pad) thr[b] = __builtin_inff();  // padding queries append nothing
+  if (thr) {
+    if (b < B) thr[b] = vals[b * ld + kprime - 1];
+    else if (b < B_pad) thr[b] = __builtin_inff();
+  }
+  if (cnt && b < B) ovf_max[b] = max(ovf_max[b], cnt[b]);
 }
-
 int kth_threshold(const float* vals, int64_t ld, int64_t B, int64_t B_pad, int kprime,
-                  float* thr, hipStream_t st) {
+                  float* thr, const int* cnt, int* ovf_max, hipStream_t st) {
   hipLaunchKernelGGL(kth_threshold_kernel, dim3((unsigned)ceil_div(B_pad, 256)), dim3(256), 0,
-                     st, vals, ld, B, B_pad, kprime, thr);
+                     st, vals, ld, B, B_pad, kprime, thr, cnt, ovf_max);
   return launch_check("kth_threshold_kernel");
 }
 

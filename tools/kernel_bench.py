@@ -43,6 +43,8 @@ def bench_gemm(dev, B, N, d, dt):
     # fused-screen (filter) epilogue: threshold high enough that ~0.3% of scores are appended
     thr = torch.full((B,), 0.0, device=dev)
     thr[:] = 3.0 * (d ** 0.5)  # raw (unnormalised) Gaussian dot products: ~3 sigma
+    if os.environ.get("EBT_KB_THR") == "inf":  # no appends at all (ablation runs)
+        thr[:] = float("inf")
     cap = 8192
     cnt = torch.zeros(B, dtype=torch.int32, device=dev)
     cv = torch.empty((B, cap), device=dev)
@@ -57,9 +59,7 @@ def bench_gemm(dev, B, N, d, dt):
     return {"kernel": "screen_gemm", "B": B, "N": N, "d": d, "dtype": str(dt), "ms": round(ms, 4),
             "tflops": round(tf, 1), "frac_2500": round(tf / 2500, 4),
             "filter_ms": round(ms_f, 4), "filter_tflops": round(tf_f, 1),
-            "mean_appended": round(float(cnt.float().mean()), 1),
-            "tile": os.environ.get("EBT_GEMM_TILE", "auto"),
-            "var": os.environ.get("EBT_GEMM_VAR", "0")}
+            "mean_appended": round(float(cnt.float().mean()), 1)}
 
 
 def bench_select(dev, B, n, kp):
