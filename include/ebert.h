@@ -107,15 +107,21 @@ int ebt_screen_scores(const void* qimg, int64_t B_pad, const void* cimg, int64_t
                       int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
                       const float* cscale, float* scores, int64_t ld_scores, void* stream);
 
-/* The fused screen's GEMM: the same product, but only scores >= thr[b] leave the kernel, appended
- * to query b's candidate list: slot p = atomicAdd(&cnt[b], 1); if p < cap,
- * cand_v/cand_i[b*ld_cand + cand_off + p] = (score, idx_base + i). cnt[b] > cap afterwards means
- * the list overflowed. thr has B_pad entries (use +inf for padding rows). */
+/* The fused screen's GEMM: the same product, but only scores >= thr[b] leave the kernel.
+ * Catalog rows are grouped by G = ebt_filter_group_rows(B_pad) (the kernel's tile: 256 rows
+ * when B_pad % 256 == 0, else 128); the hits of query b in group g go to
+ * cand[b*ld_cand + g*EBT_FILTER_SLOTS + p] (p < the group's count) as u64 composites
+ * (order-preserving key of the f32 score << 32 | ~(uint32)(idx_base + local row)), and
+ * counts[b*ld_counts + g] = the group's hit count (saturated at 255). A count above
+ * EBT_FILTER_SLOTS drops hits and sets ovf[b] = 1. Buffers have B_pad rows, ld_cand >=
+ * groups*EBT_FILTER_SLOTS, ld_counts >= groups; thr has B_pad entries (+inf for padding). */
+#define EBT_FILTER_SLOTS 16
+int64_t ebt_filter_group_rows(int64_t B_pad);
 int ebt_screen_filter(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
                       int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
-                      const float* cscale, const float* thr, int32_t* cnt, float* cand_v,
-                      int64_t* cand_i, int64_t ld_cand, int64_t cand_off, int32_t cap,
-                      int64_t idx_base, void* stream);
+                      const float* cscale, const float* thr, uint64_t* cand, int64_t ld_cand,
+                      uint8_t* counts, int64_t ld_counts, int32_t* ovf, int64_t idx_base,
+                      void* stream);
 
 /* Excluded rows (lib.py:48,55: rated movies are not candidates): for every b < B and every
  * GLOBAL row g in excl_rows[excl_off[b] .. excl_off[b+1]) with col_begin <= g < col_end,
@@ -140,7 +146,9 @@ int ebt_select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B
  * best by (score desc, row asc) go to out_scores/out_rows[b*k + j] (rows + row_offset; empty
  * slots NaN / -1). certified[b] = 1 iff the candidate set provably contains the exact top-k:
  * kprime >= n_rows (every row is a candidate),
- * fewer than kprime valid candidates, or approx[kprime-1] < approx[k-1] - 2*eps[b]. */
+ * fewer than kprime valid candidates, or approx[kprime-1] < approx[k-1] - 2*eps[b].
+ * Candidates with approx < approx[k-1] - 2*eps[b] cannot be in the top k and are not gathered
+ * (equal cand_vals and eps = 0 rescore every candidate). */
 int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype, int64_t ld,
                 const double* gnorm64, int64_t row_offset, const float* cand_vals,
                 const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
@@ -167,7 +175,7 @@ int ebt_screen_exact(const double* q64, int64_t B, int32_t d, const void* cat, i
 #define EBT_FLAG_EXACT 2
 #define EBT_EXACT_EPS 1.1920928955078125e-07f /* 2^-23 >= f32 rounding of |s| <= 1 + f64 error */
 /* How ebt_cosine_topk will run these sizes (host pointers out): head rows screened unfused,
- * fused-candidate capacity per query (0 = not fused), score chunk rows, fused flag. */
+ * the largest fused tail segment in rows (cap; 0 = not fused), score chunk rows, fused flag. */
 int ebt_cosine_topk_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
                          int64_t chunk_rows, int flags, int64_t* head_rows, int64_t* cap,
                          int64_t* chunk, int32_t* fused);

@@ -1,6 +1,7 @@
 // extern "C" entry points of libebert.so (declared in include/ebert.h), the pipeline
 // orchestrator ebt_cosine_topk, the per-stage hipEvent timer and error reporting.
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -47,14 +48,13 @@ int rescore(const double*, int64_t, int32_t, const void*, int, int64_t, const do
             const float*, const int64_t*, int32_t, int32_t, int64_t, const float*, double*, int64_t*,
             int32_t*, hipStream_t, const int*, int);
 int screen_gemm_filter(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
-                       const float*, const float*, const float*, int*, float*, int64_t*, int64_t,
-                       int64_t, int, int64_t, hipStream_t);
-int select_topk_counted(const float*, const int64_t*, int64_t, int64_t, int64_t, const int*, int,
-                        int32_t, float*, int64_t*, int64_t, hipStream_t);
-int kth_threshold(const float*, int64_t, int64_t, int64_t, int, float*, const int*, int*,
-                  hipStream_t);
-int mask_candidates(float*, const int64_t*, int64_t, int64_t, int64_t, const int*, int, int64_t,
-                    const int64_t*, const int64_t*, hipStream_t);
+                       const float*, const float*, const float*, uint64_t*, int64_t, uint8_t*,
+                       int64_t, int*, int64_t, hipStream_t);
+int64_t filter_group_rows(int64_t);
+
+int kth_threshold(const float*, int64_t, int64_t, int64_t, int, float*, hipStream_t);
+int merge_segment(float*, int64_t*, int64_t, int, const uint64_t*, int64_t, const uint8_t*,
+                  int64_t, int64_t, int64_t, const int64_t*, const int64_t*, int*, hipStream_t);
 int merge_topk(const double*, const int64_t*, int32_t, int64_t, int32_t, double*, int64_t*,
                hipStream_t);
 int screen_exact(const double*, int64_t, int32_t, const void*, int, int64_t, const double*, int64_t,
@@ -122,10 +122,10 @@ struct StageScope {
 //           [B][kprime + cap] (head top-k' then appended tail candidates), counters and
 //           thresholds. The tail rows [H, n) never materialise scores.
 struct WsLayout {
-  int64_t chunk, ld_s, n_chunks, head, cap, ld_cand;
+  int64_t chunk, ld_s, n_chunks, head, seg_max, groups_max, group_rows, ld_cand, ld_counts;
   int segs;
   bool fused;
-  size_t off_s, off_segv, off_segi, off_chv, off_chi, off_fv, off_fi, off_cv, off_ci, off_cnt,
+  size_t off_s, off_segv, off_segi, off_chv, off_chi, off_fv, off_fi, off_cand, off_counts,
       off_thr, off_ovf, off_eps, bytes;
 };
 
@@ -134,19 +134,28 @@ static size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
                           int64_t chunk_rows, int flags) {
   WsLayout L{};
-  // fused screen: head H rows processed unfused give each query a threshold; the tail is
-  // filtered inside the GEMM epilogue. Expected tail candidates ~ kprime * (n - H) / H.
+  // fused screen: the head H rows, processed unfused, give each query its first threshold; the
+  // tail is filtered inside the GEMM epilogue in doubling segments (each as large as all rows
+  // before it, so ~k' hits per query per segment), capped so the per-group hit slots
+  // (B_pad x groups x EBT_FILTER_SLOTS u64) stay within 1 GiB.
+  static const int64_t h_min = [] {
+    const char* v = getenv("EBT_FUSE_HEAD");
+    return v ? atoll(v) : 65536LL;
+  }();
   int64_t H = 256LL * kprime;
-  H = H < 65536 ? 65536 : H;
+  H = H < h_min ? h_min : H;
   H = (H + 255) / 256 * 256;
   L.fused = !(flags & (EBT_FLAG_NO_FUSE | EBT_FLAG_EXACT)) && n_rows >= 2 * H;
   L.head = L.fused ? H : n_rows;
   if (L.fused) {
-    // the tail is screened in doubling segments (each as large as all rows before it), so a
-    // segment appends ~k' candidates per query whatever n is
-    int64_t cap = 4 * (int64_t)kprime + 2048;
-    L.cap = (cap + 255) / 256 * 256;
-    L.ld_cand = (kprime + L.cap + 3) / 4 * 4;
+    L.group_rows = filter_group_rows(B_pad);
+    int64_t gmax = (1LL << 30) / (B_pad * EBT_FILTER_SLOTS * 8);
+    gmax = gmax < 16 ? 16 : gmax;
+    const int64_t need = ceil_div(n_rows - H, L.group_rows);
+    L.groups_max = gmax < need ? gmax : need;
+    L.seg_max = L.groups_max * L.group_rows;
+    L.ld_cand = L.groups_max * EBT_FILTER_SLOTS;
+    L.ld_counts = (L.groups_max + 15) / 16 * 16;
   }
   L.chunk = chunk_rows < L.head ? chunk_rows : L.head;
   if (L.chunk < 1) L.chunk = 1;
@@ -175,12 +184,10 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
   L.off_fi = o;
   o = align_up(o + (size_t)B * kprime * 8);
   if (L.fused) {
-    L.off_cv = o;
-    o = align_up(o + (size_t)B * L.ld_cand * 4);
-    L.off_ci = o;
-    o = align_up(o + (size_t)B * L.ld_cand * 8);
-    L.off_cnt = o;
-    o = align_up(o + (size_t)B_pad * 4);
+    L.off_cand = o;
+    o = align_up(o + (size_t)B_pad * L.ld_cand * 8);
+    L.off_counts = o;
+    o = align_up(o + (size_t)B_pad * L.ld_counts);
     L.off_thr = o;
     o = align_up(o + (size_t)B_pad * 4);
     L.off_ovf = o;
@@ -306,13 +313,15 @@ int ebt_screen_scores(const void* qimg, int64_t B_pad, const void* cimg, int64_t
                      ld_scores, (hipStream_t)stream);
 }
 
+int64_t ebt_filter_group_rows(int64_t B_pad) { return filter_group_rows(B_pad); }
+
 int ebt_screen_filter(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
                       int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
-                      const float* cscale, const float* thr, int32_t* cnt, float* cand_v,
-                      int64_t* cand_i, int64_t ld_cand, int64_t cand_off, int32_t cap,
-                      int64_t idx_base, void* stream) {
+                      const float* cscale, const float* thr, uint64_t* cand, int64_t ld_cand,
+                      uint8_t* counts, int64_t ld_counts, int32_t* ovf, int64_t idx_base,
+                      void* stream) {
   return screen_gemm_filter(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale, cscale,
-                            thr, cnt, cand_v, cand_i, ld_cand, cand_off, cap, idx_base,
+                            thr, cand, ld_cand, counts, ld_counts, ovf, idx_base,
                             (hipStream_t)stream);
 }
 
@@ -366,7 +375,7 @@ int ebt_cosine_topk_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprim
   }
   const WsLayout L = ws_layout(B, B_pad, n_rows, kprime, chunk_rows, flags);
   *head_rows = L.head;
-  *cap = L.fused ? L.cap : 0;
+  *cap = L.fused ? L.seg_max : 0;
   *chunk = L.chunk;
   *fused = L.fused ? 1 : 0;
   return EBT_OK;
@@ -430,66 +439,43 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
     return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, fv, fi, kprime, k, n_rows, eps,
                    out_scores, out_rows, certified, st, nullptr, 0);
   }
-  float* cv = (float*)(ws + L.off_cv);
-  int64_t* ci = (int64_t*)(ws + L.off_ci);
-  int* cnt = (int*)(ws + L.off_cnt);
+  uint64_t* cand = (uint64_t*)(ws + L.off_cand);
+  uint8_t* counts = (uint8_t*)(ws + L.off_counts);
   float* thr = (float*)(ws + L.off_thr);
-  // 1. head rows [0, H): exact top-k' per query into the first k' slots of the candidate rows
-  rc = head_topk(L, ws, qimg, qscale, B, B_pad, cimg, cscale, img_dtype, ld_img, 0, L.head, d_pad,
-                 row_offset, excl_off, excl_rows, kprime, cv, ci, L.ld_cand, timer, st);
-  if (rc) return rc;
-  // 2. per-query threshold = the head's k'-th best approx score
   int* ovf = (int*)(ws + L.off_ovf);
+  // 1. head rows [0, H): exact top-k' per query (the list fv/fi)
+  rc = head_topk(L, ws, qimg, qscale, B, B_pad, cimg, cscale, img_dtype, ld_img, 0, L.head, d_pad,
+                 row_offset, excl_off, excl_rows, kprime, fv, fi, kprime, timer, st);
+  if (rc) return rc;
   rc = hip_check(hipMemsetAsync(ovf, 0, (size_t)B_pad * 4, st), "hipMemsetAsync");
   if (rc) return rc;
-  rc = kth_threshold(cv, L.ld_cand, B, B_pad, kprime, thr, nullptr, nullptr, st);
-  if (rc) return rc;
-  // 3. tail rows [H, n) in doubling segments: GEMM with the threshold filter in the epilogue,
-  //    exclusions dropped from the appended candidates, the k' best of list + appended kept,
-  //    and the threshold raised to the new k'-th best before the next segment
+  // 2. tail rows [H, n) in doubling segments: threshold = the list's k'-th score, GEMM with the
+  //    filter epilogue, merge of list + hits (exclusions dropped) back into the list
   int64_t r0 = L.head;
   while (r0 < n_rows) {
     int64_t seg = n_rows - r0 < r0 ? n_rows - r0 : r0;
     if (n_rows - (r0 + seg) < seg / 2) seg = n_rows - r0;  // no small last segment
-    const bool last = r0 + seg >= n_rows;
-    rc = hip_check(hipMemsetAsync(cnt, 0, (size_t)B_pad * 4, st), "hipMemsetAsync");
+    seg = seg < L.seg_max ? seg : L.seg_max;
+    rc = kth_threshold(fv, kprime, B, B_pad, kprime, thr, st);
     if (rc) return rc;
     {
       StageScope s(timer, EBT_STAGE_GEMM_FILTER, st);
       rc = screen_gemm_filter(qimg, B_pad, (const char*)cimg + r0 * ld_img * 2, seg, d_pad,
                               ld_img, img_dtype, qscale, cscale ? cscale + r0 : nullptr, thr,
-                              cnt, cv, ci, L.ld_cand, kprime, (int)L.cap, r0, st);
+                              cand, L.ld_cand, counts, L.ld_counts, ovf, r0, st);
     }
     if (rc) return rc;
-    if (excl_off) {
-      StageScope s(timer, EBT_STAGE_MASK, st);
-      rc = mask_candidates(cv, ci, L.ld_cand, kprime, B, cnt, (int)L.cap, row_offset, excl_off,
-                           excl_rows, st);
-      if (rc) return rc;
-    }
     {
       StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
-      rc = select_topk_counted(cv, ci, L.ld_cand, B, kprime, cnt, (int)L.cap, kprime, fv, fi,
-                               kprime, st);
-      if (rc) return rc;
-      if (!last) {  // the list so far back into the candidate rows' first k' slots
-        rc = hip_check(hipMemcpy2DAsync(cv, (size_t)L.ld_cand * 4, fv, (size_t)kprime * 4,
-                                        (size_t)kprime * 4, (size_t)B, hipMemcpyDeviceToDevice,
-                                        st), "hipMemcpy2DAsync");
-        if (!rc)
-          rc = hip_check(hipMemcpy2DAsync(ci, (size_t)L.ld_cand * 8, fi, (size_t)kprime * 8,
-                                          (size_t)kprime * 8, (size_t)B,
-                                          hipMemcpyDeviceToDevice, st), "hipMemcpy2DAsync");
-      }
-      if (!rc)
-        rc = kth_threshold(cv, L.ld_cand, B, B_pad, kprime, last ? nullptr : thr, cnt, ovf, st);
+      rc = merge_segment(fv, fi, B, kprime, cand, L.ld_cand, counts, L.ld_counts,
+                         ceil_div(seg, L.group_rows), row_offset, excl_off, excl_rows, ovf, st);
     }
     if (rc) return rc;
     r0 += seg;
   }
   StageScope s(timer, EBT_STAGE_RESCORE, st);
   return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, fv, fi, kprime, k, n_rows, eps,
-                 out_scores, out_rows, certified, st, ovf, (int)L.cap);
+                 out_scores, out_rows, certified, st, ovf, 0);
 }
 
 void* ebt_timer_create(void) { return new (std::nothrow) Timer(); }

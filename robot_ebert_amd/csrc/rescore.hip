@@ -67,11 +67,17 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
   for (int j = tid; j < d; j += RTHREADS) qs[j] = q64[b * d + j];
   __syncthreads();
   const int64_t* cr = cand_rows + b * kprime;
+  // Candidates whose approx score is below approx[k-1] - 2 eps cannot be in the top k (the k
+  // best candidates all have exact >= approx[k-1] - eps > their exact), so their rows are not
+  // gathered: about k + (rows in the 2 eps band) of the k' candidates are rescored.
+  const float* cv = cand_vals + b * kprime;
+  const double cut = (double)cv[k - 1] - 2.0 * (double)eps[b];
   int myvalid = 0;
   for (int c = wave; c < kprime; c += RTHREADS / 64) {
     const int64_t row = cr[c];
+    const bool skip = (double)cv[c] < cut;
     double s = 0.0;
-    if (row >= 0) {
+    if (row >= 0 && !skip) {
       if constexpr (VEC) {
         constexpr int ES = (DT == EBT_F64) ? 8 : (DT == EBT_F32 ? 4 : 2);
         constexpr int PER = 16 / ES;
@@ -101,7 +107,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     if (lane == 0) {
       if (row >= 0) {
         const double v = s / gnorm[row];
-        sc[c] = (v == v) ? v : -__builtin_inf();
+        sc[c] = (v == v && !skip) ? v : -__builtin_inf();
         rw[c] = row;
         ++myvalid;
       } else {
@@ -130,7 +136,6 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
   if (tid == 0) {
     int ok = 1;
     if (nvalid >= kprime && n_rows > kprime) {  // kprime >= n_rows: every row is a candidate
-      const float* cv = cand_vals + b * kprime;
       const double T = (double)cv[k - 1];
       const double amin = (double)cv[kprime - 1];
       ok = amin < T - 2.0 * (double)eps[b];

@@ -73,23 +73,31 @@ __device__ __forceinline__ f32x4_t mfma16(const u16x8_t& a, const u16x8_t& b, f3
 // (cand_v / cand_i [q*ld_cand + cand_off + slot], slot from an atomic counter cnt[q]; slots past
 // `cap` are dropped and counted, so cnt[q] > cap flags an overflow). thr[q] is a lower bound of
 // the query's k'-th best approx score, so no candidate of the true top-k' is ever filtered.
+// Filter-mode output (the fused screen): catalog rows are grouped by the kernel's tile
+// (FILTER_GROUP rows: 256 for the quadrant-phase kernel, 128 for the small-batch one); for query
+// q and group g, up to EBT_FILTER_SLOTS hits go to cand[q*ld_cand + g*SLOTS + p] as u64
+// composites (f2key(score) << 32 | ~row, row = idx_base + local row) and the group's hit count to
+// counts[q*ld_counts + g] (saturated at 255; > SLOTS sets ovf[q]). Slots are claimed with LDS
+// atomics per workgroup tile, so the epilogue does no global atomics and no dependent loads.
+constexpr int FILTER_SLOTS = EBT_FILTER_SLOTS;
+
 struct EpiArgs {
-  float* S;
+  float* S;  // store mode
   int64_t ld_s;
-  const float* thr;
-  int* cnt;
-  float* cand_v;
-  int64_t* cand_i;
+  const float* thr;  // filter mode
+  uint64_t* cand;
   int64_t ld_cand;
-  int64_t cand_off;
-  int cap;
+  uint8_t* counts;
+  int64_t ld_counts;
+  int* ovf;
   int64_t idx_base;
 };
 
 template <bool FILTER>
 __device__ __forceinline__ void epilogue4(const EpiArgs& e, int64_t q, int64_t i0,
                                           int64_t n_rows, const f32x4_t& acc, float qs,
-                                          float th, const float* __restrict__ cscale) {
+                                          float th, const float* __restrict__ cscale,
+                                          uint32_t* lcnt, int64_t grp) {
   if constexpr (!FILTER) {
     float* srow = e.S + q * e.ld_s;
     if (i0 + 3 < n_rows) {
@@ -111,7 +119,8 @@ __device__ __forceinline__ void epilogue4(const EpiArgs& e, int64_t q, int64_t i
     }
   } else {
     // one vector load of the row scales and a cheap all-miss test first: the append path is
-    // taken for ~k'/H of the values, and keeping it cold keeps the accumulators in registers
+    // taken for ~k'/rows-so-far of the values; keeping it cold keeps the accumulators in
+    // registers
     float4 cs = make_float4(1.f, 1.f, 1.f, 1.f);
     if (cscale) {
       if (i0 + 3 < n_rows) {
@@ -132,15 +141,28 @@ __device__ __forceinline__ void epilogue4(const EpiArgs& e, int64_t q, int64_t i
       for (int r = 0; r < 4; ++r) {
         const int64_t i = i0 + r;
         if (i < n_rows && v[r] >= th) {
-          const int p = atomicAdd(e.cnt + q, 1);
-          if (p < e.cap) {
-            const int64_t o = q * e.ld_cand + e.cand_off + p;
-            e.cand_v[o] = v[r];
-            e.cand_i[o] = e.idx_base + i;
+          const uint32_t p = atomicAdd(lcnt, 1u);
+          if (p < (uint32_t)FILTER_SLOTS) {
+            const uint32_t row = (uint32_t)(e.idx_base + i);
+            e.cand[q * e.ld_cand + grp * FILTER_SLOTS + p] =
+                ((uint64_t)f2key(v[r]) << 32) | (uint64_t)(~row);
           }
         }
       }
     }
+  }
+}
+
+// End of a filter-mode tile: publish the per-query hit counts of group `grp` (LDS counters of
+// queries q0 .. q0 + nq - 1), after every wave's epilogue.
+__device__ __forceinline__ void filter_finish(const EpiArgs& e, const uint32_t* lcnt, int64_t q0,
+                                              int nq, int64_t grp) {
+  __syncthreads();
+  for (int t = threadIdx.x; t < nq; t += blockDim.x) {
+    const uint32_t c = lcnt[t];
+    const int64_t q = q0 + t;
+    e.counts[q * e.ld_counts + grp] = (uint8_t)(c < 255u ? c : 255u);
+    if (c > (uint32_t)FILTER_SLOTS) e.ovf[q] = 1;
   }
 }
 
@@ -167,6 +189,10 @@ __global__ __launch_bounds__(GTHREADS, 2) void screen_gemm_kernel(
   const int64_t qt = w / gc;
   const int64_t c0 = ct * GBM;
   const int64_t q0 = qt * GBN;
+  uint32_t* lcnt = (uint32_t*)(smem + GLDS_BYTES);  // filter mode: hits per query of the tile
+  if constexpr (FILTER) {
+    if (tid < GBN) lcnt[tid] = 0u;
+  }
 
   const int wi = wave >> 1;  // catalog half
   const int wj = wave & 1;   // query half
@@ -229,9 +255,10 @@ __global__ __launch_bounds__(GTHREADS, 2) void screen_gemm_kernel(
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int64_t i0 = c0 + wi * 64 + a * 16 + 4 * (lane >> 4);
-      epilogue4<FILTER>(e, q, i0, n_rows, acc[a][b], qs, th, cscale);
+      epilogue4<FILTER>(e, q, i0, n_rows, acc[a][b], qs, th, cscale, lcnt + (q - q0), ct);
     }
   }
+  if constexpr (FILTER) filter_finish(e, lcnt, q0, GBN, ct);
 }
 
 // =============================================================================================
@@ -252,6 +279,7 @@ constexpr int QP_HALF = 128 * 128;            // 16 KiB: 128 rows x 64 k x 2 B
 constexpr int QP_BUF = 4 * QP_HALF;           // one K-tile
 constexpr int QP_LDS = 2 * QP_BUF;            // 128 KiB
 constexpr int QP_GROUP_C = 4;
+constexpr int QP_TILE = 256;
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -330,6 +358,10 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
   const int64_t qt = w / gc;
   const int64_t c0 = ct * 256;
   const int64_t q0 = qt * 256;
+  uint32_t* lcnt = (uint32_t*)(smem + QP_LDS);  // filter mode: hits per query of the tile
+  if constexpr (FILTER) {
+    if (tid < QP_TILE) lcnt[tid] = 0u;
+  }
 
   const int wa = wave >> 2;
   const int wb = wave & 3;
@@ -476,7 +508,7 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t i0 = c0 + ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
-        epilogue4<FILTER>(e, q, i0, n_rows, acc[i][j], qs, th, cscale);
+        epilogue4<FILTER>(e, q, i0, n_rows, acc[i][j], qs, th, cscale, lcnt + (q - q0), ct);
       }
     }
   };
@@ -484,6 +516,7 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
   store_quadrant(acc1, 0, 1);
   store_quadrant(acc2, 1, 1);
   store_quadrant(acc3, 1, 0);
+  if constexpr (FILTER) filter_finish(e, lcnt, q0, QP_TILE, ct);
 }
 
 // Kernel choice: batches padded to a multiple of 256 queries take the 256 x 256 quadrant-phase
@@ -491,8 +524,6 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
 // MI355X ("screening GEMM"): a 4-slot ring with k32 slices, one barrier per phase
 // with two barriers (qp), a persistent one-workgroup-per-CU walk of the same tiles, and a
 // 4-wave 128 x 128-per-wave tile (LDS-DMA issue cost with one wave per SIMD).
-constexpr int QP_TILE = 256;
-
 template <bool FILTER>
 static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
                        int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
@@ -511,15 +542,18 @@ static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_
     dim3 grid((unsigned)nwg), block(QP_THREADS);
     auto k = img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, FILTER>
                                    : screen_gemm_qp2_kernel<false, FILTER>;
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, QP_LDS);
-    hipLaunchKernelGGL(k, grid, block, QP_LDS, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
+    const int lds = QP_LDS + (FILTER ? QP_TILE * 4 : 0);
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(k, grid, block, lds, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
                        n_ctiles, d_pad / 64, qscale, cscale, e);
     return launch_check("screen_gemm_qp2_kernel");
   }
   dim3 grid((unsigned)nwg), block(GTHREADS);
   auto k = img_dtype == EBT_BF16 ? screen_gemm_kernel<true, FILTER>
                                  : screen_gemm_kernel<false, FILTER>;
-  hipLaunchKernelGGL(k, grid, block, GLDS_BYTES, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
+  const int lds = GLDS_BYTES + (FILTER ? GBN * 4 : 0);
+  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL(k, grid, block, lds, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
                      n_ctiles, d_pad / GBK, qscale, cscale, e);
   return launch_check("screen_gemm_kernel");
 }
@@ -561,26 +595,30 @@ int screen_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_row
                             e, stream);
 }
 
+int64_t filter_group_rows(int64_t B_pad) { return B_pad % QP_TILE == 0 ? QP_TILE : GBM; }
+
 int screen_gemm_filter(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
                        int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
-                       const float* cscale, const float* thr, int* cnt, float* cand_v,
-                       int64_t* cand_i, int64_t ld_cand, int64_t cand_off, int cap,
-                       int64_t idx_base, hipStream_t stream) {
-  int rc = check_gemm_args("screen_gemm_filter", qimg, B_pad, cimg, n_rows, d_pad, ld_img,
+                       const float* cscale, const float* thr, uint64_t* cand, int64_t ld_cand,
+                       uint8_t* counts, int64_t ld_counts, int* ovf, int64_t idx_base,
+                       hipStream_t stream) {
+  int rc = check_gemm_args("ebt_screen_filter", qimg, B_pad, cimg, n_rows, d_pad, ld_img,
                            img_dtype, qscale, cscale);
   if (rc) return rc;
-  if (!thr || !cnt || !cand_v || !cand_i || cap < 1 || ld_cand < cand_off + cap) {
-    set_error("screen_gemm_filter: bad candidate buffer");
+  const int64_t groups = ceil_div(n_rows, filter_group_rows(B_pad));
+  if (!thr || !cand || !counts || !ovf || ld_counts < groups ||
+      ld_cand < groups * FILTER_SLOTS || idx_base < 0 || idx_base + n_rows > 0xffffffffLL) {
+    set_error("ebt_screen_filter: bad candidate buffers (groups=%lld ld_cand=%lld ld_counts=%lld)",
+              (long long)groups, (long long)ld_cand, (long long)ld_counts);
     return EBT_EINVAL;
   }
   EpiArgs e{};
   e.thr = thr;
-  e.cnt = cnt;
-  e.cand_v = cand_v;
-  e.cand_i = cand_i;
+  e.cand = cand;
   e.ld_cand = ld_cand;
-  e.cand_off = cand_off;
-  e.cap = cap;
+  e.counts = counts;
+  e.ld_counts = ld_counts;
+  e.ovf = ovf;
   e.idx_base = idx_base;
   return launch_gemm<true>(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale, cscale,
                            e, stream);

@@ -211,8 +211,7 @@ template <bool HAS_IDX, bool VEC>
 __global__ __launch_bounds__(STHREADS, 2) void select_topk_kernel(
     const float* __restrict__ vals, const int64_t* __restrict__ idxs, int64_t ld, int64_t n,
     int64_t seg_len, int64_t idx_base, int kprime, float* __restrict__ out_vals,
-    int64_t* __restrict__ out_idx, int64_t ld_out, const int* __restrict__ row_cnt,
-    int64_t n_head, int cap) {
+    int64_t* __restrict__ out_idx, int64_t ld_out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const SelLayout Lo = sel_layout(kprime);
   uint32_t* bkey = (uint32_t*)(smem + Lo.off_key);
@@ -228,11 +227,6 @@ __global__ __launch_bounds__(STHREADS, 2) void select_topk_kernel(
   const int64_t s0 = (int64_t)seg * seg_len;
   int64_t s1 = s0 + seg_len;
   s1 = s1 < n ? s1 : n;
-  if (row_cnt) {  // candidate lists: a fixed head plus a counted (capped) tail per row
-    const int c = row_cnt[row];
-    const int64_t nr = n_head + (c < cap ? c : cap);
-    s1 = s1 < nr ? s1 : nr;
-  }
   const float* vrow = vals + row * ld;
   const int64_t* irow = HAS_IDX ? idxs + row * ld : nullptr;
 
@@ -355,8 +349,7 @@ size_t select_lds_bytes(int kprime) { return sel_layout(kprime).bytes; }
 
 static int select_launch(const float* vals, const int64_t* idx, int64_t ld, int64_t B,
                          int64_t n, int64_t idx_base, int32_t kprime, int32_t segs,
-                         float* out_vals, int64_t* out_idx, int64_t ld_out, const int* row_cnt,
-                         int64_t n_head, int cap, hipStream_t stream) {
+                         float* out_vals, int64_t* out_idx, int64_t ld_out, hipStream_t stream) {
   if (!vals || !out_vals || !out_idx || B < 0 || n < 0 || ld < n || segs < 1 || kprime < 1 ||
       kprime > KPRIME_MAX || ld_out < (int64_t)segs * kprime || n >= 0x7fffffffLL ||
       segs > 65535 || B > 0x7fffffffLL) {
@@ -375,8 +368,7 @@ static int select_launch(const float* vals, const int64_t* idx, int64_t ld, int6
   (void)hipFuncSetAttribute((const void*)select_topk_kernel<H, V>,                            \
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
   hipLaunchKernelGGL((select_topk_kernel<H, V>), grid, block, lds, stream, vals, idx, ld, n, \
-                     seg_len, idx_base, (int)kprime, out_vals, out_idx, ld_out, row_cnt,     \
-                     n_head, cap)
+                     seg_len, idx_base, (int)kprime, out_vals, out_idx, ld_out)
   if (idx) {
     if (vec) { EBT_SEL_LAUNCH(true, true); }
     else { EBT_SEL_LAUNCH(true, false); }
@@ -392,73 +384,143 @@ int select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B, in
                 int64_t idx_base, int32_t kprime, int32_t segs, float* out_vals,
                 int64_t* out_idx, int64_t ld_out, hipStream_t stream) {
   return select_launch(vals, idx, ld, B, n, idx_base, kprime, segs, out_vals, out_idx, ld_out,
-                       nullptr, 0, 0, stream);
+                       stream);
 }
 
-// Candidate-list select over rows made of a fixed head of n_head entries followed by a tail
-// whose valid length is min(row_cnt[b], cap) (the fused screen's appended candidates).
-int select_topk_counted(const float* vals, const int64_t* idx, int64_t ld, int64_t B,
-                        int64_t n_head, const int* row_cnt, int cap, int32_t kprime,
-                        float* out_vals, int64_t* out_idx, int64_t ld_out, hipStream_t stream) {
-  return select_launch(vals, idx, ld, B, n_head + cap, 0, kprime, 1, out_vals, out_idx, ld_out,
-                       row_cnt, n_head, cap, stream);
+// ---------------------------------------------------------------------------------------------
+// Fused screen, between segments. merge_segment: query b's list (its k' best so far, fv/fi
+// sorted) plus the hits the last filter GEMM left in its per-group slots (screen_gemm.hip,
+// EpiArgs) -> the k' best of both, written back over fv/fi. One workgroup per query: a block
+// scan of the group counts places every hit, excluded rows (lib.py:48,55: binary search of the
+// GLOBAL row in the query's sorted exclusion list) are dropped, and the union is sorted in LDS as
+// u64 composites (key desc, row asc -- the order select_topk_kernel produces). About 2k'
+// entries per query for a doubling segment. A slot overflow (count > SLOTS) or more hits than
+// the LDS holds sets ovf[b]: the query's certificate becomes -1 and it is rerun unfused.
+// ---------------------------------------------------------------------------------------------
+constexpr int MERGE_MAX = 16384;  // LDS entries (128 KiB)
+
+static int merge_entries(int kprime) {
+  int P = 2;
+  while (P < kprime + 4 * kprime + 2048 && P < MERGE_MAX) P <<= 1;
+  return P;
 }
 
-// ------------------------------------------------------------- fused-screen helpers -------
-// thr[b] = vals[b*ld + kprime-1]: the k'-th best approx score of the head chunk, a lower bound
-// of the query's global k'-th best (-inf when the head had fewer than k' valid rows).
-// Fused-screen bookkeeping between segments: thr[b] = the k'-th best approx score of the
-// candidate list so far (a lower bound of the global k'-th: the list is the top-k' of a subset of
-// the rows), padding queries +inf (they append nothing); ovf_max[b] = max count seen (a segment
-// whose count exceeded the capacity dropped candidates -> certified -1).
-__global__ void kth_threshold_kernel(const float* __restrict__ vals, int64_t ld, int64_t B,
-                                     int64_t B_pad, int kprime, float* __restrict__ thr,
-                                     const int* __restrict__ cnt, int* __restrict__ ovf_max) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (thr) {
-    if (b < B) thr[b] = vals[b * ld + kprime - 1];
-    else if (b < B_pad) thr[b] = __builtin_inff();
+__global__ __launch_bounds__(STHREADS) void merge_segment_kernel(
+    float* __restrict__ fv, int64_t* __restrict__ fi, int kprime,
+    const uint64_t* __restrict__ cand, int64_t ld_cand, const uint8_t* __restrict__ counts,
+    int64_t ld_counts, int n_groups, int P_max, int64_t row_offset,
+    const int64_t* __restrict__ eo, const int64_t* __restrict__ er, int* __restrict__ ovf) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t mkeep[];
+  __shared__ int wsum[STHREADS / 64];
+  __shared__ int flag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = blockIdx.x;
+  const uint8_t* cr = counts + b * ld_counts;
+  const uint64_t* cb = cand + b * ld_cand;
+  if (tid == 0) flag = 0;
+  // this thread's groups and hit count
+  const int per = (n_groups + STHREADS - 1) / STHREADS;
+  const int g0 = tid * per;
+  const int g1 = g0 + per < n_groups ? g0 + per : n_groups;
+  int mine = 0;
+  bool over = false;
+  for (int g = g0; g < g1; ++g) {
+    const int c = cr[g];
+    over |= c > EBT_FILTER_SLOTS;
+    mine += c < EBT_FILTER_SLOTS ? c : EBT_FILTER_SLOTS;
   }
-  if (cnt && b < B) ovf_max[b] = max(ovf_max[b], cnt[b]);
+  // block exclusive scan
+  int incl = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  int base = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < STHREADS / 64; ++w) {
+    base += w < wave ? wsum[w] : 0;
+    total += wsum[w];
+  }
+  int pos = base + incl - mine;
+  const int room = P_max - kprime;
+  if (total > room) over = true;
+  const int64_t elo = eo ? eo[b] : 0, ehi = eo ? eo[b + 1] : 0;
+  for (int g = g0; g < g1; ++g) {
+    int c = cr[g];
+    c = c < EBT_FILTER_SLOTS ? c : EBT_FILTER_SLOTS;
+    for (int p = 0; p < c; ++p, ++pos) {
+      uint64_t comp = cb[(int64_t)g * EBT_FILTER_SLOTS + p];
+      if (ehi > elo) {
+        const int64_t gr = (int64_t)(~(uint32_t)comp) + row_offset;
+        int64_t lo = elo, hi = ehi;
+        while (lo < hi) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (er[mid] < gr) lo = mid + 1;
+          else hi = mid;
+        }
+        if (lo < ehi && er[lo] == gr) comp = 0ull;
+      }
+      if (pos < room) mkeep[kprime + pos] = comp;
+    }
+  }
+  for (int i = tid; i < kprime; i += STHREADS) {
+    const uint32_t key = f2key(fv[b * kprime + i]);
+    const int64_t ix = fi[b * kprime + i];
+    mkeep[i] = (key != 0u && ix >= 0) ? (((uint64_t)key << 32) | (uint64_t)(~(uint32_t)ix)) : 0ull;
+  }
+  if (over) flag = 1;
+  const int used = kprime + (total < room ? total : room);
+  int P = 2;
+  while (P < used) P <<= 1;
+  for (int i = used + tid; i < P; i += STHREADS) mkeep[i] = 0ull;
+  __syncthreads();
+  bitonic_desc(mkeep, P);
+  for (int i = tid; i < kprime; i += STHREADS) {
+    const uint64_t comp = mkeep[i];
+    const uint32_t key = (uint32_t)(comp >> 32);
+    fv[b * kprime + i] = key ? key2f(key) : -__builtin_inff();
+    fi[b * kprime + i] = key ? (int64_t)(~(uint32_t)comp) : -1;
+  }
+  if (tid == 0 && flag) ovf[b] = 1;
+}
+
+int merge_segment(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t* cand,
+                  int64_t ld_cand, const uint8_t* counts, int64_t ld_counts, int64_t n_groups,
+                  int64_t row_offset, const int64_t* eo, const int64_t* er, int* ovf,
+                  hipStream_t st) {
+  if (B < 0 || B > 0x7fffffffLL || kprime < 1 || kprime > KPRIME_MAX || n_groups < 1 ||
+      n_groups > 0x7fffffffLL || ld_counts < n_groups ||
+      ld_cand < n_groups * EBT_FILTER_SLOTS) {
+    set_error("merge_segment: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  const int P_max = merge_entries(kprime);
+  const size_t lds = (size_t)P_max * 8;
+  (void)hipFuncSetAttribute((const void*)merge_segment_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(merge_segment_kernel, dim3((unsigned)B), dim3(STHREADS), lds, st, fv, fi,
+                     kprime, cand, ld_cand, counts, ld_counts, (int)n_groups, P_max, row_offset,
+                     eo, er, ovf);
+  return launch_check("merge_segment_kernel");
+}
+
+// thr[b] = the k'-th best approx score of query b's list so far: a lower bound of its global
+// k'-th best (the list is the top-k' of a subset of the rows); padding queries +inf (no hits).
+__global__ void kth_threshold_kernel(const float* __restrict__ vals, int64_t ld, int64_t B,
+                                     int64_t B_pad, int kprime, float* __restrict__ thr) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) thr[b] = vals[b * ld + kprime - 1];
+  else if (b < B_pad) thr[b] = __builtin_inff();
 }
 int kth_threshold(const float* vals, int64_t ld, int64_t B, int64_t B_pad, int kprime,
-                  float* thr, const int* cnt, int* ovf_max, hipStream_t st) {
+                  float* thr, hipStream_t st) {
   hipLaunchKernelGGL(kth_threshold_kernel, dim3((unsigned)ceil_div(B_pad, 256)), dim3(256), 0,
-                     st, vals, ld, B, B_pad, kprime, thr, cnt, ovf_max);
+                     st, vals, ld, B, B_pad, kprime, thr);
   return launch_check("kth_threshold_kernel");
-}
-
-// Excluded rows among appended candidates (lib.py:48,55): binary search of each candidate's
-// GLOBAL row in the query's exclusion list (sorted ascending); hits become -inf.
-__global__ __launch_bounds__(256) void mask_candidates_kernel(
-    float* __restrict__ cand_v, const int64_t* __restrict__ cand_i, int64_t ld, int64_t off,
-    const int* __restrict__ cnt, int cap, int64_t row_offset, const int64_t* __restrict__ eo,
-    const int64_t* __restrict__ er) {
-  const int64_t b = blockIdx.x;
-  const int64_t lo0 = eo[b], hi0 = eo[b + 1];
-  if (hi0 <= lo0) return;
-  int c = cnt[b];
-  c = c < cap ? c : cap;
-  for (int j = threadIdx.x; j < c; j += blockDim.x) {
-    const int64_t o = b * ld + off + j;
-    const int64_t g = cand_i[o] + row_offset;
-    int64_t lo = lo0, hi = hi0;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (er[mid] < g) lo = mid + 1;
-      else hi = mid;
-    }
-    if (lo < hi0 && er[lo] == g) cand_v[o] = -__builtin_inff();
-  }
-}
-
-int mask_candidates(float* cand_v, const int64_t* cand_i, int64_t ld, int64_t off, int64_t B,
-                    const int* cnt, int cap, int64_t row_offset, const int64_t* eo,
-                    const int64_t* er, hipStream_t st) {
-  if (B == 0) return EBT_OK;
-  hipLaunchKernelGGL(mask_candidates_kernel, dim3((unsigned)B), dim3(256), 0, st, cand_v, cand_i,
-                     ld, off, cnt, cap, row_offset, eo, er);
-  return launch_check("mask_candidates_kernel");
 }
 
 }  // namespace ebt

@@ -167,7 +167,8 @@ def _chunk_rows(catalog: Catalog, B_pad: int, budget: int) -> int:
 def plan(catalog: Catalog, B: int, k: int, kprime: Optional[int] = None,
          chunk_rows: Optional[int] = None, fuse: bool = True) -> dict:
     """How score_topk will run a batch of B queries (ebt_cosine_topk_plan): k', fused or not,
-    head rows (screened through the materialised-score path), candidate capacity, chunk rows."""
+    head rows (screened through the materialised-score path), largest fused tail segment (rows),
+    chunk rows."""
     import ctypes
     B_pad = pad_batch(B)
     k_eff = min(k, catalog.n)
@@ -180,7 +181,7 @@ def plan(catalog: Catalog, B: int, k: int, kprime: Optional[int] = None,
          0 if fuse else _lib.EBT_FLAG_NO_FUSE, ctypes.byref(h), ctypes.byref(c), ctypes.byref(ch),
          ctypes.byref(f))
     return {"kprime": kp, "B_pad": B_pad, "fused": bool(f.value), "head_rows": h.value,
-            "cap": c.value, "chunk_rows": ch.value}
+            "segment_rows_max": c.value, "chunk_rows": ch.value}
 
 
 def run_pipeline(catalog: Catalog, qb: QueryBatch, k: int, kprime: int,

@@ -40,26 +40,28 @@ def bench_gemm(dev, B, N, d, dt):
     ms = timeit(lambda: L.call("ebt_screen_scores", L.ptr(q), B, L.ptr(c), N, d, d, code,
                                L.ptr(qs), None, L.ptr(S), N, st))
     tf = 2.0 * B * N * d / (ms * 1e-3) / 1e12
-    # fused-screen (filter) epilogue: threshold high enough that ~0.3% of scores are appended
+    # fused-screen (filter) epilogue: threshold high enough that ~0.3% of scores are kept
     thr = torch.full((B,), 0.0, device=dev)
     thr[:] = 3.0 * (d ** 0.5)  # raw (unnormalised) Gaussian dot products: ~3 sigma
-    if os.environ.get("EBT_KB_THR") == "inf":  # no appends at all (ablation runs)
+    if os.environ.get("EBT_KB_THR") == "inf":  # no hits at all (ablation runs)
         thr[:] = float("inf")
-    cap = 8192
-    cnt = torch.zeros(B, dtype=torch.int32, device=dev)
-    cv = torch.empty((B, cap), device=dev)
-    ci = torch.empty((B, cap), dtype=torch.int64, device=dev)
+    G = L.load().ebt_filter_group_rows(B)
+    groups = (N + G - 1) // G
+    cand = torch.empty((B, groups * L.EBT_FILTER_SLOTS), dtype=torch.int64, device=dev)
+    counts = torch.empty((B, groups), dtype=torch.uint8, device=dev)
+    ovf = torch.zeros(B, dtype=torch.int32, device=dev)
 
     def run_filter():
-        cnt.zero_()
         L.call("ebt_screen_filter", L.ptr(q), B, L.ptr(c), N, d, d, code, L.ptr(qs), None,
-               L.ptr(thr), L.ptr(cnt), L.ptr(cv), L.ptr(ci), cap, 0, cap, 0, st)
+               L.ptr(thr), L.ptr(cand), groups * L.EBT_FILTER_SLOTS, L.ptr(counts), groups,
+               L.ptr(ovf), 0, st)
     ms_f = timeit(run_filter)
     tf_f = 2.0 * B * N * d / (ms_f * 1e-3) / 1e12
     return {"kernel": "screen_gemm", "B": B, "N": N, "d": d, "dtype": str(dt), "ms": round(ms, 4),
             "tflops": round(tf, 1), "frac_2500": round(tf / 2500, 4),
             "filter_ms": round(ms_f, 4), "filter_tflops": round(tf_f, 1),
-            "mean_appended": round(float(cnt.float().mean()), 1)}
+            "mean_hits": round(float(counts.float().sum(1).mean()), 1),
+            "overflow": int(ovf.sum())}
 
 
 def bench_select(dev, B, n, kp):
@@ -81,6 +83,8 @@ def main():
     ap.add_argument("--select", action="store_true")
     ap.add_argument("--one", action="store_true", help="single C3-chunk GEMM config (profiling)")
     ap.add_argument("--shape", default="4096,262144,1536", help="B,N,d for --one")
+    ap.add_argument("--select-shapes", default=None,
+                    help="B,n,kprime;... for --select (default: the pipeline's shapes)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     L.load()
@@ -95,7 +99,10 @@ def main():
             res.append(bench_gemm(dev, B, N, d, dt))
             print(json.dumps(res[-1]), flush=True)
     if args.select or not args.gemm:
-        for (B, n, kp) in [(4096, 262144, 200), (4096, 262144, 104), (1024, 100000, 120)]:
+        shapes = [(4096, 262144, 200), (4096, 262144, 104), (1024, 100000, 120)]
+        if args.select_shapes:
+            shapes = [tuple(int(x) for x in t.split(",")) for t in args.select_shapes.split(";")]
+        for (B, n, kp) in shapes:
             res.append(bench_select(dev, B, n, kp))
             print(json.dumps(res[-1]), flush=True)
 
