@@ -109,19 +109,19 @@ int ebt_screen_scores(const void* qimg, int64_t B_pad, const void* cimg, int64_t
 
 /* The fused screen's GEMM: the same product, but only scores >= thr[b] leave the kernel.
  * Catalog rows are grouped by G = ebt_filter_group_rows(B_pad) (the kernel's tile: 256 rows
- * when B_pad % 256 == 0, else 128); the hits of query b in group g go to
- * cand[b*ld_cand + g*EBT_FILTER_SLOTS + p] (p < the group's count) as u64 composites
- * (order-preserving key of the f32 score << 32 | ~(uint32)(idx_base + local row)), and
- * counts[b*ld_counts + g] = the group's hit count (saturated at 255). A count above
- * EBT_FILTER_SLOTS drops hits and sets ovf[b] = 1. Buffers have B_pad rows, ld_cand >=
- * groups*EBT_FILTER_SLOTS, ld_counts >= groups; thr has B_pad entries (+inf for padding). */
-#define EBT_FILTER_SLOTS 16
+ * when B_pad % 256 == 0, else 128); the first `slots` hits of query b in group g go to
+ * cand[b*ld_cand + g*slots + p] as u64 composites (order-preserving key of the f32 score << 32 |
+ * ~(uint32)(idx_base + local row)), and counts[b*ld_counts + g] = the group's hit count
+ * (saturated at 255). A count above `slots` drops hits and sets ovf[b] = 1. Buffers have B_pad
+ * rows, 1 <= slots <= EBT_FILTER_SLOTS_MAX, ld_cand >= groups*slots, ld_counts >= groups; thr
+ * has B_pad entries (+inf for padding). */
+#define EBT_FILTER_SLOTS_MAX 128
 int64_t ebt_filter_group_rows(int64_t B_pad);
 int ebt_screen_filter(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
                       int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
                       const float* cscale, const float* thr, uint64_t* cand, int64_t ld_cand,
-                      uint8_t* counts, int64_t ld_counts, int32_t* ovf, int64_t idx_base,
-                      void* stream);
+                      int32_t slots, uint8_t* counts, int64_t ld_counts, int32_t* ovf,
+                      int64_t idx_base, void* stream);
 
 /* Excluded rows (lib.py:48,55: rated movies are not candidates): for every b < B and every
  * GLOBAL row g in excl_rows[excl_off[b] .. excl_off[b+1]) with col_begin <= g < col_end,
@@ -147,12 +147,24 @@ int ebt_select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B
  * slots NaN / -1). certified[b] = 1 iff the candidate set provably contains the exact top-k:
  * kprime >= n_rows (every row is a candidate),
  * fewer than kprime valid candidates, or approx[kprime-1] < approx[k-1] - 2*eps[b].
+ * n_rows is the catalog's row count; a candidate row >= n_rows is never read and gives
+ * certified[b] = -2 (corrupt candidate list).
  * Candidates with approx < approx[k-1] - 2*eps[b] cannot be in the top k and are not gathered
  * (equal cand_vals and eps = 0 rescore every candidate). */
 int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype, int64_t ld,
                 const double* gnorm64, int64_t row_offset, const float* cand_vals,
                 const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
                 double* out_scores, int64_t* out_rows, int32_t* certified, void* stream);
+
+/* The fused screen's merge step: query b's list (fv/fi[b*kprime + j], sorted desc as
+ * ebt_select_topk leaves it) and the hits ebt_screen_filter left in `n_groups` groups of
+ * cand/counts (same slots/ld as that call) -> the kprime best of both, back into fv/fi.
+ * Exclusions (GLOBAL rows, CSR sorted per query, or NULL) are dropped from the hits; a group
+ * count above `slots`, or more hits than the merge holds, sets ovf[b] = 1. */
+int ebt_merge_hits(float* fv, int64_t* fi, int64_t B, int32_t kprime, const uint64_t* cand,
+                   int64_t ld_cand, int32_t slots, const uint8_t* counts, int64_t ld_counts,
+                   int64_t n_groups, int64_t row_offset, const int64_t* excl_off,
+                   const int64_t* excl_rows, int32_t* ovf, void* stream);
 
 /* Merge R partial top-k lists (scores/rows [R][B][k], each sorted) into the global top-k per
  * query -- the post-all-gather step of a row-sharded catalog. R*k <= 8192. */

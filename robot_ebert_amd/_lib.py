@@ -22,7 +22,7 @@ DTYPE_CODE = {torch.float32: EBT_F32, torch.bfloat16: EBT_BF16, torch.float16: E
 STAGES = {"gemm": 0, "mask": 1, "select": 2, "merge_select": 3, "rescore": 4, "gemm_filter": 5}
 EBT_FLAG_NO_FUSE = 1
 EBT_FLAG_EXACT = 2
-EBT_FILTER_SLOTS = 16
+EBT_FILTER_SLOTS_MAX = 128
 
 
 class EbertError(RuntimeError):
@@ -44,9 +44,11 @@ _SIGNATURES = {
                          _VP], _INT),
     "ebt_screen_scores": ([_VP, _I64, _VP, _I64, _I32, _I32, _INT, _VP, _VP, _VP, _I64, _VP],
                           _INT),
-    "ebt_screen_filter": ([_VP, _I64, _VP, _I64, _I32, _I32, _INT, _VP, _VP, _VP, _VP, _I64, _VP,
-                           _I64, _VP, _I64, _VP], _INT),
+    "ebt_screen_filter": ([_VP, _I64, _VP, _I64, _I32, _I32, _INT, _VP, _VP, _VP, _VP, _I64, _I32,
+                           _VP, _I64, _VP, _I64, _VP], _INT),
     "ebt_filter_group_rows": ([_I64], _I64),
+    "ebt_merge_hits": ([_VP, _VP, _I64, _I32, _VP, _I64, _I32, _VP, _I64, _I64, _I64, _VP, _VP, _VP,
+                        _VP], _INT),
     "ebt_mask_excluded": ([_VP, _I64, _I64, _I64, _I64, _VP, _VP, _VP], _INT),
     "ebt_select_topk": ([_VP, _VP, _I64, _I64, _I64, _I64, _I32, _I32, _VP, _VP, _I64, _VP],
                         _INT),

@@ -48,13 +48,22 @@ int rescore(const double*, int64_t, int32_t, const void*, int, int64_t, const do
             const float*, const int64_t*, int32_t, int32_t, int64_t, const float*, double*, int64_t*,
             int32_t*, hipStream_t, const int*, int);
 int screen_gemm_filter(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
-                       const float*, const float*, const float*, uint64_t*, int64_t, uint8_t*,
-                       int64_t, int*, int64_t, hipStream_t);
+                       const float*, const float*, const float*, uint64_t*, int64_t, int,
+                       uint8_t*, int64_t, int*, int64_t, hipStream_t);
 int64_t filter_group_rows(int64_t);
 
-int kth_threshold(const float*, int64_t, int64_t, int64_t, int, float*, hipStream_t);
-int merge_segment(float*, int64_t*, int64_t, int, const uint64_t*, int64_t, const uint8_t*,
+int kth_threshold(const float*, int64_t, int64_t, int64_t, int, const float*, float*,
+                  hipStream_t);
+int merge_segment(float*, int64_t*, int64_t, int, const uint64_t*, int64_t, int, const uint8_t*,
                   int64_t, int64_t, int64_t, const int64_t*, const int64_t*, int*, hipStream_t);
+bool merge_wave_fits(int);
+int merge_wave_capacity();
+int64_t merge_wave_max_groups();
+int merge_segment_wave(float*, int64_t*, int64_t, int, const uint64_t*, int64_t, int,
+                       const uint8_t*, int64_t, int64_t, int64_t, const int64_t*, const int64_t*,
+                       int*, hipStream_t);
+int pilot_topk(const float*, int64_t, int64_t, int, int64_t, int, float*, int64_t*, hipStream_t);
+constexpr int64_t PILOT_ROWS = 1024;  // = WMERGE_H (select_topk.hip)
 int merge_topk(const double*, const int64_t*, int32_t, int64_t, int32_t, double*, int64_t*,
                hipStream_t);
 int screen_exact(const double*, int64_t, int32_t, const void*, int, int64_t, const double*, int64_t,
@@ -122,9 +131,9 @@ struct StageScope {
 //           [B][kprime + cap] (head top-k' then appended tail candidates), counters and
 //           thresholds. The tail rows [H, n) never materialise scores.
 struct WsLayout {
-  int64_t chunk, ld_s, n_chunks, head, seg_max, groups_max, group_rows, ld_cand, ld_counts;
+  int64_t chunk, ld_s, n_chunks, head, seg_max, group_rows, ld_cand, ld_counts;
   int segs;
-  bool fused;
+  bool fused, pilot;
   size_t off_s, off_segv, off_segi, off_chv, off_chi, off_fv, off_fi, off_cand, off_counts,
       off_thr, off_ovf, off_eps, bytes;
 };
@@ -134,28 +143,33 @@ static size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
                           int64_t chunk_rows, int flags) {
   WsLayout L{};
-  // fused screen: the head H rows, processed unfused, give each query its first threshold; the
-  // tail is filtered inside the GEMM epilogue in doubling segments (each as large as all rows
-  // before it, so ~k' hits per query per segment), capped so the per-group hit slots
-  // (B_pad x groups x EBT_FILTER_SLOTS u64) stay within 1 GiB.
+  // fused screen: the head rows give each query its first list and threshold; the tail is
+  // filtered inside the GEMM epilogue in doubling segments (each as large as all rows before
+  // it, so ~k' hits per query per segment), capped so the per-group hit slots
+  // (B_pad x groups x slots u64) stay within 1 GiB. For k' <= 512 the head is a
+  // 1024-row PILOT (scores sorted per query by one wave); larger k' take H = max(65536, 256 k')
+  // rows through the streaming select.
   static const int64_t h_min = [] {
     const char* v = getenv("EBT_FUSE_HEAD");
     return v ? atoll(v) : 65536LL;
   }();
+  L.pilot = merge_wave_fits(kprime);
   int64_t H = 256LL * kprime;
   H = H < h_min ? h_min : H;
   H = (H + 255) / 256 * 256;
+  if (L.pilot) H = PILOT_ROWS;
   L.fused = !(flags & (EBT_FLAG_NO_FUSE | EBT_FLAG_EXACT)) && n_rows >= 2 * H;
   L.head = L.fused ? H : n_rows;
   if (L.fused) {
+    // hit slots: up to 1 GiB of u64 per call, never more than the whole tail at the minimum of
+    // 16 slots per group (plus the pilot segment's few groups at up to 128 slots)
     L.group_rows = filter_group_rows(B_pad);
-    int64_t gmax = (1LL << 30) / (B_pad * EBT_FILTER_SLOTS * 8);
-    gmax = gmax < 16 ? 16 : gmax;
-    const int64_t need = ceil_div(n_rows - H, L.group_rows);
-    L.groups_max = gmax < need ? gmax : need;
-    L.seg_max = L.groups_max * L.group_rows;
-    L.ld_cand = L.groups_max * EBT_FILTER_SLOTS;
-    L.ld_counts = (L.groups_max + 15) / 16 * 16;
+    const int64_t budget = (1LL << 30) / (B_pad * 8);
+    const int64_t need = ceil_div(n_rows - H, L.group_rows) * 16 + 8 * EBT_FILTER_SLOTS_MAX;
+    L.ld_cand = budget < need ? budget : need;
+    L.ld_cand = L.ld_cand < 8 * EBT_FILTER_SLOTS_MAX ? 8 * EBT_FILTER_SLOTS_MAX : L.ld_cand;
+    L.seg_max = L.ld_cand / 16 * L.group_rows;
+    L.ld_counts = (L.ld_cand / 16 + 15) / 16 * 16;
   }
   L.chunk = chunk_rows < L.head ? chunk_rows : L.head;
   if (L.chunk < 1) L.chunk = 1;
@@ -318,10 +332,10 @@ int64_t ebt_filter_group_rows(int64_t B_pad) { return filter_group_rows(B_pad); 
 int ebt_screen_filter(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
                       int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
                       const float* cscale, const float* thr, uint64_t* cand, int64_t ld_cand,
-                      uint8_t* counts, int64_t ld_counts, int32_t* ovf, int64_t idx_base,
-                      void* stream) {
+                      int32_t slots, uint8_t* counts, int64_t ld_counts, int32_t* ovf,
+                      int64_t idx_base, void* stream) {
   return screen_gemm_filter(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale, cscale,
-                            thr, cand, ld_cand, counts, ld_counts, ovf, idx_base,
+                            thr, cand, ld_cand, slots, counts, ld_counts, ovf, idx_base,
                             (hipStream_t)stream);
 }
 
@@ -352,6 +366,22 @@ int ebt_screen_exact(const double* q64, int64_t B, int32_t d, const void* cat, i
                      int64_t ld_scores, void* stream) {
   return screen_exact(q64, B, d, cat, dtype, ld, gnorm64, n_rows, scores, ld_scores,
                       (hipStream_t)stream);
+}
+
+int ebt_merge_hits(float* fv, int64_t* fi, int64_t B, int32_t kprime, const uint64_t* cand,
+                   int64_t ld_cand, int32_t slots, const uint8_t* counts, int64_t ld_counts,
+                   int64_t n_groups, int64_t row_offset, const int64_t* excl_off,
+                   const int64_t* excl_rows, int32_t* ovf, void* stream) {
+  if (!fv || !fi || !cand || !counts || !ovf || ((excl_off == nullptr) != (excl_rows == nullptr))) {
+    set_error("ebt_merge_hits: null pointer");
+    return EBT_EINVAL;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if (merge_wave_fits(kprime) && n_groups <= merge_wave_max_groups() && ld_counts % 16 == 0)
+    return merge_segment_wave(fv, fi, B, kprime, cand, ld_cand, slots, counts, ld_counts,
+                              n_groups, row_offset, excl_off, excl_rows, ovf, st);
+  return merge_segment(fv, fi, B, kprime, cand, ld_cand, slots, counts, ld_counts, n_groups,
+                       row_offset, excl_off, excl_rows, ovf, st);
 }
 
 int ebt_merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, int32_t k,
@@ -444,8 +474,25 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
   float* thr = (float*)(ws + L.off_thr);
   int* ovf = (int*)(ws + L.off_ovf);
   // 1. head rows [0, H): exact top-k' per query (the list fv/fi)
-  rc = head_topk(L, ws, qimg, qscale, B, B_pad, cimg, cscale, img_dtype, ld_img, 0, L.head, d_pad,
-                 row_offset, excl_off, excl_rows, kprime, fv, fi, kprime, timer, st);
+  if (L.pilot) {
+    float* S = (float*)(ws + L.off_s);
+    {
+      StageScope s(timer, EBT_STAGE_GEMM, st);
+      rc = screen_gemm(qimg, B_pad, cimg, L.head, d_pad, ld_img, img_dtype, qscale, cscale, S,
+                       L.ld_s, st);
+    }
+    if (rc) return rc;
+    if (excl_off) {
+      StageScope s(timer, EBT_STAGE_MASK, st);
+      rc = mask_excluded(S, L.ld_s, B, row_offset, row_offset + L.head, excl_off, excl_rows, st);
+      if (rc) return rc;
+    }
+    StageScope s(timer, EBT_STAGE_SELECT, st);
+    rc = pilot_topk(S, L.ld_s, B, (int)L.head, 0, kprime, fv, fi, st);
+  } else {
+    rc = head_topk(L, ws, qimg, qscale, B, B_pad, cimg, cscale, img_dtype, ld_img, 0, L.head,
+                   d_pad, row_offset, excl_off, excl_rows, kprime, fv, fi, kprime, timer, st);
+  }
   if (rc) return rc;
   rc = hip_check(hipMemsetAsync(ovf, 0, (size_t)B_pad * 4, st), "hipMemsetAsync");
   if (rc) return rc;
@@ -453,22 +500,43 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
   //    filter epilogue, merge of list + hits (exclusions dropped) back into the list
   int64_t r0 = L.head;
   while (r0 < n_rows) {
-    int64_t seg = n_rows - r0 < r0 ? n_rows - r0 : r0;
-    if (n_rows - (r0 + seg) < seg / 2) seg = n_rows - r0;  // no small last segment
-    seg = seg < L.seg_max ? seg : L.seg_max;
-    rc = kth_threshold(fv, kprime, B, B_pad, kprime, thr, st);
+    // hits per group ~ G k' / r0 when the segment's rows are like the r0 before it: slots for
+    // 4x that (+8), so a group overflows (-> unfused rerun of the query) only on skewed data
+    const double per_group = (double)L.group_rows * kprime / (double)r0;
+    int slots = 16;
+    while (slots < 4.0 * per_group + 8.0 && slots < EBT_FILTER_SLOTS_MAX) slots *= 2;
+    // segment = GROW x the rows so far: ~GROW k' hits per query at most (the threshold sits 2 eps
+    // below the list's k-th best, so typically ~GROW (k + the 2 eps band)); the wave merge holds
+    // 1024 hits, the block merge 4 k' + 2048
+    int64_t grow = 2;
+    if (L.pilot) {  // the wave merge holds k' + hits <= its capacity
+      grow = (merge_wave_capacity() - kprime) / kprime;
+      grow = grow < 1 ? 1 : (grow > 3 ? 3 : grow);
+    }
+    int64_t seg = n_rows - r0 < grow * r0 ? n_rows - r0 : grow * r0;
+    if (n_rows - (r0 + seg) < seg / 2 && n_rows - r0 <= (grow + 1) * r0)
+      seg = n_rows - r0;  // no small last segment
+    int64_t seg_cap = L.ld_cand / slots * L.group_rows;
+    if (L.pilot && seg_cap > merge_wave_max_groups() * L.group_rows)
+      seg_cap = merge_wave_max_groups() * L.group_rows;
+    seg = seg < seg_cap ? seg : seg_cap;
+    const int64_t groups = ceil_div(seg, L.group_rows);
+    rc = kth_threshold(fv, kprime, B, B_pad, k, eps, thr, st);
     if (rc) return rc;
     {
       StageScope s(timer, EBT_STAGE_GEMM_FILTER, st);
       rc = screen_gemm_filter(qimg, B_pad, (const char*)cimg + r0 * ld_img * 2, seg, d_pad,
                               ld_img, img_dtype, qscale, cscale ? cscale + r0 : nullptr, thr,
-                              cand, L.ld_cand, counts, L.ld_counts, ovf, r0, st);
+                              cand, L.ld_cand, slots, counts, L.ld_counts, ovf, r0, st);
     }
     if (rc) return rc;
     {
       StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
-      rc = merge_segment(fv, fi, B, kprime, cand, L.ld_cand, counts, L.ld_counts,
-                         ceil_div(seg, L.group_rows), row_offset, excl_off, excl_rows, ovf, st);
+      rc = L.pilot ? merge_segment_wave(fv, fi, B, kprime, cand, L.ld_cand, slots, counts,
+                                        L.ld_counts, groups, row_offset, excl_off, excl_rows, ovf,
+                                        st)
+                   : merge_segment(fv, fi, B, kprime, cand, L.ld_cand, slots, counts,
+                                   L.ld_counts, groups, row_offset, excl_off, excl_rows, ovf, st);
     }
     if (rc) return rc;
     r0 += seg;

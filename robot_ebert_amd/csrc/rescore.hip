@@ -60,10 +60,13 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
   double* qs = (double*)smem;                 // d
   double* sc = qs + ((d + 1) & ~1);           // kpp
   int64_t* rw = (int64_t*)(sc + kpp);         // kpp
-  __shared__ int nvalid;
+  __shared__ int nvalid, corrupt;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
-  if (tid == 0) nvalid = 0;
+  if (tid == 0) {
+    nvalid = 0;
+    corrupt = 0;
+  }
   for (int j = tid; j < d; j += RTHREADS) qs[j] = q64[b * d + j];
   __syncthreads();
   const int64_t* cr = cand_rows + b * kprime;
@@ -74,7 +77,8 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
   const double cut = (double)cv[k - 1] - 2.0 * (double)eps[b];
   int myvalid = 0;
   for (int c = wave; c < kprime; c += RTHREADS / 64) {
-    const int64_t row = cr[c];
+    const int64_t row = cr[c] < n_rows ? cr[c] : -2;  // -2: corrupt entry, never dereferenced
+    if (row == -2 && lane == 0) corrupt = 1;
     const bool skip = (double)cv[c] < cut;
     double s = 0.0;
     if (row >= 0 && !skip) {
@@ -141,6 +145,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
       ok = amin < T - 2.0 * (double)eps[b];
     }
     if (ovf_cnt && ovf_cnt[b] > ovf_cap) ok = -1;  // fused screen dropped candidates
+    if (corrupt) ok = -2;                           // internal error: row out of range
     certified[b] = ok;
   }
 }

@@ -75,11 +75,10 @@ __device__ __forceinline__ f32x4_t mfma16(const u16x8_t& a, const u16x8_t& b, f3
 // the query's k'-th best approx score, so no candidate of the true top-k' is ever filtered.
 // Filter-mode output (the fused screen): catalog rows are grouped by the kernel's tile
 // (FILTER_GROUP rows: 256 for the quadrant-phase kernel, 128 for the small-batch one); for query
-// q and group g, up to EBT_FILTER_SLOTS hits go to cand[q*ld_cand + g*SLOTS + p] as u64
+// q and group g, up to `slots` hits go to cand[q*ld_cand + g*slots + p] as u64
 // composites (f2key(score) << 32 | ~row, row = idx_base + local row) and the group's hit count to
-// counts[q*ld_counts + g] (saturated at 255; > SLOTS sets ovf[q]). Slots are claimed with LDS
+// counts[q*ld_counts + g] (saturated at 255; > slots sets ovf[q]). Slots are claimed with LDS
 // atomics per workgroup tile, so the epilogue does no global atomics and no dependent loads.
-constexpr int FILTER_SLOTS = EBT_FILTER_SLOTS;
 
 struct EpiArgs {
   float* S;  // store mode
@@ -91,6 +90,7 @@ struct EpiArgs {
   int64_t ld_counts;
   int* ovf;
   int64_t idx_base;
+  int slots;
 };
 
 template <bool FILTER>
@@ -142,9 +142,9 @@ __device__ __forceinline__ void epilogue4(const EpiArgs& e, int64_t q, int64_t i
         const int64_t i = i0 + r;
         if (i < n_rows && v[r] >= th) {
           const uint32_t p = atomicAdd(lcnt, 1u);
-          if (p < (uint32_t)FILTER_SLOTS) {
+          if (p < (uint32_t)e.slots) {
             const uint32_t row = (uint32_t)(e.idx_base + i);
-            e.cand[q * e.ld_cand + grp * FILTER_SLOTS + p] =
+            e.cand[q * e.ld_cand + grp * e.slots + p] =
                 ((uint64_t)f2key(v[r]) << 32) | (uint64_t)(~row);
           }
         }
@@ -162,7 +162,7 @@ __device__ __forceinline__ void filter_finish(const EpiArgs& e, const uint32_t* 
     const uint32_t c = lcnt[t];
     const int64_t q = q0 + t;
     e.counts[q * e.ld_counts + grp] = (uint8_t)(c < 255u ? c : 255u);
-    if (c > (uint32_t)FILTER_SLOTS) e.ovf[q] = 1;
+    if (c > (uint32_t)e.slots) e.ovf[q] = 1;
   }
 }
 
@@ -600,14 +600,15 @@ int64_t filter_group_rows(int64_t B_pad) { return B_pad % QP_TILE == 0 ? QP_TILE
 int screen_gemm_filter(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
                        int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
                        const float* cscale, const float* thr, uint64_t* cand, int64_t ld_cand,
-                       uint8_t* counts, int64_t ld_counts, int* ovf, int64_t idx_base,
+                       int slots, uint8_t* counts, int64_t ld_counts, int* ovf, int64_t idx_base,
                        hipStream_t stream) {
   int rc = check_gemm_args("ebt_screen_filter", qimg, B_pad, cimg, n_rows, d_pad, ld_img,
                            img_dtype, qscale, cscale);
   if (rc) return rc;
   const int64_t groups = ceil_div(n_rows, filter_group_rows(B_pad));
-  if (!thr || !cand || !counts || !ovf || ld_counts < groups ||
-      ld_cand < groups * FILTER_SLOTS || idx_base < 0 || idx_base + n_rows > 0xffffffffLL) {
+  if (!thr || !cand || !counts || !ovf || slots < 1 || slots > EBT_FILTER_SLOTS_MAX ||
+      ld_counts < groups || ld_cand < groups * slots || idx_base < 0 ||
+      idx_base + n_rows > 0xffffffffLL) {
     set_error("ebt_screen_filter: bad candidate buffers (groups=%lld ld_cand=%lld ld_counts=%lld)",
               (long long)groups, (long long)ld_cand, (long long)ld_counts);
     return EBT_EINVAL;
@@ -620,6 +621,7 @@ int screen_gemm_filter(const void* qimg, int64_t B_pad, const void* cimg, int64_
   e.ld_counts = ld_counts;
   e.ovf = ovf;
   e.idx_base = idx_base;
+  e.slots = slots;
   return launch_gemm<true>(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale, cscale,
                            e, stream);
 }

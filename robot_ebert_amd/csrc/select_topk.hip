@@ -407,8 +407,9 @@ static int merge_entries(int kprime) {
 
 __global__ __launch_bounds__(STHREADS) void merge_segment_kernel(
     float* __restrict__ fv, int64_t* __restrict__ fi, int kprime,
-    const uint64_t* __restrict__ cand, int64_t ld_cand, const uint8_t* __restrict__ counts,
-    int64_t ld_counts, int n_groups, int P_max, int64_t row_offset,
+    const uint64_t* __restrict__ cand, int64_t ld_cand, int slots,
+    const uint8_t* __restrict__ counts, int64_t ld_counts, int n_groups, int P_max,
+    int64_t row_offset,
     const int64_t* __restrict__ eo, const int64_t* __restrict__ er, int* __restrict__ ovf) {
   extern __shared__ __attribute__((aligned(16))) uint64_t mkeep[];
   __shared__ int wsum[STHREADS / 64];
@@ -426,8 +427,8 @@ __global__ __launch_bounds__(STHREADS) void merge_segment_kernel(
   bool over = false;
   for (int g = g0; g < g1; ++g) {
     const int c = cr[g];
-    over |= c > EBT_FILTER_SLOTS;
-    mine += c < EBT_FILTER_SLOTS ? c : EBT_FILTER_SLOTS;
+    over |= c > slots;
+    mine += c < slots ? c : slots;
   }
   // block exclusive scan
   int incl = mine;
@@ -450,9 +451,9 @@ __global__ __launch_bounds__(STHREADS) void merge_segment_kernel(
   const int64_t elo = eo ? eo[b] : 0, ehi = eo ? eo[b + 1] : 0;
   for (int g = g0; g < g1; ++g) {
     int c = cr[g];
-    c = c < EBT_FILTER_SLOTS ? c : EBT_FILTER_SLOTS;
+    c = c < slots ? c : slots;
     for (int p = 0; p < c; ++p, ++pos) {
-      uint64_t comp = cb[(int64_t)g * EBT_FILTER_SLOTS + p];
+      uint64_t comp = cb[(int64_t)g * slots + p];
       if (ehi > elo) {
         const int64_t gr = (int64_t)(~(uint32_t)comp) + row_offset;
         int64_t lo = elo, hi = ehi;
@@ -488,12 +489,13 @@ __global__ __launch_bounds__(STHREADS) void merge_segment_kernel(
 }
 
 int merge_segment(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t* cand,
-                  int64_t ld_cand, const uint8_t* counts, int64_t ld_counts, int64_t n_groups,
+                  int64_t ld_cand, int slots, const uint8_t* counts, int64_t ld_counts,
+                  int64_t n_groups,
                   int64_t row_offset, const int64_t* eo, const int64_t* er, int* ovf,
                   hipStream_t st) {
   if (B < 0 || B > 0x7fffffffLL || kprime < 1 || kprime > KPRIME_MAX || n_groups < 1 ||
       n_groups > 0x7fffffffLL || ld_counts < n_groups ||
-      ld_cand < n_groups * EBT_FILTER_SLOTS) {
+      ld_cand < n_groups * slots) {
     set_error("merge_segment: bad arguments");
     return EBT_EINVAL;
   }
@@ -503,23 +505,312 @@ int merge_segment(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t*
   (void)hipFuncSetAttribute((const void*)merge_segment_kernel,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(merge_segment_kernel, dim3((unsigned)B), dim3(STHREADS), lds, st, fv, fi,
-                     kprime, cand, ld_cand, counts, ld_counts, (int)n_groups, P_max, row_offset,
+                     kprime, cand, ld_cand, slots, counts, ld_counts, (int)n_groups, P_max,
+                     row_offset,
                      eo, er, ovf);
   return launch_check("merge_segment_kernel");
 }
 
-// thr[b] = the k'-th best approx score of query b's list so far: a lower bound of its global
-// k'-th best (the list is the top-k' of a subset of the rows); padding queries +inf (no hits).
-__global__ void kth_threshold_kernel(const float* __restrict__ vals, int64_t ld, int64_t B,
-                                     int64_t B_pad, int kprime, float* __restrict__ thr) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < B) thr[b] = vals[b * ld + kprime - 1];
-  else if (b < B_pad) thr[b] = __builtin_inff();
+// ---------------------------------------------------------------------------------------------
+// The same merge with ONE WAVE per query (4 queries per workgroup, no block barriers) while
+// k' + hits <= WTOP_N: the wave holds the union in registers (WTOP_E composites per lane),
+// finds the k'-th largest by a binary search on the 32-bit key (a second one on the row part
+// when the k'-th key is tied), compacts the k' winners into LDS with ballots and writes each to
+// its rank = the number of winners above it (a broadcast scan of the k' winners). No sort
+// network: ~1.5k VALU + k' LDS broadcast reads per lane. Input either the per-group hit slots
+// of the filter GEMM plus the list fv/fi, or (the fused screen's pilot) a dense score row with
+// implicit rows idx_base + j and no list.
+// ---------------------------------------------------------------------------------------------
+constexpr int WTOP_E = 16;            // composites per lane
+constexpr int WTOP_N = 64 * WTOP_E;   // union size per query
+constexpr int WMERGE_K = 512;         // largest k' (winners staged in LDS)
+constexpr int WMERGE_Q = STHREADS / 64;
+constexpr int WCNT = 4;               // 16-byte count loads per lane: n_groups <= 64 * 64
+
+// The k' largest of the wave's composites x (0 = empty), written in descending order to
+// ov/oi[0..kprime) (empty tail: -inf / -1). win: kprime u64 of LDS for this wave.
+template <int R>
+__device__ void wave_topk_write(const uint64_t (&x)[WTOP_E], int kprime, float* ov, int64_t* oi,
+                                uint64_t* win, int lane, uint32_t key_lo) {
+  int nvalid = 0;
+#pragma unroll
+  for (int j = 0; j < WTOP_E; ++j) nvalid += __popcll(__ballot(x[j] != 0ull));
+  const int want = nvalid < kprime ? nvalid : kprime;
+  // selected: composite >= (t << 32 | u); t = the want-th largest key, u = the row part cut
+  uint32_t t = 0u, u = 0u;
+  if (want > 0) {
+    // t = largest key with count(key >= t) >= want, searched in [key_lo, max key]: key_lo is a
+    // known lower bound (the list's k'-th key), which leaves ~20 steps for float keys
+    uint32_t kmax = 0u;
+#pragma unroll
+    for (int j = 0; j < WTOP_E; ++j) kmax = max(kmax, (uint32_t)(x[j] >> 32));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+    uint64_t lo = key_lo > 1u ? key_lo : 1u, hi = kmax;
+    if (lo > hi) lo = hi;
+    while (lo < hi) {
+      const uint64_t mid = lo + ((hi - lo + 1) >> 1);
+      int c = 0;  // ballot counts: scalar popcounts, no cross-lane data movement
+#pragma unroll
+      for (int j = 0; j < WTOP_E; ++j) c += __popcll(__ballot((x[j] >> 32) >= mid));
+      if (c >= want) lo = mid;
+      else hi = mid - 1;
+    }
+    t = (uint32_t)lo;
+    int gt = 0, eq = 0;
+#pragma unroll
+    for (int j = 0; j < WTOP_E; ++j) {
+      gt += __popcll(__ballot((uint32_t)(x[j] >> 32) > t));
+      eq += __popcll(__ballot((uint32_t)(x[j] >> 32) == t));
+    }
+    const int need = want - gt;  // 1 <= need <= eq entries with key == t
+    if (need < eq) {  // a tie at the cut: order the tied entries by row (rare)
+      uint64_t lo2 = 0, hi2 = 0xffffffffull;  // largest u with count(key == t, low >= u) >= need
+      while (lo2 < hi2) {
+        const uint64_t mid = lo2 + ((hi2 - lo2 + 1) >> 1);
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < WTOP_E; ++j)
+          c += __popcll(
+              __ballot(((uint32_t)(x[j] >> 32) == t) && ((x[j] & 0xffffffffull) >= mid)));
+        if (c >= need) lo2 = mid;
+        else hi2 = mid - 1;
+      }
+      u = (uint32_t)lo2;
+    }
+  }
+  const uint64_t cut = ((uint64_t)t << 32) | u;
+  int base = 0;
+  const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int j = 0; j < WTOP_E; ++j) {
+    const bool sel = want > 0 && x[j] != 0ull && x[j] >= cut;
+    const uint64_t m = __ballot(sel);
+    if (sel) win[base + __popcll(m & below)] = x[j];
+    base += __popcll(m);
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const int nsel = base < want ? base : want;  // == want (composites are unique)
+  // rank of each winner = winners above it: every lane scans all winners (LDS broadcast reads,
+  // 8 per batch so the reads pipeline) against its own R (R * 64 >= k')
+  uint64_t mine[R];
+  int rank[R];
+#pragma unroll
+  for (int t2 = 0; t2 < R; ++t2) {
+    const int i = lane + 64 * t2;
+    mine[t2] = i < nsel ? win[i] : 0ull;
+    rank[t2] = 0;
+  }
+  for (int q = 0; q < nsel; q += 8) {
+    uint64_t w8[8];
+#pragma unroll
+    for (int u8 = 0; u8 < 8; ++u8) w8[u8] = q + u8 < nsel ? win[q + u8] : 0ull;
+#pragma unroll
+    for (int u8 = 0; u8 < 8; ++u8)
+#pragma unroll
+      for (int t2 = 0; t2 < R; ++t2) rank[t2] += w8[u8] > mine[t2];
+  }
+#pragma unroll
+  for (int t2 = 0; t2 < R; ++t2) {
+    const int i = lane + 64 * t2;
+    if (i < nsel) {
+      ov[rank[t2]] = key2f((uint32_t)(mine[t2] >> 32));
+      oi[rank[t2]] = (int64_t)(~(uint32_t)mine[t2]);
+    }
+  }
+  for (int i = nsel + lane; i < kprime; i += 64) {
+    ov[i] = -__builtin_inff();
+    oi[i] = -1;
+  }
 }
-int kth_threshold(const float* vals, int64_t ld, int64_t B, int64_t B_pad, int kprime,
-                  float* thr, hipStream_t st) {
+
+template <bool DENSE, int R>
+__global__ __launch_bounds__(STHREADS) void merge_wave_kernel(
+    float* __restrict__ fv, int64_t* __restrict__ fi, int64_t B, int kprime,
+    const uint64_t* __restrict__ cand, int64_t ld_cand, int slots,
+    const uint8_t* __restrict__ counts, int64_t ld_counts, int n_groups,
+    const float* __restrict__ dense, int64_t ld_dense, int n_dense, int64_t idx_base,
+    int64_t row_offset, const int64_t* __restrict__ eo, const int64_t* __restrict__ er,
+    int* __restrict__ ovf) {
+  __shared__ uint64_t stage[WMERGE_Q][WTOP_N];  // the union, then the winners
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b = (int64_t)blockIdx.x * WMERGE_Q + w;
+  if (b >= B) return;
+  uint64_t* U = stage[w];
+  uint64_t x[WTOP_E];
+  bool over = false;
+  uint32_t key_lo = 1u;  // the new k'-th key is >= the list's k'-th key
+  if constexpr (DENSE) {
+    const float* row = dense + b * ld_dense;
+#pragma unroll
+    for (int j = 0; j < WTOP_E; ++j) {
+      const int c = lane + 64 * j;
+      const uint32_t key = c < n_dense ? f2key(row[c]) : 0u;
+      x[j] = key ? (((uint64_t)key << 32) | (uint64_t)(~(uint32_t)(idx_base + c))) : 0ull;
+    }
+  } else {
+    const int64_t elo = eo ? eo[b] : 0, ehi = eo ? eo[b + 1] : 0;
+    auto excluded = [&](uint64_t comp) {
+      const int64_t gr = (int64_t)(~(uint32_t)comp) + row_offset;
+      int64_t lo = elo, hi = ehi;
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (er[mid] < gr) lo = mid + 1;
+        else hi = mid;
+      }
+      return lo < ehi && er[lo] == gr;
+    };
+    key_lo = f2key(fv[b * kprime + kprime - 1]);
+    // the list: U[0..kprime)
+    for (int i = lane; i < kprime; i += 64) {
+      const uint32_t key = f2key(fv[b * kprime + i]);
+      const int64_t ix = fi[b * kprime + i];
+      U[i] = (key != 0u && ix >= 0) ? (((uint64_t)key << 32) | (uint64_t)(~(uint32_t)ix)) : 0ull;
+    }
+    // the hits: U[kprime..), lane l owning groups [l*per, (l+1)*per), per a multiple of 16 so
+    // its counts arrive as up to WCNT independent 16-byte loads (ld_counts is a multiple of 16)
+    const uint8_t* cr = counts + b * ld_counts;
+    const uint64_t* cb = cand + b * ld_cand;
+    const int per = ((n_groups + 63) / 64 + 15) & ~15;
+    const int g0 = lane * per;
+    uint4 cv4[WCNT];
+#pragma unroll
+    for (int v = 0; v < WCNT; ++v) {
+      const int g = g0 + 16 * v;
+      cv4[v] = (16 * v < per && g < n_groups) ? *(const uint4*)(cr + g) : make_uint4(0, 0, 0, 0);
+    }
+    auto cnt_at = [&](int v, int e) -> int {  // count of group g0 + 16 v + e (0 past the end)
+      const uint32_t w4 = e < 4 ? cv4[v].x : e < 8 ? cv4[v].y : e < 12 ? cv4[v].z : cv4[v].w;
+      const int c = (int)((w4 >> (8 * (e & 3))) & 0xffu);
+      return g0 + 16 * v + e < n_groups ? c : 0;
+    };
+    int mine = 0;
+#pragma unroll
+    for (int v = 0; v < WCNT; ++v)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int c = cnt_at(v, e);
+        over |= c > slots;
+        mine += c < slots ? c : slots;
+      }
+    int incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    const int m = __shfl(incl, 63, 64);
+    if (kprime + m > WTOP_N) over = true;
+    // the hits, in two passes: each lane writes the slot index of its hits (LDS only, so the
+    // divergent per-group loop costs no memory latency), then the wave loads 64 hits at a time
+    int pos = kprime + incl - mine;
+    if (mine > 0) {
+#pragma unroll
+      for (int v = 0; v < WCNT; ++v)
+#pragma unroll 1
+        for (int e = 0; e < 16; ++e) {
+          int c = cnt_at(v, e);
+          c = c < slots ? c : slots;
+          const int64_t g = g0 + 16 * v + e;
+          for (int p = 0; p < c; ++p, ++pos)
+            if (pos < WTOP_N) U[pos] = (uint64_t)(g * slots + p);
+        }
+    }
+    const int mh = kprime + m < WTOP_N ? m : WTOP_N - kprime;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int h0 = 0; h0 < mh; h0 += 4 * 64) {
+      uint64_t comp[4];
+#pragma unroll
+      for (int u4 = 0; u4 < 4; ++u4) {
+        const int h = h0 + u4 * 64 + lane;
+        comp[u4] = h < mh ? cb[(int64_t)U[kprime + h]] : 0ull;
+      }
+#pragma unroll
+      for (int u4 = 0; u4 < 4; ++u4) {
+        const int h = h0 + u4 * 64 + lane;
+        if (h < mh) U[kprime + h] = (ehi > elo && excluded(comp[u4])) ? 0ull : comp[u4];
+      }
+    }
+    const int used = kprime + m < WTOP_N ? kprime + m : WTOP_N;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < WTOP_E; ++j) {
+      const int c = lane + 64 * j;
+      x[j] = c < used ? U[c] : 0ull;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  wave_topk_write<R>(x, kprime, fv + b * kprime, fi + b * kprime, U, lane, key_lo);
+  if (__ballot(over) != 0ull && lane == 0) ovf[b] = 1;
+}
+
+bool merge_wave_fits(int kprime) { return kprime <= WMERGE_K; }
+int64_t merge_wave_max_groups() { return 64 * 16 * WCNT; }
+int merge_wave_capacity() { return WTOP_N; }
+
+int merge_segment_wave(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t* cand,
+                       int64_t ld_cand, int slots, const uint8_t* counts, int64_t ld_counts,
+                       int64_t n_groups, int64_t row_offset, const int64_t* eo,
+                       const int64_t* er, int* ovf, hipStream_t st) {
+  if (B < 0 || kprime < 1 || kprime > WMERGE_K || n_groups < 1 || n_groups > 64 * 16 * WCNT ||
+      ld_counts < n_groups || ld_counts % 16 != 0 || ((uintptr_t)counts & 15) ||
+      ld_cand < n_groups * slots) {
+    set_error("merge_segment_wave: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  auto kern = kprime <= 256 ? merge_wave_kernel<false, 4> : merge_wave_kernel<false, 8>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)ceil_div(B, WMERGE_Q)), dim3(STHREADS), 0, st, fv, fi,
+                     B, kprime, cand, ld_cand, slots, counts, ld_counts, (int)n_groups, nullptr,
+                     0, 0, 0, row_offset, eo, er, ovf);
+  return launch_check("merge_wave_kernel");
+}
+
+// Top-k' of a dense score block (n <= WTOP_N columns per row; masked entries -inf): the fused
+// screen's pilot rows, straight into the list fv/fi.
+int pilot_topk(const float* S, int64_t ld_s, int64_t B, int n, int64_t idx_base, int kprime,
+               float* fv, int64_t* fi, hipStream_t st) {
+  if (B < 0 || n < 1 || n > WTOP_N || kprime < 1 || kprime > WMERGE_K || ld_s < n) {
+    set_error("pilot_topk: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  auto kern = kprime <= 256 ? merge_wave_kernel<true, 4> : merge_wave_kernel<true, 8>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)ceil_div(B, WMERGE_Q)), dim3(STHREADS), 0, st, fv, fi,
+                     B, kprime, nullptr, 0, 1, nullptr, 0, 0, S, ld_s, n, idx_base, 0, nullptr,
+                     nullptr, nullptr);
+  return launch_check("merge_wave_kernel");
+}
+
+// thr[b] for the next fused segment: the k-th best approx score of query b's list so far minus
+// 2 eps[b], rounded down. The list's k-th best only grows, so thr <= T - 2 eps for the FINAL
+// k-th best T: a row the filter drops (approx < thr) cannot be in the exact top k -- the
+// rescore's certificate covers it as it covers rows below the list's k'-th (rescore.hip).
+// Padding queries get +inf (no hits); a list with fewer than k entries gives -inf (keep all).
+__global__ void kth_threshold_kernel(const float* __restrict__ vals, int64_t ld, int64_t B,
+                                     int64_t B_pad, int k, const float* __restrict__ eps,
+                                     float* __restrict__ thr) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) {
+    const double t = (double)vals[b * ld + k - 1] - 2.0 * (double)eps[b];
+    float f = (float)t;
+    if ((double)f > t && f == f && f != -__builtin_inff()) {  // one float step down
+      const uint32_t u = __float_as_uint(f);
+      f = f == 0.f ? -__uint_as_float(1u) : __uint_as_float(f > 0.f ? u - 1u : u + 1u);
+    }
+    thr[b] = f;
+  } else if (b < B_pad) {
+    thr[b] = __builtin_inff();
+  }
+}
+int kth_threshold(const float* vals, int64_t ld, int64_t B, int64_t B_pad, int k,
+                  const float* eps, float* thr, hipStream_t st) {
   hipLaunchKernelGGL(kth_threshold_kernel, dim3((unsigned)ceil_div(B_pad, 256)), dim3(256), 0,
-                     st, vals, ld, B, B_pad, kprime, thr);
+                     st, vals, ld, B, B_pad, k, eps, thr);
   return launch_check("kth_threshold_kernel");
 }
 

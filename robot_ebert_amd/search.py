@@ -245,7 +245,9 @@ def score_topk(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
     # (cert -1: rerun unfused) or a candidate set that is not provably complete (cert 0: widen k')
     while True:
         flat = cert.cpu()
-        over = torch.nonzero(flat < 0).flatten().to(dev)
+        if bool((flat == -2).any()):
+            raise EbertError("internal error: candidate row out of range (libebert bug)")
+        over = torch.nonzero(flat == -1).flatten().to(dev)
         bad = torch.nonzero(flat == 0).flatten().to(dev)
         if over.numel() == 0 and bad.numel() == 0:
             break
@@ -308,6 +310,7 @@ def rescore_rows(catalog: Catalog, qb: QueryBatch, cand_rows: torch.Tensor
     out_r = torch.empty((B, m), dtype=torch.int64, device=dev)
     cert = torch.empty(B, dtype=torch.int32, device=dev)
     call("ebt_rescore", ptr(qb.q64), B, catalog.d, ptr(catalog.data), catalog.dtype_code,
-         catalog.ld, ptr(catalog.gnorm), catalog.row_offset, ptr(vals), ptr(local), m, m, m, ptr(eps),
+         catalog.ld, ptr(catalog.gnorm), catalog.row_offset, ptr(vals), ptr(local), m, m, catalog.n,
+         ptr(eps),
          ptr(out_s), ptr(out_r), ptr(cert), stream_of(dev))
     return out_s, out_r

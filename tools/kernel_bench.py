@@ -47,13 +47,14 @@ def bench_gemm(dev, B, N, d, dt):
         thr[:] = float("inf")
     G = L.load().ebt_filter_group_rows(B)
     groups = (N + G - 1) // G
-    cand = torch.empty((B, groups * L.EBT_FILTER_SLOTS), dtype=torch.int64, device=dev)
+    slots = 16
+    cand = torch.empty((B, groups * slots), dtype=torch.int64, device=dev)
     counts = torch.empty((B, groups), dtype=torch.uint8, device=dev)
     ovf = torch.zeros(B, dtype=torch.int32, device=dev)
 
     def run_filter():
         L.call("ebt_screen_filter", L.ptr(q), B, L.ptr(c), N, d, d, code, L.ptr(qs), None,
-               L.ptr(thr), L.ptr(cand), groups * L.EBT_FILTER_SLOTS, L.ptr(counts), groups,
+               L.ptr(thr), L.ptr(cand), groups * slots, slots, L.ptr(counts), groups,
                L.ptr(ovf), 0, st)
     ms_f = timeit(run_filter)
     tf_f = 2.0 * B * N * d / (ms_f * 1e-3) / 1e12
@@ -77,10 +78,41 @@ def bench_select(dev, B, n, kp):
             "GBps": round(gbs, 1), "frac_8000": round(gbs / 8000, 4)}
 
 
+def bench_merge(dev, B, kp, groups, hits, slots=16):
+    """ebt_merge_hits: a sorted k' list per query + `hits` hits spread over `groups` groups."""
+    g = torch.Generator(device=dev).manual_seed(0)
+    fv = torch.sort(torch.rand((B, kp), generator=g, device=dev), dim=1, descending=True)[0]
+    fi = torch.arange(kp, device=dev).repeat(B, 1) + 10_000_000
+    grp = torch.randint(0, groups, (B, hits), generator=g, device=dev)
+    counts = torch.zeros((B, (groups + 15) // 16 * 16), dtype=torch.uint8, device=dev)
+    ones = torch.ones_like(grp, dtype=torch.uint8)
+    counts.scatter_add_(1, grp, ones)
+    counts.clamp_(max=slots)
+    cand = torch.zeros((B, groups * slots), dtype=torch.int64, device=dev)
+    # composite: key of a score in [0,1) << 32 | ~row
+    key = (torch.rand((B, groups * slots), generator=g, device=dev) * 2**30).long() + 2**31
+    row = torch.arange(groups * slots, device=dev).repeat(B, 1)
+    cand[:] = (key << 32) | ((~row) & 0xFFFFFFFF)
+    ovf = torch.zeros(B, dtype=torch.int32, device=dev)
+    st = L.stream_of(dev)
+    fv0, fi0 = fv.clone(), fi.clone()
+
+    def run():
+        fv.copy_(fv0)
+        fi.copy_(fi0)
+        L.call("ebt_merge_hits", L.ptr(fv), L.ptr(fi), B, kp, L.ptr(cand), groups * slots, slots,
+               L.ptr(counts), counts.shape[1], groups, 0, None, None, L.ptr(ovf), st)
+    ms = timeit(run)
+    ms_copy = timeit(lambda: (fv.copy_(fv0), fi.copy_(fi0)))
+    return {"kernel": "merge_hits", "B": B, "kprime": kp, "groups": groups, "hits": hits,
+            "ms": round(ms - ms_copy, 4), "ovf": int(ovf.sum())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gemm", action="store_true")
     ap.add_argument("--select", action="store_true")
+    ap.add_argument("--merge", action="store_true")
     ap.add_argument("--one", action="store_true", help="single C3-chunk GEMM config (profiling)")
     ap.add_argument("--shape", default="4096,262144,1536", help="B,N,d for --one")
     ap.add_argument("--select-shapes", default=None,
@@ -89,6 +121,12 @@ def main():
     dev = torch.device("cuda:0")
     L.load()
     res = []
+    if args.merge:
+        for (B, kp, groups, hits) in [(4096, 200, 2048, 400), (4096, 200, 48, 400),
+                                      (4096, 200, 2048, 50), (4096, 200, 2048, 800),
+                                      (4096, 1016, 2048, 1000)]:
+            print(json.dumps(bench_merge(dev, B, kp, groups, hits)), flush=True)
+        return
     if args.one:
         B, N, d = (int(x) for x in args.shape.split(","))
         print(json.dumps(bench_gemm(dev, B, N, d, torch.float16)), flush=True)
