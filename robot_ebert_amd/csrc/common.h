@@ -57,6 +57,7 @@ __device__ __forceinline__ uint16_t f64_to_img(double v) {
 __device__ __forceinline__ uint32_t f2key(float f) {
   uint32_t u = __float_as_uint(f);
   if (!(f == f) || f == -__builtin_inff()) return 0u;
+  if (f == 0.f) return 0x80000000u;  // -0 and +0 are one value (they compare equal)
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 __device__ __forceinline__ float key2f(uint32_t k) {

@@ -132,6 +132,131 @@ def test_exact_screen_fallback_near_ties(cuda_device):
     assert_topk_equal(s, r, s_ref, r_ref)
 
 
+def _key_of(v):
+    """The order-preserving u32 key of float32 values (common.h f2key)."""
+    v = np.asarray(v, dtype=np.float32) + np.float32(0.0)  # -0 -> +0, as f2key does
+    u = v.view(np.uint32).astype(np.uint64)
+    k = np.where(u & 0x80000000, (~u) & 0xFFFFFFFF, u | 0x80000000)
+    bad = np.isnan(v) | (np.asarray(v) == -np.inf)
+    return np.where(bad, 0, k).astype(np.uint64)
+
+
+def _composite(v, rows):
+    return ((_key_of(v) << np.uint64(32)) | ((~np.asarray(rows, dtype=np.uint64)) & np.uint64(0xFFFFFFFF)))
+
+
+@pytest.mark.parametrize("B", [128, 256])
+def test_screen_filter_slots(cuda_device, B):
+    """ebt_screen_filter: the hits are exactly the scores >= thr (vs a torch fp32 reference of
+    the same product; values within 1e-4 of thr are not judged), each in its group's slots,
+    with the right group counts; a starved slot count sets ovf."""
+    ebt, L = _ebt()
+    N, d = 5000, 128
+    g = torch.Generator(device=cuda_device).manual_seed(3)
+    q = torch.randn((B, d), generator=g, device=cuda_device).half()
+    c = torch.randn((N, d), generator=g, device=cuda_device).half()
+    qs = torch.ones(B, device=cuda_device)
+    ref = (q.float() @ c.float().T)
+    thr = torch.quantile(ref[:, :2048], 0.995, dim=1).contiguous()
+    G = L.load().ebt_filter_group_rows(B)
+    groups = (N + G - 1) // G
+    for slots, expect_ovf in [(64, False), (1, True)]:
+        cand = torch.zeros((B, groups * slots), dtype=torch.int64, device=cuda_device)
+        counts = torch.zeros((B, groups), dtype=torch.uint8, device=cuda_device)
+        ovf = torch.zeros(B, dtype=torch.int32, device=cuda_device)
+        L.call("ebt_screen_filter", L.ptr(q), B, L.ptr(c), N, d, d, L.DTYPE_CODE[q.dtype],
+               L.ptr(qs), None, L.ptr(thr), L.ptr(cand), groups * slots, slots, L.ptr(counts),
+               groups, L.ptr(ovf), 7, L.stream_of(cuda_device))
+        refn, thrn = ref.cpu().numpy(), thr.cpu().numpy()
+        cn, cc = cand.cpu().numpy().view(np.uint64), counts.cpu().numpy()
+        if expect_ovf:
+            assert (ovf.cpu().numpy() == 1).any()
+            continue
+        assert not ovf.cpu().numpy().any()
+        for b in range(B):
+            want = set(np.nonzero(refn[b] >= thrn[b] + 1e-4)[0].tolist())
+            maybe = set(np.nonzero(np.abs(refn[b] - thrn[b]) <= 1e-4)[0].tolist())
+            got = {}
+            for gi in range(groups):
+                assert int(cc[b, gi]) <= slots
+                for p in range(cc[b, gi]):
+                    comp = cn[b, gi * slots + p]
+                    row = int((~comp) & np.uint64(0xFFFFFFFF)) - 7
+                    assert gi * G <= row < min((gi + 1) * G, N)
+                    got[row] = comp
+            assert want <= set(got) <= want | maybe
+            rows = np.array(sorted(got))
+            if rows.size:
+                vals = np.array([got[r] >> np.uint64(32) for r in rows], dtype=np.uint64)
+                np.testing.assert_allclose(np.array([_key_val(k) for k in vals]), refn[b, rows],
+                                           atol=2e-4)
+
+
+def _key_val(k):
+    k = int(k)
+    u = (k & 0x7FFFFFFF) if (k & 0x80000000) else (~k & 0xFFFFFFFF)
+    return float(np.array([u], dtype=np.uint32).view(np.float32)[0])
+
+
+@pytest.mark.parametrize("kp,hits,groups", [(40, 30, 7), (200, 500, 300), (200, 0, 10),
+                                            (600, 300, 50)])
+def test_merge_hits_vs_numpy(cuda_device, kp, hits, groups):
+    """ebt_merge_hits: the k' best of (sorted list + slot hits), exclusions dropped, in
+    (value desc, row asc) order -- ties included -- against numpy on the same composites."""
+    ebt, L = _ebt()
+    rng = np.random.default_rng(kp + hits)
+    B, slots = 9, 16
+    vals = np.round(rng.standard_normal((B, kp)) * 8) / 8          # ties
+    lv = -np.sort(-vals, axis=1).astype(np.float32)
+    lr = rng.permutation(100000)[:B * kp].reshape(B, kp) + 200000
+    lv[1, kp // 2:] = -np.inf                                        # short list
+    lr[1, kp // 2:] = -1
+    for b in range(B):                                               # (value desc, row asc)
+        o = np.lexsort((np.where(lr[b] < 0, 1 << 40, lr[b]), -lv[b]))
+        lv[b], lr[b] = lv[b][o], lr[b][o]
+    counts = np.zeros((B, (groups + 15) // 16 * 16), np.uint8)
+    cand = np.zeros((B, groups * slots), np.uint64)
+    hit_v, hit_r = [[] for _ in range(B)], [[] for _ in range(B)]
+    for b in range(B):
+        gsel = rng.integers(0, groups, hits)
+        for gi in gsel:
+            if counts[b, gi] >= slots:
+                continue
+            v = np.float32(np.round(rng.standard_normal() * 8) / 8)
+            r = gi * 1000 + counts[b, gi]
+            cand[b, gi * slots + counts[b, gi]] = _composite(np.array([v]), np.array([r]))[0]
+            counts[b, gi] += 1
+            hit_v[b].append(v)
+            hit_r[b].append(r)
+    excl = [sorted(hit_r[b][::3] + [int(lr[b, 0]) + 5]) for b in range(B)]  # some hits excluded
+    eo = np.concatenate([[0], np.cumsum([len(e) for e in excl])]).astype(np.int64)
+    er = np.concatenate([np.array(e, np.int64) for e in excl]) if eo[-1] else np.zeros(1, np.int64)
+    dev = cuda_device
+    fv = torch.from_numpy(lv).to(dev)
+    fi = torch.from_numpy(lr.astype(np.int64)).to(dev)
+    ovf = torch.zeros(B, dtype=torch.int32, device=dev)
+    ct = torch.from_numpy(counts).to(dev)
+    cd = torch.from_numpy(cand.view(np.int64)).to(dev)
+    eot, ert = torch.from_numpy(eo).to(dev), torch.from_numpy(er).to(dev)
+    L.call("ebt_merge_hits", L.ptr(fv), L.ptr(fi), B, kp, L.ptr(cd), groups * slots, slots,
+           L.ptr(ct), counts.shape[1], groups, 0, L.ptr(eot), L.ptr(ert), L.ptr(ovf),
+           L.stream_of(dev))
+    gv, gi_ = fv.cpu().numpy(), fi.cpu().numpy()
+    assert not ovf.cpu().numpy().any()
+    for b in range(B):
+        ex = set(excl[b])
+        hv = [v for v, r in zip(hit_v[b], hit_r[b]) if r not in ex]
+        hr = [r for r in hit_r[b] if r not in ex]
+        keep = lr[b] >= 0
+        allv = np.concatenate([lv[b][keep], np.array(hv, np.float32)])
+        allr = np.concatenate([lr[b][keep], np.array(hr, np.int64)])
+        o = np.lexsort((allr, -allv))[:kp]
+        m = len(o)
+        np.testing.assert_array_equal(gi_[b, :m], allr[o])
+        np.testing.assert_array_equal(gv[b, :m], allv[o])
+        assert np.all(gi_[b, m:] == -1)
+
+
 def _select_ref(v, k):
     n = v.shape[0]
     keys = np.where(np.isnan(v) | (v == -np.inf), -np.inf, v)
