@@ -214,9 +214,6 @@ def main() -> None:
     achieved = dom_flops / (dom_ms * 1e-3) / 1e12 if dom_ms > 0 else None
     all_gemm_ms = st["gemm"][0] + st["gemm_filter"][0]
     all_tf = 2.0 * B * n_local * d * args.steps / (all_gemm_ms * 1e-3) / 1e12 if all_gemm_ms else None
-    sel_ms, sel_n = st["select"]
-    sel_bytes = 4.0 * B * (head if pl["fused"] else n_local) * args.steps  # f32 scores read
-    sel_gbs = sel_bytes / (sel_ms * 1e-3) / 1e9 if sel_ms > 0 else None
     value = cfg["b"] * args.steps / elapsed
 
     out = None
@@ -250,15 +247,10 @@ def main() -> None:
                 "traffic": pmc_traffic(args.config, world),
                 "per_launch": {"launches": dom_n, "avg_ms": round(dom_ms / max(dom_n, 1), 4),
                                "flops": dom_flops / max(dom_n, 1),
-                               "flops_formula": "2*B*rows*d (rows = tail rows of the fused screen)"},
+                               "flops_formula": "2*B*rows*d per launch (rows = the launch's tail "
+                                                "segment of the fused screen; averaged over the "
+                                                "segments)"},
                 "all_gemm_tflops": round(all_tf, 2) if all_tf else None,
-            },
-            "topk_roofline": {
-                "bound": "hbm", "kernel": "select_topk_kernel (head rows)",
-                "achieved": round(sel_gbs, 1) if sel_gbs else None, "peak": PEAK_HBM_GBS,
-                "unit": "GB/s", "frac": round(sel_gbs / PEAK_HBM_GBS, 4) if sel_gbs else None,
-                "per_launch": {"launches": sel_n, "avg_ms": round(sel_ms / max(sel_n, 1), 4),
-                               "bytes_formula": "4*B*rows (f32 scores read once)"},
             },
             "plan": pl,
             "stage_ms_per_step": {name: round(v[0] / args.steps, 4) for name, v in st.items()},
