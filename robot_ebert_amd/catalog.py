@@ -96,12 +96,64 @@ class Catalog:
             raise EbertError(f"{len(self.ids)} ids for {self.n} rows")
         self._pos: Optional[Dict[str, int]] = None
 
-    # ---- id helpers (the DataFrame index of constants.py:56) -----------------------------
+    # ---- constructors ---------------------------------------------------------------------
     @classmethod
-    def from_matrix(cls, ids: Optional[Sequence[str]], emb, device="cuda", **kw) -> "Catalog":
+    def from_matrix(cls, ids: Optional[Sequence[str]], emb, device="cuda", shard: bool = False,
+                    **kw) -> "Catalog":
+        """SURVEY §8b's ``Catalog.from_matrix(ids, emb, shard)``: upload a host or device matrix.
+        With ``shard=True`` (an initialised torch.distributed group) this rank keeps only its
+        row range ``shard_range(n, rank, world)`` (ids sliced alike); rows stay GLOBAL ids."""
         if isinstance(emb, np.ndarray):
             emb = torch.from_numpy(np.ascontiguousarray(emb))
+        if shard:
+            import torch.distributed as dist
+            from .distributed import shard_range
+            if not (dist.is_available() and dist.is_initialized()):
+                raise EbertError("shard=True needs an initialised torch.distributed process group")
+            n = int(emb.shape[0])
+            a, b = shard_range(n, dist.get_rank(), dist.get_world_size())
+            emb = emb[a:b]
+            ids = list(ids)[a:b] if ids is not None else None
+            kw = dict(kw, row_offset=a, n_global=n)
         return cls(emb.to(device), ids=ids, **kw)
+
+    @classmethod
+    def from_parts(cls, emb: torch.Tensor, gnorm: torch.Tensor, inv32: torch.Tensor,
+                   image: torch.Tensor, row_offset: int = 0,
+                   n_global: Optional[int] = None) -> "Catalog":
+        """A catalog view over tensors already built by ``row_norms`` / ``screen_image`` (the
+        torch ops of ``ops.py``): nothing is recomputed. ``image`` is the f16 normalised image,
+        or the matrix itself for a native f16/bf16 catalog with d % 64 == 0."""
+        for t, what in ((emb, "catalog"), (gnorm, "gnorm"), (inv32, "inv"), (image, "image")):
+            require_cuda(t, what)
+        self = cls.__new__(cls)
+        self.data = emb if emb.stride(1) == 1 else emb.contiguous()
+        self.device = emb.device
+        self.n, self.d = int(emb.shape[0]), int(emb.shape[1])
+        self.ld = int(self.data.stride(0))
+        self.dtype_code = DTYPE_CODE[emb.dtype]
+        self.row_offset = int(row_offset)
+        self.n_global = int(n_global) if n_global is not None else self.n
+        self.d_pad = _round_up(self.d, IMG_ALIGN)
+        if gnorm.dtype != torch.float64 or gnorm.numel() < self.n:
+            raise EbertError("gnorm must be float64 [n]")
+        if inv32.dtype != torch.float32 or inv32.numel() < _round_up(self.n, 128):
+            raise EbertError("inv must be float32 [round_up(n, 128)]")
+        self.gnorm, self.inv32 = gnorm, inv32
+        native_16 = emb.dtype in (torch.float16, torch.bfloat16)
+        if image.dtype not in (torch.float16, torch.bfloat16) or image.shape[0] != self.n or \
+                image.stride(1) != 1 or image.stride(0) % IMG_ALIGN or image.shape[1] < self.d_pad:
+            raise EbertError("image must be a 16-bit [n, >= round_up(d, 64)] matrix, "
+                             "row stride a multiple of 64")
+        self.image, self.ld_img = image, int(image.stride(0))
+        self.img_dtype = EBT_F16 if image.dtype == torch.float16 else EBT_BF16
+        self.native = native_16  # the image holds the raw rows, scaled by inv in the epilogue
+        self.u_cat = 0.0 if native_16 else 2.0 ** -11
+        self.cscale = self.inv32 if native_16 else None
+        self.ids, self._pos = None, None
+        return self
+
+    # ---- id helpers (the DataFrame index of constants.py:56) -----------------------------
 
     @property
     def index_pos(self) -> Dict[str, int]:

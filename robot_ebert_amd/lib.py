@@ -30,17 +30,21 @@ SIMILARITY_TOP_K = 10     # constants.py:21
 
 engine = None                              # constants.py:26 (caller-supplied SQLAlchemy Engine)
 movies_collab_catalog: Optional[Catalog] = None  # constants.py:55-56, resident in HBM
+movies_content_catalog: Optional[Catalog] = None  # the movies-content collection (constants.py:29-53)
 _get_movies_override: Optional[Callable[[List[str]], List[Movie]]] = None
 
 
 def configure(engine=None, catalog: Optional[Catalog] = None,
-              get_movies: Optional[Callable[[List[str]], List[Movie]]] = None) -> None:
+              get_movies: Optional[Callable[[List[str]], List[Movie]]] = None,
+              content_catalog: Optional[Catalog] = None) -> None:
     """Install the process-global resources (the reference builds them at import time)."""
     g = globals()
     if engine is not None:
         g["engine"] = engine
     if catalog is not None:
         g["movies_collab_catalog"] = catalog
+    if content_catalog is not None:
+        g["movies_content_catalog"] = content_catalog
     g["_get_movies_override"] = get_movies
 
 
@@ -88,29 +92,81 @@ def order_recommendations(pairs: Sequence[Tuple[str, float]]) -> List[Tuple[str,
     return sorted(by_id, key=lambda t: t[1], reverse=True)
 
 
-def get_user_recs(user_id: str, k: int = 10) -> List[Recommendation]:
-    """GPU drop-in for lib.py:32-63 (same inputs, same outputs, same errors)."""
+def _user_request(user_id: str) -> Optional[Tuple[List[int], List[int]]]:
+    """lib.py:36-48: (liked rows, rated rows) of a user, None when the user has no ratings;
+    sklearn's ValueError when none of the ratings is a liked catalog movie."""
     cat = movies_collab_catalog
     with engine.begin() as cnx:  # lib.py:36-40
         statement = select(tables.ratings).where(tables.ratings.c.user_id == user_id)
         user_ratings = cnx.execute(statement).all()
         if not user_ratings:
-            return []
+            return None
     user_ratings = pd.DataFrame(user_ratings)
     user_ratings = user_ratings[user_ratings["tmdb_id"].isin(cat.index_pos.keys())]  # lib.py:44
     liked, rated = user_query_lists(user_ratings, cat)  # lib.py:47-48
     if not liked:  # sklearn check_pairwise_arrays on an empty X (lib.py:51)
         raise ValueError(f"Found array with 0 sample(s) (shape=(0, {cat.d})) while a minimum of 1 "
                          "is required by check_pairwise_arrays.")
-    scores, rows = score_topk(cat, k, liked=[liked], exclude=[rated])  # lib.py:51-55
-    s = scores[0].cpu().numpy()
-    r = rows[0].cpu().numpy()
+    return liked, rated
+
+
+def _hydrate(s: np.ndarray, r: np.ndarray) -> List[Recommendation]:
+    """lib.py:55-63 after the top-k: ids, sort_index, get_movies (ORDER BY id), zip, stable sort."""
+    cat = movies_collab_catalog
     pairs = [(cat.id_of(int(rr)), float(ss)) for ss, rr in zip(s, r) if rr >= 0]
     ordered_by_id = sorted(pairs, key=lambda t: t[0])  # .sort_index()
     movies = get_movies(tmdb_ids=[t for t, _ in ordered_by_id])  # lib.py:58
     scores_by_id = [sc for _, sc in ordered_by_id]  # lib.py:59
     recommendations = [Recommendation(movie=m, score=sc) for m, sc in zip(movies, scores_by_id)]
     return sorted(recommendations, key=lambda x: x.score, reverse=True)  # lib.py:63
+
+
+def get_user_recs(user_id: str, k: int = 10) -> List[Recommendation]:
+    """GPU drop-in for lib.py:32-63 (same inputs, same outputs, same errors)."""
+    req = _user_request(user_id)
+    if req is None:
+        return []
+    liked, rated = req
+    scores, rows = score_topk(movies_collab_catalog, k, liked=[liked], exclude=[rated])  # :51-55
+    return _hydrate(scores[0].cpu().numpy(), rows[0].cpu().numpy())
+
+
+get_user_recs_gpu = get_user_recs  # SURVEY §8b's name for the drop-in
+
+
+def get_user_recs_batched(batcher, user_id: str, k: int = 10) -> List[Recommendation]:
+    """``get_user_recs`` whose scoring step is coalesced with concurrent callers by a
+    ``batcher.RecBatcher`` over ``movies_collab_catalog``: same SQL, same errors,
+    same ordering; the GPU sees one batch for many request threads."""
+    req = _user_request(user_id)
+    if req is None:
+        return []
+    liked, rated = req
+    s, r = batcher.submit(liked, rated, k).result()
+    return _hydrate(s, r)
+
+
+def retrieve_content_matches(query_embedding, k: int = SIMILARITY_TOP_K) -> Tuple[List[str],
+                                                                                   List[float]]:
+    """the content retrieval of run_search (lib.py:71-73: the chat engine's
+    ``similarity_top_k`` matches from the ``movies-content`` Chroma collection, hnsw:space=cosine,
+    constants.py:29-53) as EXACT cosine top-k on the HBM content catalog. Returns (ids, cosine
+    scores) in score order. HNSW is approximate; its result sets are not pinned."""
+    cat = movies_content_catalog
+    q = torch.as_tensor(np.asarray(query_embedding, dtype=np.float64).reshape(1, -1),
+                        device=cat.device)
+    scores, rows = score_topk(cat, k, queries=q)
+    s, r = scores[0].cpu().numpy(), rows[0].cpu().numpy()
+    keep = r >= 0
+    return [cat.id_of(int(x)) for x in r[keep]], [float(x) for x in s[keep]]
+
+
+def run_search_exact(query_embedding, user_id: Optional[str] = None,
+                     k: int = SIMILARITY_TOP_K) -> List[Recommendation]:
+    """lib.py:66-122 without the LLM: exact content retrieval of the query embedding, then the
+    reference's re-ranking (user mean-cosine or popularity, 0.9 / 0.1 weights)."""
+    ids, scores = retrieve_content_matches(query_embedding, k)
+    return rerank_search_matches(ids, scores, user_id)
 
 
 def user_movie_scores(user_id: str, match_ids: List[str]) -> pd.Series:

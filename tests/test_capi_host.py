@@ -105,3 +105,20 @@ def test_user_query_lists():
     df = pd.DataFrame({"tmdb_id": ["a", "c", "b"], "rating": [3.5, 1.0, 5.0]})
     liked, rated = user_query_lists(df, FakeCat())
     assert liked == [0, 1] and sorted(rated) == [0, 1, 2]
+
+
+def test_torch_ops_registered_with_fake_kernels():
+    """torch.ops.ebert.* exist and trace on meta tensors (no GPU, no libebert call)."""
+    import torch
+    import robot_ebert_amd  # noqa: F401  (registers the ops)
+    x = torch.empty(1000, 100, device="meta")
+    g, inv = torch.ops.ebert.row_norms(x)
+    assert g.shape == (1000,) and g.dtype == torch.float64 and inv.shape == (1024,)
+    img = torch.ops.ebert.screen_image(x, g)
+    assert img.shape == (1000, 128) and img.dtype == torch.float16
+    q = torch.empty(7, 100, device="meta")
+    s, r = torch.ops.ebert.cosine_topk(q, x, g, inv, img, 5, None, None, 0)
+    assert s.shape == (7, 5) and r.dtype == torch.int64
+    ms, mr = torch.ops.ebert.merge_topk(torch.empty(3, 7, 5, dtype=torch.float64, device="meta"),
+                                        torch.empty(3, 7, 5, dtype=torch.int64, device="meta"), 5)
+    assert ms.shape == (7, 5)

@@ -449,7 +449,10 @@ def _collab_setup(cuda_device):
     with open(os.path.join(GOLD, "c1_collab.json")) as f:
         gold = json.load(f)
     ids, cat_np = c1_catalog()
-    engine = create_engine("sqlite://")
+    from sqlalchemy.pool import StaticPool
+    # one in-memory database shared by every thread (the batched test runs 16 request threads)
+    engine = create_engine("sqlite://", connect_args={"check_same_thread": False},
+                           poolclass=StaticPool)
     tables.ratings.create(engine)
     with engine.begin() as cnx:
         for uid, rec in gold["users"].items():
@@ -500,6 +503,78 @@ def test_search_rerank_matches_reference(cuda_device):
         np.testing.assert_allclose([g.score for g in got], [w[1] for w in want], atol=1e-12)
 
 
+@pytest.mark.parametrize("k", [10, 10000])
+def test_batched_user_recs_match_reference(cuda_device, k):
+    """§8f-2: 16 request threads through one RecBatcher give get_user_recs' golden answers
+    (errors per request, ordering), and the GPU saw coalesced batches."""
+    import concurrent.futures as cf
+    from robot_ebert_amd.batcher import RecBatcher
+    lib, gold = _collab_setup(cuda_device)
+    b = RecBatcher(lib.movies_collab_catalog, max_batch=64, max_wait_ms=20.0)
+    users = list(gold["users"].items())
+
+    def one(item):
+        uid, rec = item
+        try:
+            return uid, rec, lib.get_user_recs_batched(b, uid, k), None
+        except ValueError as e:
+            return uid, rec, None, e
+    with cf.ThreadPoolExecutor(16) as ex:
+        out = list(ex.map(one, users))
+    b.close()
+    for uid, rec, got, err in out:
+        want = rec[f"k{k}"]
+        if isinstance(want, dict):
+            assert err is not None and str(err) == want["message"], uid
+            continue
+        assert err is None, (uid, err)
+        assert [g.movie.tmdb_id for g in got] == [w[0] for w in want], uid
+        np.testing.assert_allclose([g.score for g in got], [w[1] for w in want], rtol=0,
+                                   atol=SCORE_ATOL)
+    assert max(b.batches) > 1
+
+
+def test_catalog_from_chroma_matches_reference(cuda_device):
+    """§8f-3: the C1 catalog ingested from a Chroma-style get() result (ids + embeddings, the
+    constants.py:55-56 source) serves get_user_recs with the reference's golden answers."""
+    from robot_ebert_amd import ingest
+    lib, gold = _collab_setup(cuda_device)
+    ids, cat_np = c1_catalog()
+    cat = ingest.catalog_from_chroma({"ids": ids, "embeddings": cat_np.tolist()}, device=cuda_device)
+    lib.configure(catalog=cat, get_movies=lib._get_movies_override)
+    for uid, rec in list(gold["users"].items())[:8]:
+        want = rec["k10"]
+        if isinstance(want, dict):
+            continue
+        got = lib.get_user_recs(uid, 10)
+        assert [g.movie.tmdb_id for g in got] == [w[0] for w in want], uid
+
+
+def test_exact_content_search(cuda_device):
+    """§8f-1: run_search's retrieval as exact cosine top-k over a 1536-d content catalog (HNSW
+    parity unpinned: compared with the float64 oracle), then the reference re-ranking."""
+    from robot_ebert_amd import lib as L_
+    lib, gold = _collab_setup(cuda_device)
+    ids, _ = c1_catalog()
+    rng = np.random.default_rng(77)
+    content = rng.standard_normal((len(ids), 1536))
+    lib.configure(content_catalog=ebt_catalog(content, ids, cuda_device),
+                  get_movies=lib._get_movies_override)
+    qe = rng.standard_normal(1536)
+    got_ids, got_s = lib.retrieve_content_matches(qe, 10)
+    s_ref, r_ref = R.cosine_topk(qe[None, :], content, 10)
+    assert got_ids == [ids[i] for i in r_ref[0]]
+    np.testing.assert_allclose(got_s, s_ref[0], rtol=0, atol=SCORE_ATOL)
+    recs = lib.run_search_exact(qe, None, 10)
+    want = lib.rerank_search_matches(got_ids, got_s, None)
+    assert [r.movie.tmdb_id for r in recs] == [w.movie.tmdb_id for w in want]
+
+
+def ebt_catalog(x, ids, dev):
+    ebt, _ = _ebt()
+    return ebt.Catalog(_t(x, "f64", dev), ids=ids)
+
+
 # ------------------------------------------------------------------ full-size properties ----
 def test_c3_shape_sample_parity(cuda_device):
     """Headline shape class (d=1536 f32) at 200K rows: sampled queries vs the oracle."""
@@ -520,3 +595,37 @@ def test_c3_shape_sample_parity(cuda_device):
     assert np.all(np.abs(sn) <= 1 + 1e-12)
     rn = r.cpu().numpy()
     assert all(len(set(x)) == k for x in rn)
+
+
+# ------------------------------------------------------------------ torch custom ops ----
+@pytest.mark.parametrize("case", ["d768_f32_k100_excl", "d1536_bf16_k10", "d200_f64_k50"])
+def test_torch_ops_cosine_topk(cuda_device, case):
+    """torch.ops.ebert.{row_norms, screen_image, cosine_topk, merge_topk} on plain tensors vs
+    the float64 oracle (golden case inputs, exclusions), and a 2-shard merge through the op."""
+    ebt, L = _ebt()
+    c = COS_CASES[case]
+    qv, cat_np, excl = cos_case_inputs(c)
+    k = c["k"]
+    cat = _t(cat_np, c["dtype"], cuda_device)
+    q = _t(qv, c["dtype"], cuda_device)
+    g, inv = torch.ops.ebert.row_norms(cat)
+    img = torch.ops.ebert.screen_image(cat, g)
+    eo = er = None
+    if excl is not None:
+        eo = torch.tensor(np.concatenate([[0], np.cumsum([len(e) for e in excl])]),
+                          dtype=torch.int64, device=cuda_device)
+        er = torch.tensor(np.concatenate([np.sort(e) for e in excl]), dtype=torch.int64,
+                          device=cuda_device)
+    s, r = torch.ops.ebert.cosine_topk(q, cat, g, inv, img, k, eo, er, 0)
+    s_ref, r_ref = R.cosine_topk(qv.astype(np.float64), cat_np.astype(np.float64), k, excl)
+    assert_topk_equal(s, r, s_ref, r_ref)
+    # two shards + merge through the op
+    h = cat.shape[0] // 2
+    parts = []
+    for a, b in ((0, h), (h, cat.shape[0])):
+        gs, invs = torch.ops.ebert.row_norms(cat[a:b])
+        ims = torch.ops.ebert.screen_image(cat[a:b], gs)
+        parts.append(torch.ops.ebert.cosine_topk(q, cat[a:b], gs, invs, ims, k, eo, er, a))
+    ms, mr = torch.ops.ebert.merge_topk(torch.stack([p[0] for p in parts]),
+                                        torch.stack([p[1] for p in parts]), k)
+    assert_topk_equal(ms, mr, s_ref, r_ref)

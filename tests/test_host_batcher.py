@@ -1,0 +1,91 @@
+"""CPU: the request micro-batcher (§8f-2) and the ingest helpers (§8f-3), host logic only.
+
+The batcher's scoring function is injected: here the float64 oracle (test infrastructure)
+stands in for the GPU ``score_topk`` so the coalescing, per-request slicing, error isolation and
+shutdown logic run without a GPU. The GPU path is covered in test_gpu_parity.py.
+"""
+import concurrent.futures as cf
+import threading
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from oracle import restatement as R
+from robot_ebert_amd.batcher import RecBatcher
+from robot_ebert_amd import ingest
+
+
+class _Cat:
+    def __init__(self, x):
+        self.x, self.d = x, x.shape[1]
+
+
+def _oracle_score(calls):
+    def score(cat, k, liked, exclude):
+        calls.append(len(liked))
+        qs = np.stack([R.mean_cosine_query(cat.x[l]) for l in liked])
+        return R.cosine_topk(qs, cat.x, k, exclude)
+    return score
+
+
+def _direct(cat, liked, excl, k):
+    s, r = R.cosine_topk(R.mean_cosine_query(cat.x[liked])[None, :], cat.x, k, [excl])
+    keep = r[0] >= 0
+    return s[0][keep], r[0][keep]
+
+
+def test_batcher_coalesces_and_slices():
+    rng = np.random.default_rng(0)
+    cat = _Cat(rng.standard_normal((500, 16)))
+    calls = []
+    b = RecBatcher(cat, max_batch=32, max_wait_ms=50.0, score_fn=_oracle_score(calls))
+    reqs = [(list(rng.choice(500, 3, replace=False)), list(rng.choice(500, 20, replace=False)),
+             int(k)) for k in rng.integers(1, 40, 40)]
+    with cf.ThreadPoolExecutor(16) as ex:
+        futs = list(ex.map(lambda r: b.submit(*r), reqs))
+        res = [f.result(timeout=30) for f in futs]
+    b.close()
+    for (liked, excl, k), (s, r) in zip(reqs, res):
+        ws, wr = _direct(cat, liked, excl, k)
+        np.testing.assert_array_equal(r, wr)
+        np.testing.assert_allclose(s, ws, atol=1e-15)
+    assert sum(calls) == len(reqs) and max(calls) > 1 and max(calls) <= 32
+
+
+def test_batcher_errors_are_per_request():
+    cat = _Cat(np.random.default_rng(1).standard_normal((50, 8)))
+    b = RecBatcher(cat, max_batch=8, max_wait_ms=5.0, score_fn=_oracle_score([]))
+    bad = b.submit([], [1, 2], 5)
+    good = b.submit([3], [], 5)
+    with pytest.raises(ValueError, match="0 sample"):
+        bad.result(timeout=10)
+    s, r = good.result(timeout=10)
+    assert len(r) == 5
+    b.close()
+    assert isinstance(b.submit([1], [], 3).exception(timeout=1), RuntimeError)
+
+
+def test_batcher_batch_failure_reaches_every_caller():
+    def boom(cat, k, liked, exclude):
+        raise MemoryError("out of HBM")
+    b = RecBatcher(_Cat(np.zeros((4, 2))), max_batch=4, max_wait_ms=50.0, score_fn=boom)
+    fs = [b.submit([0], [], 1) for _ in range(3)]
+    for f in fs:
+        assert isinstance(f.exception(timeout=10), MemoryError)
+    b.close()
+
+
+def test_ingest_chroma_matrix_and_id_order():
+    ids = ["862", "10", "2", "1000", "99"]
+    emb = np.arange(15, dtype=np.float32).reshape(5, 3)
+    got_ids, m = ingest.chroma_matrix({"ids": ids, "embeddings": emb.tolist(), "documents": None})
+    assert got_ids == ids and m.dtype == np.float64
+    np.testing.assert_array_equal(m, emb)
+    # lexicographic, as pandas sort_index on the str index of constants.py:56
+    df = pd.DataFrame(m, index=ids)
+    assert [ids[i] for i in ingest.id_order(ids)] == list(df.sort_index().index)
+    with pytest.raises(Exception):
+        ingest.chroma_matrix({"ids": ids[:4], "embeddings": emb.tolist()})
+    with pytest.raises(Exception):
+        ingest.chroma_matrix({"ids": ["a", "a"], "embeddings": [[1.0], [2.0]]})
