@@ -406,6 +406,15 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
   const int piece_step = (int)(8 * row_bytes);
   const int half_step = (int)(128 * row_bytes);
   const int total = 4 * ktiles;
+  auto issue_u = [&](int idx) {  // no bounds check: the caller guarantees idx < total
+    const int tile = idx >> 2, type = idx & 3;
+    char* dst = smem + (tile & 1) * QP_BUF + p_half_off(type) + wave * 2048;
+    const int soff = tile * 128 + ((type == P_A1 || type == P_B1) ? half_step : 0);
+    const __amdgpu_buffer_rsrc_t rs = (type == P_A0 || type == P_A1) ? rsC : rsQ;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)dst, 16, voff, soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + 1024), 16, voff,
+                                             soff + piece_step, 0, 0);
+  };
   auto issue = [&](int idx) {
     if (idx < total) {
       const int tile = idx >> 2, type = idx & 3;
@@ -446,57 +455,127 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
   wait_for(2, 6);  // B1(0), read in Q1(0)
 
   // One tile of four phases. B0(t) lives in `s0`, B1(t) in `s1`; Q4 reads B0(t+1) into s1.
-#define QP2_TILE(T, s0, s1)                                                                       \
+// GUARD = false in the steady state (every issued half-tile exists): the LDS-DMA pieces then
+// live in the same basic block as the MFMAs and are spread between them by the
+// sched_group_barrier patterns (masks: 0x008 MFMA, 0x100 DS read, 0x020 VMEM read) instead of
+// sitting in front of the phase's first MFMA, where both waves of a SIMD stalled on their DMA
+// issue at once.
+#define QP2_ISSUE(IDX, GUARD)                                                                    \
+  {                                                                                              \
+    if (GUARD) issue(IDX);                                                                       \
+    else issue_u(IDX);                                                                           \
+  }
+#define QP2_TILE(T, s0, s1, GUARD)                                                                \
   {                                                                                              \
     const int t_ = (T);                                                                          \
     const char* buf = smem + (t_ & 1) * QP_BUF;                                                  \
     const char* nbuf = smem + ((t_ + 1) & 1) * QP_BUF;                                           \
     /* Q1 (A0, B0): read B1(t) */                                                                \
     qp_barrier();                                                                                \
-    issue(4 * t_ + 7);                                                                           \
+    QP2_ISSUE(4 * t_ + 7, GUARD);                                                                \
     qp2_mma<BF16>(acc0, fa0, s0);                                                                \
     read_b(s1, buf + p_half_off(P_B1));                                                          \
-    _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_) {                                           \
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
-    }                                                                                            \
-    wait_for(4 * t_ + 3, 4 * t_ + 7); /* A1(t) for Q2 */                                         \
-    /* Q2 (A0, B1): read A1(t) */                                                                \
-    qp_barrier();                                                                                \
-    issue(4 * t_ + 8);                                                                           \
-    qp2_mma<BF16>(acc1, fa0, s1);                                                                \
-    read_a(fa1, buf + p_half_off(P_A1));                                                         \
-    _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                           \
+    if (!(GUARD)) {                                                                              \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
       __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
+      _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                         \
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                       \
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
+      }                                                                                          \
+    } else {                                                                                     \
+      _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_) {                                         \
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                       \
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
+      }                                                                                          \
+    }                                                                                            \
+    if (GUARD) wait_for(4 * t_ + 3, 4 * t_ + 7); else wait_vm<8>(); /* A1(t) for Q2 */           \
+    /* Q2 (A0, B1): read A1(t) */                                                                \
+    qp_barrier();                                                                                \
+    QP2_ISSUE(4 * t_ + 8, GUARD);                                                                \
+    qp2_mma<BF16>(acc1, fa0, s1);                                                                \
+    read_a(fa1, buf + p_half_off(P_A1));                                                         \
+    if (!(GUARD)) {                                                                              \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
+      _Pragma("unroll") for (int i_ = 0; i_ < 5; ++i_) {                                         \
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                       \
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
+      }                                                                                          \
+    } else {                                                                                     \
+      _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                         \
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                       \
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
+      }                                                                                          \
     }                                                                                            \
     /* Q3 (A1, B1): no reads */                                                                  \
     qp_barrier();                                                                                \
-    issue(4 * t_ + 9);                                                                           \
+    QP2_ISSUE(4 * t_ + 9, GUARD);                                                                \
     qp2_mma<BF16>(acc2, fa1, s1);                                                                \
-    wait_for(4 * t_ + 5, 4 * t_ + 9); /* A0(t+1), B0(t+1) for Q4 */                              \
+    if (!(GUARD)) {                                                                              \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x008, 10, 0);                                        \
+    }                                                                                            \
+    if (GUARD) wait_for(4 * t_ + 5, 4 * t_ + 9); else wait_vm<8>(); /* A0(t+1), B0(t+1) for Q4 */\
     /* Q4 (A1, B0): read A0(t+1), B0(t+1) */                                                     \
     qp_barrier();                                                                                \
-    issue(4 * t_ + 10);                                                                          \
+    QP2_ISSUE(4 * t_ + 10, GUARD);                                                               \
     qp2_mma<BF16>(acc3, fa1, s0);                                                                \
-    if (t_ + 1 < ktiles) {                                                                       \
+    if (!(GUARD) || t_ + 1 < ktiles) {                                                           \
       read_a(fa0, nbuf + p_half_off(P_A0));                                                      \
       read_b(s1, nbuf + p_half_off(P_B0));                                                       \
     }                                                                                            \
-    _Pragma("unroll") for (int i_ = 0; i_ < 12; ++i_) {                                          \
+    if (!(GUARD)) {                                                                              \
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
+      _Pragma("unroll") for (int i_ = 0; i_ < 3; ++i_) {                                         \
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                       \
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
+      }                                                                                          \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
+      _Pragma("unroll") for (int i_ = 0; i_ < 7; ++i_) {                                         \
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                       \
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
+      }                                                                                          \
+    } else {                                                                                     \
+      _Pragma("unroll") for (int i_ = 0; i_ < 12; ++i_) {                                        \
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                       \
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
+      }                                                                                          \
     }                                                                                            \
-    wait_for(4 * t_ + 6, 4 * t_ + 10); /* B1(t+1) for Q1(t+1) */                                 \
+    if (GUARD) wait_for(4 * t_ + 6, 4 * t_ + 10); else wait_vm<8>(); /* B1(t+1) for Q1(t+1) */   \
   }
 
   int t = 0;
-  for (; t + 1 < ktiles; t += 2) {
-    QP2_TILE(t, fbx, fby);
-    QP2_TILE(t + 1, fby, fbx);
+  // steady state: the last half-tile issued by the pair (t, t+1) is 4 (t+1) + 10 < 4 ktiles
+  for (; t + 4 < ktiles; t += 2) {
+    QP2_TILE(t, fbx, fby, false);
+    QP2_TILE(t + 1, fby, fbx, false);
   }
-  if (t < ktiles) QP2_TILE(t, fbx, fby);
+  for (; t + 1 < ktiles; t += 2) {
+    QP2_TILE(t, fbx, fby, true);
+    QP2_TILE(t + 1, fby, fbx, true);
+  }
+  if (t < ktiles) QP2_TILE(t, fbx, fby, true);
 #undef QP2_TILE
+#undef QP2_ISSUE
 
   // ---- epilogue: quadrant (ah, bh) = catalog half ah x query half bh ----
   auto store_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh) {
