@@ -425,6 +425,31 @@ def test_fused_screen_equals_unfused_and_oracle(cuda_device, dt):
     assert_topk_equal(s1[sample], r1[sample], s_ref, r_ref)
 
 
+def test_fused_large_kprime_block_path(cuda_device):
+    """k' > 512 (C5's k = 1000 class) takes the 256 k'-row head + block-level merges: equal to
+    the unfused path and to the oracle on sampled queries, with exclusions."""
+    ebt, L = _ebt()
+    n, d, B, k = 400_000, 128, 130, 600
+    c = gaussian(4, n, d, "f16")
+    q = gaussian(5, B, d, "f16")
+    rng = np.random.default_rng(6)
+    excl = [np.sort(rng.choice(n, 500, replace=False)) for _ in range(B)]
+    cat = ebt.Catalog(_t(c, "f16", cuda_device))
+    qt = _t(q, "f16", cuda_device)
+    pl = ebt.search.plan(cat, B, k)
+    assert pl["fused"] and pl["kprime"] > 512 and pl["head_rows"] >= 256 * pl["kprime"]
+    timer = ebt.Timer()
+    s1, r1 = ebt.score_topk(cat, k, queries=qt, exclude=[list(e) for e in excl], timer=timer)
+    assert timer.query("gemm_filter")[1] >= 1, "fused path not taken"
+    s2, r2 = ebt.score_topk(cat, k, queries=qt, exclude=[list(e) for e in excl], fuse=False)
+    assert torch.equal(r1, r2)
+    torch.testing.assert_close(s1, s2, rtol=0, atol=0)
+    sample = [0, 64, 129]
+    s_ref, r_ref = R.cosine_topk(q[sample].astype(np.float64), c.astype(np.float64), k,
+                                 [excl[i] for i in sample])
+    assert_topk_equal(s1[sample], r1[sample], s_ref, r_ref)
+
+
 def test_fused_overflow_falls_back(cuda_device):
     """Scores that grow with the row index make the head threshold useless: every tail row
     passes, the candidate list overflows, and the query must be redone unfused -- exactly."""
