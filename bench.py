@@ -3,8 +3,8 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
 
 One step = one batch of B synthetic Gaussian queries through the whole path (query prep ->
-MFMA screening GEMM -> streaming top-k' select -> exact float64 rescore -> certification, and
-for N > 1 the RCCL all-gather of the per-shard top-k + merge). The catalog (seeded Gaussian,
+fused MFMA screen (pilot, filtered GEMM segments, merges) -> exact float64 rescore ->
+certification; for N > 1 the RCCL all-gather of the per-shard top-k + merge). The catalog (seeded Gaussian,
 generated on the GPU in fixed 65536-row blocks so every N sees the same global matrix) is
 row-sharded over the N ranks and resident in HBM before timing starts: `scaling` = "strong"
 (fixed total work). Rank 0 prints ONE JSON line. The CPU baseline (rank 0, N = 1 only) times the
@@ -154,7 +154,7 @@ def main() -> None:
     dev = torch.device("cuda", local_rank)
 
     import robot_ebert_amd as ebt
-    from robot_ebert_amd.distributed import gather_partials, shard_range
+    from robot_ebert_amd.distributed import score_topk_sharded_local, shard_range
     ebt.load()
 
     begin, end = shard_range(cfg["n"], rank, world)
@@ -167,11 +167,9 @@ def main() -> None:
     k = cfg["k"]
 
     def step():
-        s, r = ebt.score_topk(cat, k, queries=q, timer=timer)
-        if world > 1:
-            gs, gr = gather_partials(s, r)
-            s, r = ebt.merge_topk(gs, gr, k)
-        return s, r
+        if world > 1:  # per-shard exact top-k, one RCCL all-gather, merge
+            return score_topk_sharded_local(cat, k, queries=q, timer=timer)
+        return ebt.score_topk(cat, k, queries=q, timer=timer)
 
     for i in range(args.warmup):
         t0 = time.perf_counter()

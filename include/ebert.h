@@ -222,6 +222,34 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
                     double* out_scores, int64_t* out_rows, int32_t* certified, void* timer,
                     void* stream);
 
+/* ---- two-phase top-k over a row-sharded catalog (robot_ebert_amd/distributed.py) ---------
+ * Phase 1, every rank: ebt_cosine_screen = ebt_cosine_topk without the rescore: the shard's k'
+ * best approx candidates, list_vals (f32) / list_rows (GLOBAL, -1 empty) [B][kprime] sorted,
+ * ovf_out[b] = 1 when the fused screen overflowed for b, eps_out = the eps the certificate
+ * must use. The ranks all-gather the lists and keep the k' best of all shards
+ * (ebt_select_topk over [B][R*kprime] with the rows as indices).
+ * Phase 2: ebt_rescore_owned writes the exact float64 score of every merged candidate whose
+ * row is in [row_offset, row_offset + n_rows) and whose approx is >= approx[k-1] - 2 eps, 0.0
+ * for the rest; an all-reduce (SUM) of `exact` completes it; ebt_finalize_topk sorts the
+ * candidates above the cut by (exact desc, row asc) into out_scores/out_rows [B][k] and
+ * certifies like ebt_rescore (ovf = the all-reduced (MAX) overflow flags -> certified -1). */
+int ebt_cosine_screen(const double* q64, const void* qimg, const float* qscale, const float* eps,
+                      int64_t B, int64_t B_pad, const void* cat, int dtype, int64_t ld,
+                      const double* gnorm64, const void* cimg, const float* cscale, int img_dtype,
+                      int32_t ld_img, int64_t n_rows, int32_t d, int32_t d_pad, int64_t row_offset,
+                      const int64_t* excl_off, const int64_t* excl_rows, int32_t k, int32_t kprime,
+                      int64_t chunk_rows, int flags, void* workspace, size_t ws_bytes,
+                      float* list_vals, int64_t* list_rows, int32_t* ovf_out, float* eps_out,
+                      void* timer, void* stream);
+int ebt_rescore_owned(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
+                      int64_t ld, const double* gnorm64, int64_t row_offset, int64_t n_rows,
+                      const float* cand_vals, const int64_t* cand_rows, int32_t kprime, int32_t k,
+                      const float* eps, double* exact, void* stream);
+int ebt_finalize_topk(const float* cand_vals, const int64_t* cand_rows, const double* exact,
+                      int64_t B, int32_t kprime, int32_t k, int64_t n_rows_global,
+                      const float* eps, const int32_t* ovf, double* out_scores, int64_t* out_rows,
+                      int32_t* certified, void* stream);
+
 /* ---- per-stage GPU timing (hipEvents recorded on the launch stream) -----------------------
  * Stages: 0 screening GEMM (score-writing), 1 exclusion mask, 2 chunk select, 3 candidate
  * select (across chunks / head + fused tail), 4 rescore, 5 fused screening GEMM (filtering).

@@ -47,6 +47,13 @@ _SIGNATURES = {
     "ebt_screen_filter": ([_VP, _I64, _VP, _I64, _I32, _I32, _INT, _VP, _VP, _VP, _VP, _I64, _I32,
                            _VP, _I64, _VP, _I64, _VP], _INT),
     "ebt_filter_group_rows": ([_I64], _I64),
+    "ebt_cosine_screen": ([_VP, _VP, _VP, _VP, _I64, _I64, _VP, _INT, _I64, _VP, _VP, _VP, _INT,
+                           _I32, _I64, _I32, _I32, _I64, _VP, _VP, _I32, _I32, _I64, _INT, _VP,
+                           ctypes.c_size_t, _VP, _VP, _VP, _VP, _VP, _VP], _INT),
+    "ebt_rescore_owned": ([_VP, _I64, _I32, _VP, _INT, _I64, _VP, _I64, _I64, _VP, _VP, _I32,
+                           _I32, _VP, _VP, _VP], _INT),
+    "ebt_finalize_topk": ([_VP, _VP, _VP, _I64, _I32, _I32, _I64, _VP, _VP, _VP, _VP, _VP, _VP],
+                          _INT),
     "ebt_merge_hits": ([_VP, _VP, _I64, _I32, _VP, _I64, _I32, _VP, _I64, _I64, _I64, _VP, _VP, _VP,
                         _VP], _INT),
     "ebt_mask_excluded": ([_VP, _I64, _I64, _I64, _I64, _VP, _VP, _VP], _INT),

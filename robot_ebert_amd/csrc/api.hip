@@ -68,6 +68,13 @@ int merge_topk(const double*, const int64_t*, int32_t, int64_t, int32_t, double*
                hipStream_t);
 int screen_exact(const double*, int64_t, int32_t, const void*, int, int64_t, const double*, int64_t,
                  float*, int64_t, hipStream_t);
+int export_list(int64_t*, int64_t, int32_t, int64_t, const int*, const float*, int32_t*, float*,
+                hipStream_t);
+int rescore_owned(const double*, int64_t, int32_t, const void*, int, int64_t, const double*,
+                  int64_t, int64_t, const float*, const int64_t*, int32_t, int32_t, const float*,
+                  double*, hipStream_t);
+int finalize_topk(const float*, const int64_t*, const double*, int64_t, int32_t, int32_t, int64_t,
+                  const float*, const int32_t*, double*, int64_t*, int32_t*, hipStream_t);
 
 // EBT_FLAG_EXACT screening operands (the float64 catalog path), null for the MFMA screen
 struct ExactScreen {
@@ -411,41 +418,71 @@ int ebt_cosine_topk_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprim
   return EBT_OK;
 }
 
-int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, const float* eps,
-                    int64_t B, int64_t B_pad, const void* cat, int dtype, int64_t ld,
-                    const double* gnorm64, const void* cimg, const float* cscale, int img_dtype,
-                    int32_t ld_img, int64_t n_rows, int32_t d, int32_t d_pad, int64_t row_offset,
-                    const int64_t* excl_off, const int64_t* excl_rows, int32_t k, int32_t kprime,
-                    int64_t chunk_rows, int flags, void* workspace, size_t ws_bytes,
-                    double* out_scores, int64_t* out_rows, int32_t* certified, void* timer,
-                    void* stream) {
-  hipStream_t st = (hipStream_t)stream;
-  const bool exact = flags & EBT_FLAG_EXACT;
-  if (!q64 || (!exact && (!qimg || !qscale || !eps || !cimg)) || !cat || !gnorm64 || !workspace ||
-      !out_scores || !out_rows || !certified) {
-    set_error("ebt_cosine_topk: null pointer");
+}  // extern "C"
+
+namespace ebt {
+
+// What the rescore needs from the screen: the eps the certificate uses (the caller's, or the
+// exact screen's constant) and the fused screen's overflow flags (null when not fused).
+struct ScreenOut {
+  const float* eps;
+  const int* ovf;
+};
+
+struct PipeArgs {
+  const double* q64;
+  const void* qimg;
+  const float* qscale;
+  const float* eps;
+  int64_t B, B_pad;
+  const void* cat;
+  int dtype;
+  int64_t ld;
+  const double* gnorm64;
+  const void* cimg;
+  const float* cscale;
+  int img_dtype;
+  int32_t ld_img;
+  int64_t n_rows;
+  int32_t d, d_pad;
+  int64_t row_offset;
+  const int64_t* excl_off;
+  const int64_t* excl_rows;
+  int32_t k, kprime;
+  int64_t chunk_rows;
+  int flags;
+};
+
+static int check_pipe(const PipeArgs& a, const char* who) {
+  const bool exact = a.flags & EBT_FLAG_EXACT;
+  if (!a.q64 || (!exact && (!a.qimg || !a.qscale || !a.eps || !a.cimg)) || !a.cat ||
+      !a.gnorm64) {
+    set_error("%s: null pointer", who);
     return EBT_EINVAL;
   }
-  if (B < 1 || B_pad < B || B_pad % 128 != 0 || n_rows < 1 || d < 1 || d_pad < d ||
-      d_pad % 64 != 0 || ld_img < d_pad || k < 1 || kprime < k || kprime > 4096 ||
-      kprime % 4 != 0 || chunk_rows < 128 || chunk_rows % 128 != 0 ||
-      ((excl_off == nullptr) != (excl_rows == nullptr))) {
-    set_error("ebt_cosine_topk: bad arguments (B=%lld B_pad=%lld n=%lld d=%d d_pad=%d k=%d "
-              "kprime=%d chunk=%lld)", (long long)B, (long long)B_pad, (long long)n_rows, d,
-              d_pad, k, kprime, (long long)chunk_rows);
+  if (a.B < 1 || a.B_pad < a.B || a.B_pad % 128 != 0 || a.n_rows < 1 || a.d < 1 ||
+      a.d_pad < a.d || a.d_pad % 64 != 0 || a.ld_img < a.d_pad || a.k < 1 || a.kprime < a.k ||
+      a.kprime > 4096 || a.kprime % 4 != 0 || a.chunk_rows < 128 || a.chunk_rows % 128 != 0 ||
+      ((a.excl_off == nullptr) != (a.excl_rows == nullptr))) {
+    set_error("%s: bad arguments (B=%lld B_pad=%lld n=%lld d=%d d_pad=%d k=%d kprime=%d "
+              "chunk=%lld)", who, (long long)a.B, (long long)a.B_pad, (long long)a.n_rows, a.d,
+              a.d_pad, a.k, a.kprime, (long long)a.chunk_rows);
     return EBT_EINVAL;
   }
-  const WsLayout L = ws_layout(B, B_pad, n_rows, kprime, chunk_rows, flags);
-  if (ws_bytes < L.bytes) {
-    set_error("ebt_cosine_topk: workspace %zu < %zu bytes", ws_bytes, L.bytes);
-    return EBT_ENOMEM;
-  }
-  char* ws = (char*)workspace;
-  float* fv = (float*)(ws + L.off_fv);
-  int64_t* fi = (int64_t*)(ws + L.off_fi);
+  return EBT_OK;
+}
+
+// The screen: the k' best approx candidates per query into fv/fi (LOCAL rows, sorted), by the
+// exact (float64) screen, the unfused chunked screen or the fused pilot/segment screen.
+static int run_screen(const PipeArgs& a, const WsLayout& L, char* ws, float* fv, int64_t* fi,
+                      void* timer, hipStream_t st, ScreenOut* so) {
   int rc;
-  if (exact) {  // float64 screen; its bound replaces the caller's eps
-    const ExactScreen ex{q64, d, cat, dtype, ld, gnorm64};
+  so->eps = a.eps;
+  so->ovf = nullptr;
+  const int64_t B = a.B, B_pad = a.B_pad, n_rows = a.n_rows, row_offset = a.row_offset;
+  const int32_t k = a.k, kprime = a.kprime, d_pad = a.d_pad, ld_img = a.ld_img;
+  if (a.flags & EBT_FLAG_EXACT) {  // float64 screen; its bound replaces the caller's eps
+    const ExactScreen ex{a.q64, a.d, a.cat, a.dtype, a.ld, a.gnorm64};
     float* xeps = (float*)(ws + L.off_eps);
     const float e = EBT_EXACT_EPS;
     uint32_t bits;
@@ -453,50 +490,46 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
     rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)xeps, (int)bits, (size_t)B, st),
                    "hipMemsetD32Async");
     if (rc) return rc;
-    rc = head_topk(L, ws, nullptr, nullptr, B, B_pad, nullptr, nullptr, img_dtype, ld_img, 0,
-                   n_rows, d_pad, row_offset, excl_off, excl_rows, kprime, fv, fi, kprime, timer,
-                   st, &ex);
-    if (rc) return rc;
-    StageScope s(timer, EBT_STAGE_RESCORE, st);
-    return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, fv, fi, kprime, k, n_rows, xeps,
-                   out_scores, out_rows, certified, st, nullptr, 0);
+    so->eps = xeps;
+    return head_topk(L, ws, nullptr, nullptr, B, B_pad, nullptr, nullptr, a.img_dtype, ld_img, 0,
+                     n_rows, d_pad, row_offset, a.excl_off, a.excl_rows, kprime, fv, fi, kprime,
+                     timer, st, &ex);
   }
-  if (!L.fused) {
-    rc = head_topk(L, ws, qimg, qscale, B, B_pad, cimg, cscale, img_dtype, ld_img, 0, n_rows,
-                   d_pad, row_offset, excl_off, excl_rows, kprime, fv, fi, kprime, timer, st);
-    if (rc) return rc;
-    StageScope s(timer, EBT_STAGE_RESCORE, st);
-    return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, fv, fi, kprime, k, n_rows, eps,
-                   out_scores, out_rows, certified, st, nullptr, 0);
-  }
+  if (!L.fused)
+    return head_topk(L, ws, a.qimg, a.qscale, B, B_pad, a.cimg, a.cscale, a.img_dtype, ld_img, 0,
+                     n_rows, d_pad, row_offset, a.excl_off, a.excl_rows, kprime, fv, fi, kprime,
+                     timer, st);
   uint64_t* cand = (uint64_t*)(ws + L.off_cand);
   uint8_t* counts = (uint8_t*)(ws + L.off_counts);
   float* thr = (float*)(ws + L.off_thr);
   int* ovf = (int*)(ws + L.off_ovf);
+  so->ovf = ovf;
   // 1. head rows [0, H): exact top-k' per query (the list fv/fi)
   if (L.pilot) {
     float* S = (float*)(ws + L.off_s);
     {
       StageScope s(timer, EBT_STAGE_GEMM, st);
-      rc = screen_gemm(qimg, B_pad, cimg, L.head, d_pad, ld_img, img_dtype, qscale, cscale, S,
-                       L.ld_s, st);
+      rc = screen_gemm(a.qimg, B_pad, a.cimg, L.head, d_pad, ld_img, a.img_dtype, a.qscale,
+                       a.cscale, S, L.ld_s, st);
     }
     if (rc) return rc;
-    if (excl_off) {
+    if (a.excl_off) {
       StageScope s(timer, EBT_STAGE_MASK, st);
-      rc = mask_excluded(S, L.ld_s, B, row_offset, row_offset + L.head, excl_off, excl_rows, st);
+      rc = mask_excluded(S, L.ld_s, B, row_offset, row_offset + L.head, a.excl_off, a.excl_rows,
+                         st);
       if (rc) return rc;
     }
     StageScope s(timer, EBT_STAGE_SELECT, st);
     rc = pilot_topk(S, L.ld_s, B, (int)L.head, 0, kprime, fv, fi, st);
   } else {
-    rc = head_topk(L, ws, qimg, qscale, B, B_pad, cimg, cscale, img_dtype, ld_img, 0, L.head,
-                   d_pad, row_offset, excl_off, excl_rows, kprime, fv, fi, kprime, timer, st);
+    rc = head_topk(L, ws, a.qimg, a.qscale, B, B_pad, a.cimg, a.cscale, a.img_dtype, ld_img, 0,
+                   L.head, d_pad, row_offset, a.excl_off, a.excl_rows, kprime, fv, fi, kprime,
+                   timer, st);
   }
   if (rc) return rc;
   rc = hip_check(hipMemsetAsync(ovf, 0, (size_t)B_pad * 4, st), "hipMemsetAsync");
   if (rc) return rc;
-  // 2. tail rows [H, n) in doubling segments: threshold = the list's k'-th score, GEMM with the
+  // 2. tail rows [H, n) in segments: threshold = the list's k-th approx - 2 eps, GEMM with the
   //    filter epilogue, merge of list + hits (exclusions dropped) back into the list
   int64_t r0 = L.head;
   while (r0 < n_rows) {
@@ -521,29 +554,112 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
       seg_cap = merge_wave_max_groups() * L.group_rows;
     seg = seg < seg_cap ? seg : seg_cap;
     const int64_t groups = ceil_div(seg, L.group_rows);
-    rc = kth_threshold(fv, kprime, B, B_pad, k, eps, thr, st);
+    rc = kth_threshold(fv, kprime, B, B_pad, k, a.eps, thr, st);
     if (rc) return rc;
     {
       StageScope s(timer, EBT_STAGE_GEMM_FILTER, st);
-      rc = screen_gemm_filter(qimg, B_pad, (const char*)cimg + r0 * ld_img * 2, seg, d_pad,
-                              ld_img, img_dtype, qscale, cscale ? cscale + r0 : nullptr, thr,
-                              cand, L.ld_cand, slots, counts, L.ld_counts, ovf, r0, st);
+      rc = screen_gemm_filter(a.qimg, B_pad, (const char*)a.cimg + r0 * ld_img * 2, seg, d_pad,
+                              ld_img, a.img_dtype, a.qscale, a.cscale ? a.cscale + r0 : nullptr,
+                              thr, cand, L.ld_cand, slots, counts, L.ld_counts, ovf, r0, st);
     }
     if (rc) return rc;
     {
       StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
       rc = L.pilot ? merge_segment_wave(fv, fi, B, kprime, cand, L.ld_cand, slots, counts,
-                                        L.ld_counts, groups, row_offset, excl_off, excl_rows, ovf,
-                                        st)
+                                        L.ld_counts, groups, row_offset, a.excl_off, a.excl_rows,
+                                        ovf, st)
                    : merge_segment(fv, fi, B, kprime, cand, L.ld_cand, slots, counts,
-                                   L.ld_counts, groups, row_offset, excl_off, excl_rows, ovf, st);
+                                   L.ld_counts, groups, row_offset, a.excl_off, a.excl_rows, ovf,
+                                   st);
     }
     if (rc) return rc;
     r0 += seg;
   }
+  return EBT_OK;
+}
+
+}  // namespace ebt
+
+extern "C" {
+
+int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, const float* eps,
+                    int64_t B, int64_t B_pad, const void* cat, int dtype, int64_t ld,
+                    const double* gnorm64, const void* cimg, const float* cscale, int img_dtype,
+                    int32_t ld_img, int64_t n_rows, int32_t d, int32_t d_pad, int64_t row_offset,
+                    const int64_t* excl_off, const int64_t* excl_rows, int32_t k, int32_t kprime,
+                    int64_t chunk_rows, int flags, void* workspace, size_t ws_bytes,
+                    double* out_scores, int64_t* out_rows, int32_t* certified, void* timer,
+                    void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const PipeArgs a{q64, qimg, qscale, eps, B, B_pad, cat, dtype, ld, gnorm64, cimg, cscale,
+                   img_dtype, ld_img, n_rows, d, d_pad, row_offset, excl_off, excl_rows, k, kprime,
+                   chunk_rows, flags};
+  int rc = check_pipe(a, "ebt_cosine_topk");
+  if (rc) return rc;
+  if (!workspace || !out_scores || !out_rows || !certified) {
+    set_error("ebt_cosine_topk: null pointer");
+    return EBT_EINVAL;
+  }
+  const WsLayout L = ws_layout(B, B_pad, n_rows, kprime, chunk_rows, flags);
+  if (ws_bytes < L.bytes) {
+    set_error("ebt_cosine_topk: workspace %zu < %zu bytes", ws_bytes, L.bytes);
+    return EBT_ENOMEM;
+  }
+  char* ws = (char*)workspace;
+  float* fv = (float*)(ws + L.off_fv);
+  int64_t* fi = (int64_t*)(ws + L.off_fi);
+  ScreenOut so{};
+  rc = run_screen(a, L, ws, fv, fi, timer, st, &so);
+  if (rc) return rc;
   StageScope s(timer, EBT_STAGE_RESCORE, st);
-  return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, fv, fi, kprime, k, n_rows, eps,
-                 out_scores, out_rows, certified, st, ovf, 0);
+  return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, fv, fi, kprime, k, n_rows,
+                 so.eps, out_scores, out_rows, certified, st, so.ovf, 0);
+}
+
+int ebt_cosine_screen(const double* q64, const void* qimg, const float* qscale, const float* eps,
+                      int64_t B, int64_t B_pad, const void* cat, int dtype, int64_t ld,
+                      const double* gnorm64, const void* cimg, const float* cscale, int img_dtype,
+                      int32_t ld_img, int64_t n_rows, int32_t d, int32_t d_pad, int64_t row_offset,
+                      const int64_t* excl_off, const int64_t* excl_rows, int32_t k, int32_t kprime,
+                      int64_t chunk_rows, int flags, void* workspace, size_t ws_bytes,
+                      float* list_vals, int64_t* list_rows, int32_t* ovf_out, float* eps_out,
+                      void* timer, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const PipeArgs a{q64, qimg, qscale, eps, B, B_pad, cat, dtype, ld, gnorm64, cimg, cscale,
+                   img_dtype, ld_img, n_rows, d, d_pad, row_offset, excl_off, excl_rows, k, kprime,
+                   chunk_rows, flags};
+  int rc = check_pipe(a, "ebt_cosine_screen");
+  if (rc) return rc;
+  if (!workspace || !list_vals || !list_rows || !ovf_out || !eps_out) {
+    set_error("ebt_cosine_screen: null pointer");
+    return EBT_EINVAL;
+  }
+  const WsLayout L = ws_layout(B, B_pad, n_rows, kprime, chunk_rows, flags);
+  if (ws_bytes < L.bytes) {
+    set_error("ebt_cosine_screen: workspace %zu < %zu bytes", ws_bytes, L.bytes);
+    return EBT_ENOMEM;
+  }
+  char* ws = (char*)workspace;
+  ScreenOut so{};
+  rc = run_screen(a, L, ws, list_vals, list_rows, timer, st, &so);
+  if (rc) return rc;
+  return export_list(list_rows, B, kprime, row_offset, so.ovf, so.eps, ovf_out, eps_out, st);
+}
+
+int ebt_rescore_owned(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
+                      int64_t ld, const double* gnorm64, int64_t row_offset, int64_t n_rows,
+                      const float* cand_vals, const int64_t* cand_rows, int32_t kprime, int32_t k,
+                      const float* eps, double* exact, void* stream) {
+  return rescore_owned(q64, B, d, cat, dtype, ld, gnorm64, row_offset, n_rows, cand_vals,
+                       cand_rows, kprime, k, eps, exact, (hipStream_t)stream);
+}
+
+int ebt_finalize_topk(const float* cand_vals, const int64_t* cand_rows, const double* exact,
+                      int64_t B, int32_t kprime, int32_t k, int64_t n_rows_global,
+                      const float* eps, const int32_t* ovf, double* out_scores, int64_t* out_rows,
+                      int32_t* certified, void* stream) {
+  return finalize_topk(cand_vals, cand_rows, exact, B, kprime, k, n_rows_global, eps, ovf,
+                       out_scores, out_rows, certified, (hipStream_t)stream);
 }
 
 void* ebt_timer_create(void) { return new (std::nothrow) Timer(); }

@@ -344,4 +344,198 @@ int screen_exact(const double* q64, int64_t B, int32_t d, const void* cat, int d
   return launch_check("screen_exact_kernel");
 }
 
+// ---------------------------------------------------------------------------------------------
+// Two-phase certification over a row-sharded catalog (distributed.py). Phase 1 on every rank:
+// ebt_cosine_screen leaves the shard's k' best approx candidates (GLOBAL rows) -> all-gather ->
+// the k' best of all shards (same on every rank). Phase 2: each rank computes the exact float64
+// score of the merged candidates IT owns (rescore_owned: 0 elsewhere), an all-reduce (SUM)
+// completes them, and finalize_topk sorts and certifies exactly like rescore_kernel. A row
+// outside the merged list has approx <= the merged k'-th (it lost a merge or a shard's own
+// selection, whose k'-th is <= the merged k'-th) or was dropped by a segment threshold below
+// the list's k-th - 2 eps, so "merged[k'-1] < merged[k-1] - 2 eps" certifies the global top-k.
+// ---------------------------------------------------------------------------------------------
+__global__ void export_list_kernel(int64_t* __restrict__ rows, int64_t B, int kprime,
+                                   int64_t row_offset, const int* __restrict__ ovf,
+                                   const float* __restrict__ eps, int32_t* __restrict__ ovf_out,
+                                   float* __restrict__ eps_out) {
+  const int64_t b = blockIdx.x;
+  for (int j = threadIdx.x; j < kprime; j += blockDim.x) {
+    const int64_t r = rows[b * kprime + j];
+    rows[b * kprime + j] = r >= 0 ? r + row_offset : -1;
+  }
+  if (threadIdx.x == 0) {
+    ovf_out[b] = ovf ? (ovf[b] > 0 ? 1 : 0) : 0;
+    eps_out[b] = eps[b];
+  }
+}
+
+int export_list(int64_t* rows, int64_t B, int32_t kprime, int64_t row_offset, const int* ovf,
+                const float* eps, int32_t* ovf_out, float* eps_out, hipStream_t st) {
+  if (B <= 0) return EBT_OK;
+  hipLaunchKernelGGL(export_list_kernel, dim3((unsigned)B), dim3(256), 0, st, rows, B, kprime,
+                     row_offset, ovf, eps, ovf_out, eps_out);
+  return launch_check("export_list_kernel");
+}
+
+template <int DT, bool VEC>
+__global__ __launch_bounds__(RTHREADS) void rescore_owned_kernel(
+    const double* __restrict__ q64, int d, const void* __restrict__ cat, int64_t ld,
+    const double* __restrict__ gnorm, int64_t row_offset, int64_t n_local,
+    const float* __restrict__ cand_vals, const int64_t* __restrict__ cand_rows, int kprime, int k,
+    const float* __restrict__ eps, double* __restrict__ exact) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* qs = (double*)smem;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = blockIdx.x;
+  for (int j = tid; j < d; j += RTHREADS) qs[j] = q64[b * d + j];
+  __syncthreads();
+  const float* cv = cand_vals + b * kprime;
+  const double cut = (double)cv[k - 1] - 2.0 * (double)eps[b];
+  for (int c = wave; c < kprime; c += RTHREADS / 64) {
+    const int64_t g = cand_rows[b * kprime + c];
+    const int64_t row = g - row_offset;
+    const bool mine = g >= 0 && row >= 0 && row < n_local && !((double)cv[c] < cut);
+    double s = 0.0;
+    if (mine) {
+      if constexpr (VEC) {
+        constexpr int ES = (DT == EBT_F64) ? 8 : (DT == EBT_F32 ? 4 : 2);
+        constexpr int PER = 16 / ES;
+        const char* base = (const char*)cat + row * ld * ES;
+        for (int ch = lane; ch < d / PER; ch += 64) {
+          const uint4 raw = *(const uint4*)(base + (int64_t)ch * 16);
+          const int j0 = ch * PER;
+          if constexpr (DT == EBT_F32) {
+            const float* f = (const float*)&raw;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s += qs[j0 + e] * (double)f[e];
+          } else if constexpr (DT == EBT_F64) {
+            const double* f = (const double*)&raw;
+            s += qs[j0] * f[0] + qs[j0 + 1] * f[1];
+          } else {
+            const uint16_t* h = (const uint16_t*)&raw;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              s += qs[j0 + e] * (DT == EBT_BF16 ? bf16_bits_to_f64(h[e]) : f16_bits_to_f64(h[e]));
+          }
+        }
+      } else {
+        for (int j = lane; j < d; j += 64) s += qs[j] * load_as_f64<DT>(cat, row * ld + j);
+      }
+      s = wave_sum_f64(s);
+    }
+    if (lane == 0) exact[b * kprime + c] = mine ? s / gnorm[row] : 0.0;
+  }
+}
+
+int rescore_owned(const double* q64, int64_t B, int32_t d, const void* cat, int dtype, int64_t ld,
+                  const double* gnorm, int64_t row_offset, int64_t n_local,
+                  const float* cand_vals, const int64_t* cand_rows, int32_t kprime, int32_t k,
+                  const float* eps, double* exact, hipStream_t st) {
+  if (!q64 || !cat || !gnorm || !cand_vals || !cand_rows || !eps || !exact || B < 0 || d <= 0 ||
+      ld < d || k < 1 || kprime < k || kprime > 4096 || dtype < 0 || dtype > 3 || n_local < 0) {
+    set_error("ebt_rescore_owned: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  const size_t lds = (size_t)((d + 1) & ~1) * 8;
+  if (lds > 150 * 1024) {
+    set_error("ebt_rescore_owned: d=%d exceeds LDS", d);
+    return EBT_EUNSUPPORTED;
+  }
+  const int es = dtype == EBT_F64 ? 8 : (dtype == EBT_F32 ? 4 : 2);
+  const bool vec = (((uintptr_t)cat & 15) == 0) && ((ld * es) % 16 == 0) &&
+                   (((int64_t)d * es) % 16 == 0);
+  dim3 grid((unsigned)B), block(RTHREADS);
+#define EBT_RO(DT)                                                                              \
+  (void)hipFuncSetAttribute((const void*)rescore_owned_kernel<DT, true>,                        \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
+  (void)hipFuncSetAttribute((const void*)rescore_owned_kernel<DT, false>,                       \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
+  if (vec)                                                                                      \
+    hipLaunchKernelGGL((rescore_owned_kernel<DT, true>), grid, block, lds, st, q64, d, cat, ld, \
+                       gnorm, row_offset, n_local, cand_vals, cand_rows, kprime, k, eps, exact); \
+  else                                                                                          \
+    hipLaunchKernelGGL((rescore_owned_kernel<DT, false>), grid, block, lds, st, q64, d, cat,    \
+                       ld, gnorm, row_offset, n_local, cand_vals, cand_rows, kprime, k, eps,    \
+                       exact);
+  switch (dtype) {
+    case EBT_F32: EBT_RO(EBT_F32) break;
+    case EBT_BF16: EBT_RO(EBT_BF16) break;
+    case EBT_F16: EBT_RO(EBT_F16) break;
+    default: EBT_RO(EBT_F64) break;
+  }
+#undef EBT_RO
+  return launch_check("rescore_owned_kernel");
+}
+
+// Sort the merged candidates above the cut by (exact desc, row asc), keep k, certify.
+__global__ __launch_bounds__(RTHREADS) void finalize_topk_kernel(
+    const float* __restrict__ cand_vals, const int64_t* __restrict__ cand_rows,
+    const double* __restrict__ exact, int kprime, int kpp, int k, int64_t n_rows,
+    const float* __restrict__ eps, const int32_t* __restrict__ ovf, double* __restrict__ out_s,
+    int64_t* __restrict__ out_r, int32_t* __restrict__ certified) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* sc = (double*)smem;
+  int64_t* rw = (int64_t*)(sc + kpp);
+  __shared__ int nvalid;
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  if (tid == 0) nvalid = 0;
+  __syncthreads();
+  const float* cv = cand_vals + b * kprime;
+  const double cut = (double)cv[k - 1] - 2.0 * (double)eps[b];
+  int myvalid = 0;
+  for (int c = tid; c < kpp; c += RTHREADS) {
+    const int64_t r = c < kprime ? cand_rows[b * kprime + c] : -1;
+    if (r >= 0) {
+      ++myvalid;
+      const double v = exact[b * kprime + c];
+      sc[c] = ((double)cv[c] < cut || !(v == v)) ? -__builtin_inf() : v;
+      rw[c] = r;
+    } else {
+      sc[c] = -__builtin_inf();
+      rw[c] = INT64_MAX;
+    }
+  }
+  if (myvalid) atomicAdd(&nvalid, myvalid);
+  __syncthreads();
+  bitonic_pairs(sc, rw, kpp);
+  for (int j = tid; j < k; j += RTHREADS) {
+    const int64_t r = rw[j];
+    if (r == INT64_MAX) {
+      out_s[b * k + j] = __builtin_nan("");
+      out_r[b * k + j] = -1;
+    } else {
+      out_s[b * k + j] = sc[j];
+      out_r[b * k + j] = r;
+    }
+  }
+  if (tid == 0) {
+    int ok = 1;
+    if (nvalid >= kprime && n_rows > kprime)
+      ok = (double)cv[kprime - 1] < (double)cv[k - 1] - 2.0 * (double)eps[b];
+    if (ovf && ovf[b]) ok = -1;
+    certified[b] = ok;
+  }
+}
+
+int finalize_topk(const float* cand_vals, const int64_t* cand_rows, const double* exact,
+                  int64_t B, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
+                  const int32_t* ovf, double* out_s, int64_t* out_r, int32_t* certified,
+                  hipStream_t st) {
+  if (!cand_vals || !cand_rows || !exact || !eps || !out_s || !out_r || !certified || B < 0 ||
+      k < 1 || kprime < k || kprime > 4096) {
+    set_error("ebt_finalize_topk: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  const int kpp = next_pow2_h(kprime);
+  const size_t lds = (size_t)kpp * 16;
+  (void)hipFuncSetAttribute((const void*)finalize_topk_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(finalize_topk_kernel, dim3((unsigned)B), dim3(RTHREADS), lds, st, cand_vals,
+                     cand_rows, exact, kprime, kpp, k, n_rows, eps, ovf, out_s, out_r, certified);
+  return launch_check("finalize_topk_kernel");
+}
+
 }  // namespace ebt

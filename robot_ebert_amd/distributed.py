@@ -2,12 +2,26 @@
 
 The reference scales only by Cloud Run replicas (README.md:78-82) and has no collective. Here
 the catalog rows are split into contiguous blocks, rank r holding rows
-[shard_range(n, r, R)), and every rank scores the full query batch against its shard (global row
-ids via ``row_offset``). The ONE exchange step is an all-gather of the per-shard top-k
-(B x k float64 scores + B x k int64 rows, a few MB) over RCCL/xGMI, followed by the
-``ebt_merge_topk`` kernel on every rank. For the collaborative path the liked rows of a user live
-on several shards: each rank sums its local normalised liked rows and one all-reduce (SUM) of the
-B x d float64 partial sums completes the query vectors before screening.
+[shard_range(n, r, R)), and every rank screens the full query batch against its shard (global row
+ids via ``row_offset``). Two exchange patterns:
+
+* ``score_topk_sharded`` (two-phase): every rank screens its shard
+  (``ebt_cosine_screen``: approx k' candidates, no rescore), ONE all-gather of the candidate lists
+  (B x k' f32 + i64 over RCCL/xGMI), every rank keeps the k' best of all shards, computes the
+  exact float64 scores of the merged candidates IT owns (``ebt_rescore_owned``), ONE all-reduce
+  (SUM, B x k' f64) completes them, and ``ebt_finalize_topk`` sorts and certifies. Each candidate
+  row is gathered and rescored once in the whole job instead of once per shard. Simulated on one
+  GPU (tools/shard_sim.py) its per-rank compute at 8 ranks of C3 is within 2 % of the other
+  path's while it moves more data (B x k' candidates + a B x k' all-reduce), so it is offered,
+  not the bench default.
+* ``score_topk_sharded_local`` (bench.py's N > 1 step): every rank runs the full single-GPU path
+  on its shard and the per-shard exact top-k are all-gathered and merged (``ebt_merge_topk``):
+  one collective of B x k (f64, i64) per step.
+
+For the collaborative path the liked rows of a user live on several shards: each rank sums its
+local normalised liked rows and one all-reduce (SUM) of the B x d float64 partial sums completes
+the query vectors before screening. Retries (uncertified / overflowed queries) are decided from
+all-gathered data, so every rank takes the same retry and the collectives stay in lockstep.
 """
 from __future__ import annotations
 
@@ -16,8 +30,11 @@ from typing import Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from . import _lib
+from ._lib import EbertError, call, ptr, stream_of
 from .catalog import Catalog
-from .search import csr_from_lists, merge_topk, score_topk
+from .search import (KPRIME_MAX, _round_up, csr_from_lists, csr_subset, default_kprime,
+                     merge_topk, prepare_queries, run_screen, score_topk)
 
 
 def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
@@ -48,25 +65,137 @@ def split_liked(liked: Sequence[Sequence[int]], begin: int, end: int):
     return local, counts
 
 
+class TorchCollectives:
+    """The three collectives the two-phase path uses, over a torch.distributed group (RCCL on
+    MI355X: backend "nccl"; gloo on CPU)."""
+
+    def __init__(self, group: Optional[dist.ProcessGroup] = None) -> None:
+        self.group = group
+        self.world = dist.get_world_size(group)
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
+                          device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out.view((self.world,) + tuple(t.shape))
+
+    def all_reduce_sum(self, t: torch.Tensor) -> torch.Tensor:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def all_reduce_max(self, t: torch.Tensor) -> torch.Tensor:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return t
+
+
+def _liked_queries(catalog: Catalog, liked, coll):
+    local, counts = split_liked(liked, catalog.row_offset, catalog.row_offset + catalog.n)
+    dev = catalog.device
+    return (csr_from_lists(local, dev), torch.tensor(counts, dtype=torch.int64, device=dev),
+            lambda q64: coll.all_reduce_sum(q64))
+
+
+def _two_phase(catalog: Catalog, qb, k: int, kprime: int, exclude, chunk_rows, timer, flags,
+               coll):
+    dev = catalog.device
+    st = stream_of(dev)
+    B = qb.B
+    lv, lr, ovf, eps = run_screen(catalog, qb, k, kprime, exclude, chunk_rows, timer, flags)
+    R = coll.world
+    gv = coll.all_gather(lv)        # [R, B, k']
+    gr = coll.all_gather(lr)
+    ovf = coll.all_reduce_max(ovf)
+    # every rank: the k' best of all shards (rows are the select's indices)
+    vals = gv.permute(1, 0, 2).reshape(B, R * kprime).contiguous()
+    rows = gr.permute(1, 0, 2).reshape(B, R * kprime).contiguous()
+    mv = torch.empty((B, kprime), dtype=torch.float32, device=dev)
+    mr = torch.empty((B, kprime), dtype=torch.int64, device=dev)
+    call("ebt_select_topk", ptr(vals), ptr(rows), R * kprime, B, R * kprime, 0, kprime, 1,
+         ptr(mv), ptr(mr), kprime, st)
+    exact = torch.empty((B, kprime), dtype=torch.float64, device=dev)
+    call("ebt_rescore_owned", ptr(qb.q64), B, catalog.d, ptr(catalog.data), catalog.dtype_code,
+         catalog.ld, ptr(catalog.gnorm), catalog.row_offset, catalog.n, ptr(mv), ptr(mr), kprime,
+         k, ptr(eps), ptr(exact), st)
+    exact = coll.all_reduce_sum(exact)
+    out_s = torch.empty((B, k), dtype=torch.float64, device=dev)
+    out_r = torch.empty((B, k), dtype=torch.int64, device=dev)
+    cert = torch.empty(B, dtype=torch.int32, device=dev)
+    call("ebt_finalize_topk", ptr(mv), ptr(mr), ptr(exact), B, kprime, k, catalog.n_global,
+         ptr(eps), ptr(ovf), ptr(out_s), ptr(out_r), ptr(cert), st)
+    return out_s, out_r, cert
+
+
 def score_topk_sharded(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
                        liked: Optional[Sequence[Sequence[int]]] = None,
                        exclude=None, group: Optional[dist.ProcessGroup] = None,
-                       **kw) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Global top-k over a row-sharded catalog; every rank returns the same [B, k] result."""
+                       kprime: Optional[int] = None, chunk_rows: Optional[int] = None,
+                       timer=None, fuse: bool = True, collectives=None
+                       ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Global top-k over a row-sharded catalog, two-phase (see the module doc); every rank
+    returns the same (scores f64 [B, k], GLOBAL rows i64 [B, k]). ``exclude``: per-query GLOBAL
+    rows (lists or device CSR). ``collectives`` replaces the torch.distributed calls (tests)."""
+    coll = collectives if collectives is not None else TorchCollectives(group)
     dev = catalog.device
-    hook = None
-    liked_arg = None
-    counts_t = None
+    if k < 1:
+        raise EbertError("k must be >= 1")
+    if exclude is not None and not isinstance(exclude, tuple):
+        exclude = csr_from_lists(exclude, dev)
     if liked is not None:
-        local, counts = split_liked(liked, catalog.row_offset, catalog.row_offset + catalog.n)
-        liked_arg = csr_from_lists(local, dev)
-        counts_t = torch.tensor(counts, dtype=torch.int64, device=dev)
+        liked_csr, counts, hook = _liked_queries(catalog, liked, coll)
+        qb = prepare_queries(catalog, liked=liked_csr, liked_counts=counts, liked_sum_hook=hook)
+    else:
+        qb = prepare_queries(catalog, queries=queries)
+    n_cap = _round_up(catalog.n_global, 4)
+    k_eff = min(k, catalog.n_global)
+    if k_eff > KPRIME_MAX:
+        raise EbertError(f"k={k} > {KPRIME_MAX} is not supported")
+    kp = kprime or default_kprime(catalog, k_eff)
+    kp = max(_round_up(k_eff, 4), min(_round_up(kp, 4), n_cap, KPRIME_MAX))
+    flags = 0 if fuse else _lib.EBT_FLAG_NO_FUSE
+    s, r, cert = _two_phase(catalog, qb, k_eff, kp, exclude, chunk_rows, timer, flags, coll)
+    while True:  # identical certificates on every rank -> identical retries
+        flat = cert.cpu()
+        over = torch.nonzero(flat == -1).flatten().to(dev)
+        bad = torch.nonzero(flat == 0).flatten().to(dev)
+        if over.numel() == 0 and bad.numel() == 0:
+            break
+        if over.numel():
+            sub_ex = csr_subset(exclude[0], exclude[1], over) if exclude is not None else None
+            s2, r2, c2 = _two_phase(catalog, qb.subset(over), k_eff, kp, sub_ex, chunk_rows,
+                                    timer, _lib.EBT_FLAG_NO_FUSE, coll)
+            s[over], r[over], cert[over] = s2, r2, c2
+            continue
+        widen = kp < min(n_cap, KPRIME_MAX)
+        if not widen and flags & _lib.EBT_FLAG_EXACT:
+            raise EbertError(f"{bad.numel()} queries could not be certified at k'={kp} "
+                             "(more than k' rows tie with the k-th score at f32 precision)")
+        if widen:
+            kp = min(kp * 4, n_cap, KPRIME_MAX)
+        else:
+            flags = _lib.EBT_FLAG_EXACT
+            kp = max(_round_up(k_eff, 4), min(_round_up(default_kprime(catalog, k_eff), 4),
+                                              n_cap, KPRIME_MAX))
+        sub_ex = csr_subset(exclude[0], exclude[1], bad) if exclude is not None else None
+        s2, r2, c2 = _two_phase(catalog, qb.subset(bad), k_eff, kp, sub_ex, chunk_rows, timer,
+                                flags, coll)
+        s[bad], r[bad], cert[bad] = s2, r2, c2
+    if k_eff < k:
+        pad_s = torch.full((qb.B, k - k_eff), float("nan"), dtype=torch.float64, device=dev)
+        pad_r = torch.full((qb.B, k - k_eff), -1, dtype=torch.int64, device=dev)
+        s, r = torch.cat([s, pad_s], 1), torch.cat([r, pad_r], 1)
+    return s, r
 
-        def hook(q64: torch.Tensor) -> torch.Tensor:
-            dist.all_reduce(q64, op=dist.ReduceOp.SUM, group=group)
-            return q64
 
+def score_topk_sharded_local(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
+                             liked: Optional[Sequence[Sequence[int]]] = None,
+                             exclude=None, group: Optional[dist.ProcessGroup] = None,
+                             collectives=None, **kw) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-shard exact top-k (the single-GPU path on each shard) + all-gather + merge."""
+    coll = collectives if collectives is not None else TorchCollectives(group)
+    dev = catalog.device
+    liked_arg = counts_t = hook = None
+    if liked is not None:
+        liked_arg, counts_t, hook = _liked_queries(catalog, liked, coll)
     s, r = score_topk(catalog, k, queries=queries, liked=liked_arg, exclude=exclude,
                       liked_counts=counts_t, liked_sum_hook=hook, **kw)
-    gs, gr = gather_partials(s, r, group)
-    return merge_topk(gs, gr, k)
+    return merge_topk(coll.all_gather(s), coll.all_gather(r), k)

@@ -212,6 +212,33 @@ def run_pipeline(catalog: Catalog, qb: QueryBatch, k: int, kprime: int,
     return out_s, out_r, cert
 
 
+def run_screen(catalog: Catalog, qb: QueryBatch, k: int, kprime: int,
+               exclude: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+               chunk_rows: Optional[int] = None, timer: Optional[_lib.Timer] = None,
+               flags: int = 0):
+    """Phase 1 of the two-phase sharded top-k (ebt_cosine_screen): this shard's k' best approx
+    candidates. Returns (vals f32 [B,k'], GLOBAL rows i64 [B,k'], ovf i32 [B], eps f32 [B])."""
+    dev = catalog.device
+    B, B_pad = qb.B, qb.B_pad
+    chunk = chunk_rows or _chunk_rows(catalog, B_pad, DEFAULT_SCORE_BUDGET)
+    need = _lib.load().ebt_cosine_topk_workspace(B, B_pad, catalog.n, kprime, chunk, flags)
+    if need == 0:
+        raise EbertError("invalid workspace request")
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    lv = torch.empty((B, kprime), dtype=torch.float32, device=dev)
+    lr = torch.empty((B, kprime), dtype=torch.int64, device=dev)
+    ovf = torch.empty(B, dtype=torch.int32, device=dev)
+    eps = torch.empty(B, dtype=torch.float32, device=dev)
+    eo, er = (exclude if exclude is not None else (None, None))
+    call("ebt_cosine_screen", ptr(qb.q64), ptr(qb.qimg), ptr(qb.qscale), ptr(qb.eps), B, B_pad,
+         ptr(catalog.data), catalog.dtype_code, catalog.ld, ptr(catalog.gnorm), ptr(catalog.image),
+         ptr(catalog.cscale), catalog.img_dtype, catalog.ld_img, catalog.n, catalog.d,
+         catalog.d_pad, catalog.row_offset, ptr(eo), ptr(er), k, kprime, chunk, flags, ptr(ws),
+         int(ws.numel()), ptr(lv), ptr(lr), ptr(ovf), ptr(eps),
+         timer.handle if timer is not None else None, stream_of(dev))
+    return lv, lr, ovf, eps
+
+
 def score_topk(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
                liked: Optional[Union[Tuple[torch.Tensor, torch.Tensor], Sequence[Sequence[int]]]] = None,
                exclude: Optional[Union[Tuple[torch.Tensor, torch.Tensor], Sequence[Sequence[int]]]] = None,

@@ -65,6 +65,15 @@ def _body(rank, world, q):
         qmean = part.numpy() / np.array(counts)[:, None]
         want = np.stack([R.mean_cosine_query(c[l]) for l in liked])
         ok = ok and bool(np.allclose(qmean, want, atol=1e-14))
+        # the two-phase path's collectives wrapper (the GPU kernels around it need a GPU)
+        from robot_ebert_amd.distributed import TorchCollectives
+        coll = TorchCollectives()
+        g = coll.all_gather(torch.full((3, 4), float(rank)))
+        ok = ok and g.shape == (world, 3, 4) and all(bool((g[r] == r).all()) for r in range(world))
+        t = torch.full((5,), rank + 1.0, dtype=torch.float64)
+        ok = ok and bool((coll.all_reduce_sum(t) == sum(range(1, world + 1))).all())
+        m = torch.tensor([rank, 1 - rank], dtype=torch.int32)
+        ok = ok and coll.all_reduce_max(m).tolist() == [world - 1, 1]
         q.put((rank, ok))
 
 

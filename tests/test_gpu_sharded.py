@@ -1,0 +1,126 @@
+"""GPU: the two-phase sharded top-k (distributed.score_topk_sharded) on ONE GPU, R ranks
+simulated by R threads whose collectives are an in-process exchange (same tensors, same
+order as all_gather_into_tensor / all_reduce). Every rank's answer must equal the single-catalog
+score_topk and the float64 oracle; the torch.distributed calls themselves are covered by
+test_dist_gloo.py."""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from inputs import gaussian
+from oracle import restatement as R
+
+pytestmark = pytest.mark.gpu
+
+
+class ThreadCollectives:
+    def __init__(self, rank, shared):
+        self.rank, self.s = rank, shared
+        self.world = shared["world"]
+
+    def _exchange(self, t):
+        self.s["slots"][self.rank] = t.clone()
+        self.s["barrier"].wait()
+        vals = list(self.s["slots"])
+        self.s["barrier"].wait()
+        return vals
+
+    def all_gather(self, t):
+        return torch.stack(self._exchange(t))
+
+    def all_reduce_sum(self, t):
+        t.copy_(torch.stack(self._exchange(t)).sum(0))
+        return t
+
+    def all_reduce_max(self, t):
+        t.copy_(torch.stack(self._exchange(t)).max(0).values)
+        return t
+
+
+def _run_sharded(full, world, fn):
+    """fn(rank, catalog_shard, collectives) in `world` threads; returns the per-rank results."""
+    import robot_ebert_amd as ebt
+    from robot_ebert_amd.distributed import shard_range
+    n = full.shape[0]
+    shared = {"world": world, "slots": [None] * world, "barrier": threading.Barrier(world)}
+    cats = []
+    for r in range(world):
+        a, b = shard_range(n, r, world)
+        cats.append(ebt.Catalog(full[a:b].contiguous(), row_offset=a, n_global=n))
+    out, errs = [None] * world, []
+
+    def body(r):
+        try:
+            out[r] = fn(r, cats[r], ThreadCollectives(r, shared))
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            shared["barrier"].abort()
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(300)
+    if errs:
+        raise errs[0]
+    return out
+
+
+@pytest.mark.parametrize("world,dt", [(3, "f32"), (2, "bf16")])
+def test_two_phase_matches_single_and_oracle(cuda_device, world, dt):
+    import robot_ebert_amd as ebt
+    from robot_ebert_amd.distributed import score_topk_sharded
+    from test_gpu_parity import TORCH_DT, _t, assert_topk_equal
+    n, d, B, k = 150_000, 256, 70, 50
+    c = gaussian(31, n, d, dt)
+    q = gaussian(32, B, d, dt)
+    rng = np.random.default_rng(33)
+    excl = [sorted(rng.choice(n, 300, replace=False).tolist()) for _ in range(B)]
+    full = _t(c, dt, cuda_device)
+    qt = _t(q, dt, cuda_device)
+    res = _run_sharded(full, world, lambda r, cat, coll: score_topk_sharded(
+        cat, k, queries=qt, exclude=excl, collectives=coll))
+    single = ebt.score_topk(ebt.Catalog(full), k, queries=qt, exclude=excl)
+    for s, r in res:
+        assert torch.equal(r, single[1])
+        torch.testing.assert_close(s, single[0], rtol=0, atol=0)
+    sample = [0, 35, 69]
+    s_ref, r_ref = R.cosine_topk(q[sample].astype(np.float64), c.astype(np.float64), k,
+                                 [excl[i] for i in sample])
+    assert_topk_equal(res[0][0][sample], res[0][1][sample], s_ref, r_ref)
+
+
+def test_two_phase_liked_queries(cuda_device):
+    """Liked rows spread over shards: the all-reduce of partial sums completes the mean."""
+    from robot_ebert_amd.distributed import score_topk_sharded
+    from test_gpu_parity import _t, assert_topk_equal
+    n, d, k = 20_000, 64, 30
+    c = gaussian(41, n, d, "f64")
+    liked = [[1, 2, 19_999], [10_000], [5, 6_000, 12_000, 18_000]]
+    rated = [l + [7, 8] for l in liked]
+    full = _t(c, "f64", cuda_device)
+    res = _run_sharded(full, 3, lambda r, cat, coll: score_topk_sharded(
+        cat, k, liked=liked, exclude=rated, collectives=coll))
+    want_s, want_r = R.liked_topk(c, liked, k, rated)
+    for s, r in res:
+        assert_topk_equal(s, r, want_s, want_r)
+
+
+def test_two_phase_overflow_and_retry(cuda_device):
+    """Scores rising with the row id overflow the fused screen's hit slots on the last shard:
+    the flag is all-reduced, every rank reruns that query unfused, the answer stays exact."""
+    from robot_ebert_amd.distributed import score_topk_sharded
+    from test_gpu_parity import _t, assert_topk_equal
+    n, d, k = 300_000, 64, 16
+    rng = np.random.default_rng(9)
+    q = rng.standard_normal((2, d))
+    t = (np.arange(n) / n)[:, None]
+    c = q[0][None, :] * t + rng.standard_normal((n, d)) * (1.0 - t) * 0.5
+    full = _t(c, "f64", cuda_device)
+    qt = _t(q, "f64", cuda_device)
+    res = _run_sharded(full, 2, lambda r, cat, coll: score_topk_sharded(
+        cat, k, queries=qt, collectives=coll))
+    s_ref, r_ref = R.cosine_topk(q, c, k)
+    for s, r in res:
+        assert_topk_equal(s, r, s_ref, r_ref)
