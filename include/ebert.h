@@ -149,12 +149,17 @@ int ebt_select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B
  * fewer than kprime valid candidates, or approx[kprime-1] < approx[k-1] - 2*eps[b].
  * n_rows is the catalog's row count; a candidate row >= n_rows is never read and gives
  * certified[b] = -2 (corrupt candidate list).
- * Candidates with approx < approx[k-1] - 2*eps[b] cannot be in the top k and are not gathered
- * (equal cand_vals and eps = 0 rescore every candidate). */
+ * Candidates with approx < max(approx[k-1] - 2*eps[b], t_floor[b] - eps[b]) cannot be in the
+ * top k and are not gathered (equal cand_vals and eps = 0 rescore every candidate). t_floor
+ * (float64 [B], NULL = none) is a lower bound of the k-th best EXACT score over the whole
+ * (sharded) catalog, e.g. the all-reduced max over shards of approx[k-1] - eps: a shard then
+ * rescores only rows that can enter the GLOBAL top k, and the slots of its top k that such a
+ * cut leaves empty read NaN / -1. The certificate is unchanged (it is about this list). */
 int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype, int64_t ld,
                 const double* gnorm64, int64_t row_offset, const float* cand_vals,
                 const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
-                double* out_scores, int64_t* out_rows, int32_t* certified, void* stream);
+                const double* t_floor, double* out_scores, int64_t* out_rows, int32_t* certified,
+                void* stream);
 
 /* The fused screen's merge step: query b's list (fv/fi[b*kprime + j], sorted desc as
  * ebt_select_topk leaves it) and the hits ebt_screen_filter left in `n_groups` groups of

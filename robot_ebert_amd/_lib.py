@@ -60,7 +60,7 @@ _SIGNATURES = {
     "ebt_select_topk": ([_VP, _VP, _I64, _I64, _I64, _I64, _I32, _I32, _VP, _VP, _I64, _VP],
                         _INT),
     "ebt_rescore": ([_VP, _I64, _I32, _VP, _INT, _I64, _VP, _I64, _VP, _VP, _I32, _I32, _I64, _VP,
-                     _VP, _VP, _VP, _VP], _INT),
+                     _VP, _VP, _VP, _VP, _VP], _INT),
     "ebt_merge_topk": ([_VP, _VP, _I32, _I64, _I32, _VP, _VP, _VP], _INT),
     "ebt_screen_exact": ([_VP, _I64, _I32, _VP, _INT, _I64, _VP, _I64, _VP, _I64, _VP], _INT),
     "ebt_cosine_topk_workspace": ([_I64, _I64, _I64, _I32, _I64, _INT], _SZ),

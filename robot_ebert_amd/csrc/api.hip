@@ -45,8 +45,8 @@ int query_image(const double*, int64_t, int64_t, int32_t, int, const void*, int6
 int mask_excluded(float*, int64_t, int64_t, int64_t, int64_t, const int64_t*, const int64_t*,
                   hipStream_t);
 int rescore(const double*, int64_t, int32_t, const void*, int, int64_t, const double*, int64_t,
-            const float*, const int64_t*, int32_t, int32_t, int64_t, const float*, double*, int64_t*,
-            int32_t*, hipStream_t, const int*, int);
+            const float*, const int64_t*, int32_t, int32_t, int64_t, const float*, const double*,
+            double*, int64_t*, int32_t*, hipStream_t, const int*, int);
 int screen_gemm_filter(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
                        const float*, const float*, const float*, uint64_t*, int64_t, int,
                        uint8_t*, int64_t, int*, int64_t, hipStream_t);
@@ -363,9 +363,11 @@ int ebt_select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B
 int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype, int64_t ld,
                 const double* gnorm64, int64_t row_offset, const float* cand_vals,
                 const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
-                double* out_scores, int64_t* out_rows, int32_t* certified, void* stream) {
-  return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, cand_vals, cand_rows, kprime, k, n_rows,
-                 eps, out_scores, out_rows, certified, (hipStream_t)stream, nullptr, 0);
+                const double* t_floor, double* out_scores, int64_t* out_rows, int32_t* certified,
+                void* stream) {
+  return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, cand_vals, cand_rows, kprime, k,
+                 n_rows, eps, t_floor, out_scores, out_rows, certified, (hipStream_t)stream,
+                 nullptr, 0);
 }
 
 int ebt_screen_exact(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
@@ -613,7 +615,7 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
   if (rc) return rc;
   StageScope s(timer, EBT_STAGE_RESCORE, st);
   return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, fv, fi, kprime, k, n_rows,
-                 so.eps, out_scores, out_rows, certified, st, so.ovf, 0);
+                 so.eps, nullptr, out_scores, out_rows, certified, st, so.ovf, 0);
 }
 
 int ebt_cosine_screen(const double* q64, const void* qimg, const float* qscale, const float* eps,

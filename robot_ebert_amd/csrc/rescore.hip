@@ -49,84 +49,145 @@ static int next_pow2_h(int v) {
   return p;
 }
 
+// Sum of q . row over one lane's share of the row (16-byte chunks ch = lane, lane+64, ...),
+// accumulated in chunk order; the caller's wave_sum_f64 completes the dot product.
+template <int DT>
+__device__ __forceinline__ double chunk_dot(const double* qs, int j0, uint4 raw) {
+  double s = 0.0;
+  if constexpr (DT == EBT_F32) {
+    const float* f = (const float*)&raw;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += qs[j0 + e] * (double)f[e];
+  } else if constexpr (DT == EBT_F64) {
+    const double* f = (const double*)&raw;
+    s += qs[j0] * f[0] + qs[j0 + 1] * f[1];
+  } else {
+    const uint16_t* h = (const uint16_t*)&raw;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      s += qs[j0 + e] * (DT == EBT_BF16 ? bf16_bits_to_f64(h[e]) : f16_bits_to_f64(h[e]));
+  }
+  return s;
+}
+
 template <int DT, bool VEC>
 __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     const double* __restrict__ q64, int d, const void* __restrict__ cat, int64_t ld,
     const double* __restrict__ gnorm, int64_t row_offset, const float* __restrict__ cand_vals,
     const int64_t* __restrict__ cand_rows, int kprime, int kpp, int k, int64_t n_rows,
-    const float* __restrict__ eps, double* __restrict__ out_s, int64_t* __restrict__ out_r,
-    int32_t* __restrict__ certified, const int* __restrict__ ovf_cnt, int ovf_cap) {
+    const float* __restrict__ eps, const double* __restrict__ t_floor, double* __restrict__ out_s,
+    int64_t* __restrict__ out_r, int32_t* __restrict__ certified, const int* __restrict__ ovf_cnt,
+    int ovf_cap) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* qs = (double*)smem;                 // d
   double* sc = qs + ((d + 1) & ~1);           // kpp
   int64_t* rw = (int64_t*)(sc + kpp);         // kpp
-  __shared__ int nvalid, corrupt;
+  __shared__ int nvalid, corrupt, nkeep;
+  constexpr int NW = RTHREADS / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
   if (tid == 0) {
     nvalid = 0;
     corrupt = 0;
+    nkeep = 0;
   }
   for (int j = tid; j < d; j += RTHREADS) qs[j] = q64[b * d + j];
-  __syncthreads();
   const int64_t* cr = cand_rows + b * kprime;
   // Candidates whose approx score is below approx[k-1] - 2 eps cannot be in the top k (the k
   // best candidates all have exact >= approx[k-1] - eps > their exact), so their rows are not
   // gathered: about k + (rows in the 2 eps band) of the k' candidates are rescored.
+  // t_floor (optional): a lower bound of the k-th best EXACT score over the whole (sharded)
+  // catalog, e.g. max over shards of (shard's approx[k-1] - eps). A row of the global top k has
+  // exact >= t_floor, so approx >= t_floor - eps: the cut may rise to that.
   const float* cv = cand_vals + b * kprime;
-  const double cut = (double)cv[k - 1] - 2.0 * (double)eps[b];
-  int myvalid = 0;
-  for (int c = wave; c < kprime; c += RTHREADS / 64) {
-    const int64_t row = cr[c] < n_rows ? cr[c] : -2;  // -2: corrupt entry, never dereferenced
-    if (row == -2 && lane == 0) corrupt = 1;
-    const bool skip = (double)cv[c] < cut;
-    double s = 0.0;
-    if (row >= 0 && !skip) {
-      if constexpr (VEC) {
-        constexpr int ES = (DT == EBT_F64) ? 8 : (DT == EBT_F32 ? 4 : 2);
-        constexpr int PER = 16 / ES;
-        const char* base = (const char*)cat + row * ld * ES;
-        for (int ch = lane; ch < d / PER; ch += 64) {
-          const uint4 raw = *(const uint4*)(base + (int64_t)ch * 16);
-          const int j0 = ch * PER;
-          if constexpr (DT == EBT_F32) {
-            const float* f = (const float*)&raw;
+  double cut = (double)cv[k - 1] - 2.0 * (double)eps[b];
+  if (t_floor && t_floor[b] - (double)eps[b] > cut) cut = t_floor[b] - (double)eps[b];
+  __syncthreads();
+  // 1. the whole list at once (no per-candidate load latency): count valid rows, flag corrupt
+  //    ones, compact the rows above the cut into rw[0, nkeep)
+  for (int c0 = 0; c0 < kprime; c0 += RTHREADS) {
+    const int c = c0 + tid;
+    int64_t row = -1;
+    float v = 0.f;
+    if (c < kprime) {
+      row = cr[c];
+      v = cv[c];
+    }
+    const bool bad = c < kprime && row >= n_rows;  // corrupt entry, never dereferenced
+    const bool valid = c < kprime && row >= 0 && !bad;
+    const bool keep = valid && !((double)v < cut);
+    if (bad) corrupt = 1;
+    const uint64_t vb = __ballot(valid), kb = __ballot(keep);
+    int base = 0;
+    if (lane == 0) {
+      if (vb) atomicAdd(&nvalid, __popcll(vb));
+      if (kb) base = atomicAdd(&nkeep, __popcll(kb));
+    }
+    base = __shfl(base, 0, 64);
+    if (keep) rw[base + __popcll(kb & ((1ull << lane) - 1))] = row;
+  }
+  __syncthreads();
+  const int nk = nkeep;
+  // 2. exact scores, two rows per wave at a time with all of a lane's loads for both rows
+  //    issued before the arithmetic (chunk order per lane unchanged: bit-identical sums)
+  for (int j = wave; j < nk; j += 2 * NW) {
+    const int jb = j + NW;
+    const bool hb = jb < nk;
+    const int64_t ra = rw[j], rb = hb ? rw[jb] : ra;
+    const double ga = gnorm[ra], gb = gnorm[rb];
+    double sa = 0.0, sb = 0.0;
+    if constexpr (VEC) {
+      constexpr int ES = (DT == EBT_F64) ? 8 : (DT == EBT_F32 ? 4 : 2);
+      constexpr int PER = 16 / ES;
+      constexpr int U = 4;
+      const int nch = d / PER;
+      const char* pa = (const char*)cat + ra * ld * ES;
+      const char* pb = (const char*)cat + rb * ld * ES;
+      for (int ch0 = lane; ch0 < nch; ch0 += 64 * U) {
+        uint4 xa[U], xb[U];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) s += qs[j0 + e] * (double)f[e];
-          } else if constexpr (DT == EBT_F64) {
-            const double* f = (const double*)&raw;
-            s += qs[j0] * f[0] + qs[j0 + 1] * f[1];
-          } else {
-            const uint16_t* h = (const uint16_t*)&raw;
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              s += qs[j0 + e] * (DT == EBT_BF16 ? bf16_bits_to_f64(h[e]) : f16_bits_to_f64(h[e]));
+        for (int u = 0; u < U; ++u) {
+          const int ch = ch0 + 64 * u;
+          if (ch < nch) {
+            xa[u] = *(const uint4*)(pa + (int64_t)ch * 16);
+            if (hb) xb[u] = *(const uint4*)(pb + (int64_t)ch * 16);
           }
         }
-      } else {
-        for (int j = lane; j < d; j += 64) s += qs[j] * load_as_f64<DT>(cat, row * ld + j);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int ch = ch0 + 64 * u;
+          if (ch < nch) {
+            sa += chunk_dot<DT>(qs, ch * PER, xa[u]);
+            if (hb) sb += chunk_dot<DT>(qs, ch * PER, xb[u]);
+          }
+        }
+      }
+    } else {
+      for (int e = lane; e < d; e += 64) {
+        sa += qs[e] * load_as_f64<DT>(cat, ra * ld + e);
+        if (hb) sb += qs[e] * load_as_f64<DT>(cat, rb * ld + e);
       }
     }
-    s = wave_sum_f64(s);
+    sa = wave_sum_f64(sa);
+    sb = wave_sum_f64(sb);
     if (lane == 0) {
-      if (row >= 0) {
-        const double v = s / gnorm[row];
-        sc[c] = (v == v && !skip) ? v : -__builtin_inf();
-        rw[c] = row;
-        ++myvalid;
-      } else {
-        sc[c] = -__builtin_inf();
-        rw[c] = INT64_MAX;
+      const double va = sa / ga;
+      sc[j] = (va == va) ? va : -__builtin_inf();
+      if (hb) {
+        const double vb2 = sb / gb;
+        sc[jb] = (vb2 == vb2) ? vb2 : -__builtin_inf();
       }
     }
   }
-  for (int c = kprime + tid; c < kpp; c += RTHREADS) {
+  // 3. sort the kept rows (padded to a power of two >= k); slots past them read NaN / -1
+  int P = 1;
+  while (P < nk || P < k) P <<= 1;
+  for (int c = nk + tid; c < P; c += RTHREADS) {
     sc[c] = -__builtin_inf();
     rw[c] = INT64_MAX;
   }
-  if (lane == 0 && myvalid) atomicAdd(&nvalid, myvalid);
   __syncthreads();
-  bitonic_pairs(sc, rw, kpp);
+  bitonic_pairs(sc, rw, P);
   for (int j = tid; j < k; j += RTHREADS) {
     const int64_t r = rw[j];
     if (r == INT64_MAX) {
@@ -158,8 +219,8 @@ size_t rescore_lds_bytes(int d, int kprime) {
 int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype, int64_t ld,
             const double* gnorm, int64_t row_offset, const float* cand_vals,
             const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
-            double* out_s, int64_t* out_r, int32_t* certified, hipStream_t st,
-            const int* ovf_cnt, int ovf_cap) {
+            const double* t_floor, double* out_s, int64_t* out_r, int32_t* certified,
+            hipStream_t st, const int* ovf_cnt, int ovf_cap) {
   if (!q64 || !cat || !gnorm || !cand_vals || !cand_rows || !eps || !out_s || !out_r ||
       !certified || B < 0 || d <= 0 || ld < d || k < 1 || kprime < k || kprime > 4096 ||
       dtype < 0 || dtype > 3) {
@@ -184,12 +245,12 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
   if (vec)                                                                                      \
     hipLaunchKernelGGL((rescore_kernel<DT, true>), grid, block, lds, st, q64, d, cat, ld,       \
-                       gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps, out_s, \
-                       out_r, certified, ovf_cnt, ovf_cap);                                     \
+                       gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,    \
+                       t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap);                     \
   else                                                                                          \
     hipLaunchKernelGGL((rescore_kernel<DT, false>), grid, block, lds, st, q64, d, cat, ld,      \
-                       gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps, out_s, \
-                       out_r, certified, ovf_cnt, ovf_cap);
+                       gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,    \
+                       t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap);
   switch (dtype) {
     case EBT_F32: EBT_RS(EBT_F32) break;
     case EBT_BF16: EBT_RS(EBT_BF16) break;

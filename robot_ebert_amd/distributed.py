@@ -34,7 +34,7 @@ from . import _lib
 from ._lib import EbertError, call, ptr, stream_of
 from .catalog import Catalog
 from .search import (KPRIME_MAX, _round_up, csr_from_lists, csr_subset, default_kprime,
-                     merge_topk, prepare_queries, run_screen, score_topk)
+                     merge_topk, prepare_queries, run_screen, score_topk, union_floor)
 
 
 def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
@@ -196,6 +196,7 @@ def score_topk_sharded_local(catalog: Catalog, k: int, queries: Optional[torch.T
     liked_arg = counts_t = hook = None
     if liked is not None:
         liked_arg, counts_t, hook = _liked_queries(catalog, liked, coll)
+    kw.setdefault("t_floor_hook", lambda v, e: union_floor(coll.all_gather(v), coll.all_gather(e), k))
     s, r = score_topk(catalog, k, queries=queries, liked=liked_arg, exclude=exclude,
                       liked_counts=counts_t, liked_sum_hook=hook, **kw)
     return merge_topk(coll.all_gather(s), coll.all_gather(r), k)

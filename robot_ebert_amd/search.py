@@ -244,12 +244,23 @@ def score_topk(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
                exclude: Optional[Union[Tuple[torch.Tensor, torch.Tensor], Sequence[Sequence[int]]]] = None,
                kprime: Optional[int] = None, chunk_rows: Optional[int] = None,
                timer: Optional[_lib.Timer] = None, liked_counts: Optional[torch.Tensor] = None,
-               liked_sum_hook=None, fuse: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+               liked_sum_hook=None, fuse: bool = True,
+               t_floor_hook=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Top-k by cosine (mean cosine over liked rows) with exclusions.
 
     Returns (scores float64 [B, k], rows int64 [B, k]) on the catalog's device, ordered by
     (score desc, row asc); rows are GLOBAL row ids; missing entries (fewer than k candidates)
     are NaN / -1. ``exclude`` and ``liked`` take device CSR pairs or host lists of global rows.
+
+    t_floor_hook (row-sharded catalogs): hook(vals f32 [B, k], eps f32 [B]) -> float64 [B], a
+    lower bound of the k-th best EXACT score over the whole catalog. vals are this shard's k
+    best approx scores (-inf padded); every vals[b, j] - eps[b] bounds a distinct row's exact
+    score from below, so the k-th largest of those bounds over all shards (union_floor, after
+    an all-gather) is such a bound. The first pass then screens (ebt_cosine_screen), calls the
+    hook, and rescores only the rows that can enter the GLOBAL top k (ebt_rescore with
+    t_floor); slots that cut empties read NaN / -1, which merge_topk sorts last. The hook runs
+    exactly once per call on every shard (retries below are local, no collective), so shards
+    cannot fall out of step.
     """
     if k < 1:
         raise EbertError("k must be >= 1")
@@ -267,7 +278,11 @@ def score_topk(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
     kp = kprime or default_kprime(catalog, k_eff)
     kp = max(_round_up(k_eff, 4), min(_round_up(kp, 4), n_cap, KPRIME_MAX))
     flags = 0 if fuse else _lib.EBT_FLAG_NO_FUSE
-    s, r, cert = run_pipeline(catalog, qb, k_eff, kp, exclude, chunk_rows, timer, flags=flags)
+    if t_floor_hook is None:
+        s, r, cert = run_pipeline(catalog, qb, k_eff, kp, exclude, chunk_rows, timer, flags=flags)
+    else:
+        s, r, cert = _screen_global_cut(catalog, qb, k_eff, k, kp, exclude, chunk_rows, timer,
+                                        flags, t_floor_hook)
     # retries, only for the queries that need one: a fused candidate list that overflowed
     # (cert -1: rerun unfused) or a candidate set that is not provably complete (cert 0: widen k')
     while True:
@@ -308,6 +323,41 @@ def score_topk(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
     return s, r
 
 
+def union_floor(vals: torch.Tensor, eps: torch.Tensor, k: int) -> torch.Tensor:
+    """The k-th largest of vals[r, b, j] - eps[r, b] over all shards r and slots j: a lower bound
+    of query b's k-th best exact score (vals f32 [R, B, k] approx, eps f32 [R, B])."""
+    R, B, kk = vals.shape
+    lo = vals.double() - eps.double()[:, :, None]
+    lo = torch.nan_to_num(lo, nan=float("-inf")).permute(1, 0, 2).reshape(B, R * kk)
+    return torch.topk(lo, k, dim=1).values[:, k - 1].contiguous()
+
+
+def _screen_global_cut(catalog: Catalog, qb: QueryBatch, k: int, k_req: int, kprime: int,
+                       exclude, chunk_rows, timer, flags, t_floor_hook):
+    """score_topk's first pass under a catalog-wide cut: screen, t_floor_hook, rescore. A shard
+    with fewer rows than the requested k_req pads its bounds with -inf."""
+    dev = catalog.device
+    B = qb.B
+    lv, lr, ovf, eps = run_screen(catalog, qb, k, kprime, exclude, chunk_rows, timer, flags)
+    vals = lv[:, :k]
+    if k < k_req:
+        vals = torch.cat([vals, torch.full((B, k_req - k), float("-inf"), device=dev)], 1)
+    t_floor = t_floor_hook(vals.contiguous(), eps[:B].contiguous()).contiguous()
+    if t_floor.dtype != torch.float64 or t_floor.shape != (B,):
+        raise EbertError("t_floor_hook must return float64 [B]")
+    local = lr - catalog.row_offset if catalog.row_offset else lr
+    out_s = torch.empty((B, k), dtype=torch.float64, device=dev)
+    out_r = torch.empty((B, k), dtype=torch.int64, device=dev)
+    cert = torch.empty(B, dtype=torch.int32, device=dev)
+    call("ebt_rescore", ptr(qb.q64), B, catalog.d, ptr(catalog.data), catalog.dtype_code,
+         catalog.ld, ptr(catalog.gnorm), catalog.row_offset, ptr(lv), ptr(local.contiguous()),
+         kprime, k, catalog.n, ptr(eps), ptr(t_floor), ptr(out_s), ptr(out_r), ptr(cert),
+         stream_of(dev))
+    # an overflowed fused list is rerun unfused (cert -1), unless a row is corrupt (-2)
+    cert = torch.where((ovf != 0) & (cert != -2), torch.full_like(cert, -1), cert)
+    return out_s, out_r, cert
+
+
 def merge_topk(scores: torch.Tensor, rows: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
     """Merge [R, B, k] partial lists (the all-gathered shard results) into the global top-k."""
     require_cuda(scores, "scores")
@@ -338,6 +388,5 @@ def rescore_rows(catalog: Catalog, qb: QueryBatch, cand_rows: torch.Tensor
     cert = torch.empty(B, dtype=torch.int32, device=dev)
     call("ebt_rescore", ptr(qb.q64), B, catalog.d, ptr(catalog.data), catalog.dtype_code,
          catalog.ld, ptr(catalog.gnorm), catalog.row_offset, ptr(vals), ptr(local), m, m, catalog.n,
-         ptr(eps),
-         ptr(out_s), ptr(out_r), ptr(cert), stream_of(dev))
+         ptr(eps), None, ptr(out_s), ptr(out_r), ptr(cert), stream_of(dev))
     return out_s, out_r

@@ -74,6 +74,21 @@ def _body(rank, world, q):
         ok = ok and bool((coll.all_reduce_sum(t) == sum(range(1, world + 1))).all())
         m = torch.tensor([rank, 1 - rank], dtype=torch.int32)
         ok = ok and coll.all_reduce_max(m).tolist() == [world - 1, 1]
+        # the per-shard path's global cut: union_floor of the gathered (approx, eps) lists is a
+        # lower bound of the global k-th exact score, and no shard cuts a global top-k row
+        from robot_ebert_amd.search import union_floor
+        vals = torch.from_numpy(np.nan_to_num(s, nan=-np.inf).astype(np.float32))
+        eps = torch.full((vals.shape[0],), 1e-6, dtype=torch.float32)
+        floor = union_floor(coll.all_gather(vals), coll.all_gather(eps), k).numpy()
+        ok = ok and bool((floor <= s_full[:, k - 1]).all())
+        cut = floor - 1e-6
+        for bq in range(vals.shape[0]):
+            mine = [int(x) for x in r_full[bq] if a <= x < b]
+            kept = set(int(x) for x, v in zip(r[bq], vals[bq].tolist()) if v >= cut[bq])
+            ok = ok and set(mine) <= kept
+        # and it is tight: about k/world + ties of each shard's k rows survive
+        ok = ok and float(np.mean([(vals[bq].numpy() >= cut[bq]).sum()
+                                   for bq in range(vals.shape[0])])) < 0.75 * k
         q.put((rank, ok))
 
 

@@ -39,15 +39,16 @@ class ThreadCollectives:
         return t
 
 
-def _run_sharded(full, world, fn):
-    """fn(rank, catalog_shard, collectives) in `world` threads; returns the per-rank results."""
+def _run_sharded(full, world, fn, cuts=None):
+    """fn(rank, catalog_shard, collectives) in `world` threads; returns the per-rank results.
+    cuts: explicit shard boundaries [0, ..., n] (default: shard_range)."""
     import robot_ebert_amd as ebt
     from robot_ebert_amd.distributed import shard_range
     n = full.shape[0]
     shared = {"world": world, "slots": [None] * world, "barrier": threading.Barrier(world)}
     cats = []
     for r in range(world):
-        a, b = shard_range(n, r, world)
+        a, b = (cuts[r], cuts[r + 1]) if cuts is not None else shard_range(n, r, world)
         cats.append(ebt.Catalog(full[a:b].contiguous(), row_offset=a, n_global=n))
     out, errs = [None] * world, []
 
@@ -120,6 +121,97 @@ def test_two_phase_overflow_and_retry(cuda_device):
     full = _t(c, "f64", cuda_device)
     qt = _t(q, "f64", cuda_device)
     res = _run_sharded(full, 2, lambda r, cat, coll: score_topk_sharded(
+        cat, k, queries=qt, collectives=coll))
+    s_ref, r_ref = R.cosine_topk(q, c, k)
+    for s, r in res:
+        assert_topk_equal(s, r, s_ref, r_ref)
+
+
+def cat_has(row, r, n, world):
+    from robot_ebert_amd.distributed import shard_range
+    a, b = shard_range(n, r, world)
+    return a <= row < b
+
+
+@pytest.mark.parametrize("world,dt", [(4, "f32"), (2, "bf16")])
+def test_per_shard_global_cut_matches_single(cuda_device, world, dt):
+    """score_topk_sharded_local: each shard rescores only rows above the all-reduced floor
+    (t_floor), leaving NaN / -1 slots; the merged answer equals the single-GPU one exactly."""
+    import robot_ebert_amd as ebt
+    from robot_ebert_amd.distributed import score_topk_sharded_local
+    from robot_ebert_amd.search import union_floor
+    from test_gpu_parity import _t, assert_topk_equal
+    n, d, B, k = 160_000, 256, 64, 100
+    c = gaussian(51, n, d, dt)
+    q = gaussian(52, B, d, dt)
+    rng = np.random.default_rng(53)
+    excl = [sorted(rng.choice(n, 200, replace=False).tolist()) for _ in range(B)]
+    full = _t(c, dt, cuda_device)
+    qt = _t(q, dt, cuda_device)
+    partial = {}
+
+    def body(r, cat, coll):
+        out = score_topk_sharded_local(cat, k, queries=qt, exclude=excl, collectives=coll)
+        # the shard's own (cut) list, for the empty-slot checks below
+        partial[r] = ebt.score_topk(cat, k, queries=qt, exclude=excl,
+                                    t_floor_hook=lambda v, e: union_floor(
+                                        coll.all_gather(v), coll.all_gather(e), k))
+        return out
+    res = _run_sharded(full, world, body)
+    single = ebt.score_topk(ebt.Catalog(full), k, queries=qt, exclude=excl)
+    for s, r in res:
+        assert torch.equal(r, single[1])
+        torch.testing.assert_close(s, single[0], rtol=0, atol=0)
+    # the cut removed work: a shard keeps about k/world + (rows in the eps band) of its top k
+    empty = sum(int((partial[r][1] < 0).sum()) for r in range(world))
+    assert empty >= B * k * (world - 1) // 4
+    glob = set(map(tuple, [(b, int(x)) for b in range(B) for x in single[1][b].tolist()]))
+    for r in range(world):
+        ps, pr = partial[r]
+        valid = pr >= 0
+        assert bool(torch.isnan(ps[~valid]).all())
+        # the kept rows are a prefix, and every kept row within the global k-th score's
+        # neighbourhood: a row of the global top k is never cut
+        assert bool((valid[:, 1:] <= valid[:, :-1]).all())
+        kept = set((b, int(x)) for b in range(B) for x in pr[b][valid[b]].tolist())
+        mine = set(p for p in glob if cat_has(p[1], r, n, world))
+        assert mine <= kept
+    sample = [0, 63]
+    s_ref, r_ref = R.cosine_topk(q[sample].astype(np.float64), c.astype(np.float64), k,
+                                 [excl[i] for i in sample])
+    assert_topk_equal(res[0][0][sample], res[0][1][sample], s_ref, r_ref)
+
+
+def test_per_shard_global_cut_uneven_shards(cuda_device):
+    """A shard smaller than k contributes no floor (its list ends in -inf / holds < k rows);
+    liked queries spread over the shards; the merge still equals the oracle."""
+    from robot_ebert_amd.distributed import score_topk_sharded_local
+    from test_gpu_parity import _t, assert_topk_equal
+    n, d, k = 30_000, 64, 40
+    c = gaussian(61, n, d, "f64")
+    liked = [[1, 2, 29_999], [29_990], [5, 6_000, 12_000, 29_995]]
+    rated = [l + [7, 8, 29_980] for l in liked]
+    full = _t(c, "f64", cuda_device)
+    cuts = [0, 14_000, 29_975, n]   # the last shard holds 25 < k rows
+    res = _run_sharded(full, 3, lambda r, cat, coll: score_topk_sharded_local(
+        cat, k, liked=liked, exclude=rated, collectives=coll), cuts=cuts)
+    want_s, want_r = R.liked_topk(c, liked, k, rated)
+    for s, r in res:
+        assert_topk_equal(s, r, want_s, want_r)
+
+
+def test_per_shard_global_cut_overflow_retry(cuda_device):
+    """Overflowed fused lists under the global cut rerun unfused locally (no collective)."""
+    from robot_ebert_amd.distributed import score_topk_sharded_local
+    from test_gpu_parity import _t, assert_topk_equal
+    n, d, k = 300_000, 64, 16
+    rng = np.random.default_rng(9)
+    q = rng.standard_normal((2, d))
+    t = (np.arange(n) / n)[:, None]
+    c = q[0][None, :] * t + rng.standard_normal((n, d)) * (1.0 - t) * 0.5
+    full = _t(c, "f64", cuda_device)
+    qt = _t(q, "f64", cuda_device)
+    res = _run_sharded(full, 2, lambda r, cat, coll: score_topk_sharded_local(
         cat, k, queries=qt, collectives=coll))
     s_ref, r_ref = R.cosine_topk(q, c, k)
     for s, r in res:

@@ -42,11 +42,69 @@ class ThreadCollectives:
         return t
 
 
+def one_rank(args):
+    """Per-rank GPU time of score_topk_sharded_local without thread contention: every shard's
+    floor (approx[k-1] - eps) is computed first, then rank 0 runs alone with the all-reduce
+    replaced by the stored max."""
+    from robot_ebert_amd import _lib, search
+    cfg = bench.CONFIGS["C3"]
+    dev = torch.device("cuda:0")
+    q = bench.make_queries(cfg, dev)
+    k = cfg["k"]
+    for R in args.ranks:
+        floors = []
+        cat0 = None
+        for r in range(R):
+            a, b = shard_range(cfg["n"], r, R)
+            cat = ebt.Catalog(bench.make_catalog_shard(cfg, a, b, dev), row_offset=a,
+                              n_global=cfg["n"])
+            qb = search.prepare_queries(cat, queries=q)
+            kp = search.default_kprime(cat, k)
+            lv, _, _, eps = search.run_screen(cat, qb, k, kp)
+            floors.append((lv[:, :k].clone(), eps[:qb.B].clone()))
+            if r == 0:
+                cat0, lv0, eps0 = cat, lv.double(), eps[:qb.B].double()
+            else:
+                del cat
+            torch.cuda.empty_cache()
+        t_glob = search.union_floor(torch.stack([f[0] for f in floors]),
+                                    torch.stack([f[1] for f in floors]), k)
+        cut0 = lv0[:, k - 1] - 2 * eps0
+        cut1 = torch.maximum(cut0, t_glob - eps0)
+        print(json.dumps({"ranks": R, "kprime": lv0.shape[1],
+                          "eps_mean": float(eps0.mean()),
+                          "kth_minus_first_mean": float((lv0[:, 0] - lv0[:, k - 1]).mean()),
+                          "rescored_nocut": float((lv0 >= cut0[:, None]).sum(1).double().mean()),
+                          "rescored_cut": float((lv0 >= cut1[:, None]).sum(1).double().mean())}),
+              flush=True)
+        for name, hook in (("cut", lambda v, e: t_glob.clone()), ("nocut", None)):
+            for i in range(args.steps + 1):
+                if i == 1:
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                search.score_topk(cat0, k, queries=q, t_floor_hook=hook)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3 / args.steps
+            tm = ebt.Timer()
+            search.score_topk(cat0, k, queries=q, t_floor_hook=hook, timer=tm)
+            torch.cuda.synchronize()
+            print(json.dumps({"ranks": R, "path": "one_rank_" + name, "ms_per_step": round(ms, 3),
+                              "stages_ms": {kk: round(tm.query(kk)[0], 3) for kk in _lib.STAGES}}),
+                  flush=True)
+        del cat0
+        torch.cuda.empty_cache()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ranks", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--one-rank", action="store_true",
+                    help="time rank 0's own work alone (the floor all-reduce replaced by its "
+                         "precomputed result) with and without the global cut")
     args = ap.parse_args()
+    if args.one_rank:
+        return one_rank(args)
     cfg = bench.CONFIGS["C3"]
     dev = torch.device("cuda:0")
     q = bench.make_queries(cfg, dev)
@@ -58,7 +116,10 @@ def main():
             a, b = shard_range(cfg["n"], r, R)
             cats.append(ebt.Catalog(bench.make_catalog_shard(cfg, a, b, dev), row_offset=a,
                                     n_global=cfg["n"]))
-        for name, fn in (("two_phase", score_topk_sharded), ("per_shard", score_topk_sharded_local)):
+        def per_shard_nocut(*a, **kw):
+            return score_topk_sharded_local(*a, t_floor_hook=None, **kw)
+        for name, fn in (("two_phase", score_topk_sharded), ("per_shard", score_topk_sharded_local),
+                         ("per_shard_nocut", per_shard_nocut)):
             shared = {"world": R, "slots": [None] * R, "barrier": threading.Barrier(R)}
 
             def rank_body(r):
