@@ -161,15 +161,19 @@ int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dt
                 const double* t_floor, double* out_scores, int64_t* out_rows, int32_t* certified,
                 void* stream);
 
-/* The fused screen's merge step: query b's list (fv/fi[b*kprime + j], sorted desc as
- * ebt_select_topk leaves it) and the hits ebt_screen_filter left in `n_groups` groups of
- * cand/counts (same slots/ld as that call) -> the kprime best of both, back into fv/fi.
+/* The fused screen's merge step: query b's candidate list (fv/fi[b*kprime + j], a PARTITIONED
+ * list: see below; a sorted list, as ebt_select_topk leaves it, is one) and the hits
+ * ebt_screen_filter left in `n_groups` groups of cand/counts (same slots/ld as that call) -> the
+ * kprime best of both, back into fv/fi, partitioned at k (1 <= k <= kprime):
+ *   [0, k-1) the k-1 best in any order, [k-1] the k-th best, [k, n-1) the rest in any order,
+ *   [n-1] the smallest kept, [n, kprime) empty (-inf / -1), n = min(kprime, entries).
+ * (Lists of k' > 512, merged by the block kernel, come back fully sorted: also partitioned.)
  * Exclusions (GLOBAL rows, CSR sorted per query, or NULL) are dropped from the hits; a group
  * count above `slots`, or more hits than the merge holds, sets ovf[b] = 1. */
-int ebt_merge_hits(float* fv, int64_t* fi, int64_t B, int32_t kprime, const uint64_t* cand,
-                   int64_t ld_cand, int32_t slots, const uint8_t* counts, int64_t ld_counts,
-                   int64_t n_groups, int64_t row_offset, const int64_t* excl_off,
-                   const int64_t* excl_rows, int32_t* ovf, void* stream);
+int ebt_merge_hits(float* fv, int64_t* fi, int64_t B, int32_t kprime, int32_t k,
+                   const uint64_t* cand, int64_t ld_cand, int32_t slots, const uint8_t* counts,
+                   int64_t ld_counts, int64_t n_groups, int64_t row_offset,
+                   const int64_t* excl_off, const int64_t* excl_rows, int32_t* ovf, void* stream);
 
 /* Merge R partial top-k lists (scores/rows [R][B][k], each sorted) into the global top-k per
  * query -- the post-all-gather step of a row-sharded catalog. R*k <= 8192. */
@@ -229,7 +233,8 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
 
 /* ---- two-phase top-k over a row-sharded catalog (robot_ebert_amd/distributed.py) ---------
  * Phase 1, every rank: ebt_cosine_screen = ebt_cosine_topk without the rescore: the shard's k'
- * best approx candidates, list_vals (f32) / list_rows (GLOBAL, -1 empty) [B][kprime] sorted,
+ * best approx candidates, list_vals (f32) / list_rows (GLOBAL, -1 empty) [B][kprime]
+ * partitioned at k as ebt_merge_hits describes (sorted when the unfused path ran),
  * ovf_out[b] = 1 when the fused screen overflowed for b, eps_out = the eps the certificate
  * must use. The ranks all-gather the lists and keep the k' best of all shards
  * (ebt_select_topk over [B][R*kprime] with the rows as indices).

@@ -54,7 +54,7 @@ _SIGNATURES = {
                            _I32, _VP, _VP, _VP], _INT),
     "ebt_finalize_topk": ([_VP, _VP, _VP, _I64, _I32, _I32, _I64, _VP, _VP, _VP, _VP, _VP, _VP],
                           _INT),
-    "ebt_merge_hits": ([_VP, _VP, _I64, _I32, _VP, _I64, _I32, _VP, _I64, _I64, _I64, _VP, _VP, _VP,
+    "ebt_merge_hits": ([_VP, _VP, _I64, _I32, _I32, _VP, _I64, _I32, _VP, _I64, _I64, _I64, _VP, _VP, _VP,
                         _VP], _INT),
     "ebt_mask_excluded": ([_VP, _I64, _I64, _I64, _I64, _VP, _VP, _VP], _INT),
     "ebt_select_topk": ([_VP, _VP, _I64, _I64, _I64, _I64, _I32, _I32, _VP, _VP, _I64, _VP],

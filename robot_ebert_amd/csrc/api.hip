@@ -59,10 +59,11 @@ int merge_segment(float*, int64_t*, int64_t, int, const uint64_t*, int64_t, int,
 bool merge_wave_fits(int);
 int merge_wave_capacity();
 int64_t merge_wave_max_groups();
-int merge_segment_wave(float*, int64_t*, int64_t, int, const uint64_t*, int64_t, int,
+int merge_segment_wave(float*, int64_t*, int64_t, int, int, const uint64_t*, int64_t, int,
                        const uint8_t*, int64_t, int64_t, int64_t, const int64_t*, const int64_t*,
                        int*, hipStream_t);
-int pilot_topk(const float*, int64_t, int64_t, int, int64_t, int, float*, int64_t*, hipStream_t);
+int pilot_topk(const float*, int64_t, int64_t, int, int64_t, int, int, float*, int64_t*,
+               hipStream_t);
 constexpr int64_t PILOT_ROWS = 1024;  // = WMERGE_H (select_topk.hip)
 int merge_topk(const double*, const int64_t*, int32_t, int64_t, int32_t, double*, int64_t*,
                hipStream_t);
@@ -377,7 +378,8 @@ int ebt_screen_exact(const double* q64, int64_t B, int32_t d, const void* cat, i
                       (hipStream_t)stream);
 }
 
-int ebt_merge_hits(float* fv, int64_t* fi, int64_t B, int32_t kprime, const uint64_t* cand,
+int ebt_merge_hits(float* fv, int64_t* fi, int64_t B, int32_t kprime, int32_t k,
+                   const uint64_t* cand,
                    int64_t ld_cand, int32_t slots, const uint8_t* counts, int64_t ld_counts,
                    int64_t n_groups, int64_t row_offset, const int64_t* excl_off,
                    const int64_t* excl_rows, int32_t* ovf, void* stream) {
@@ -385,9 +387,13 @@ int ebt_merge_hits(float* fv, int64_t* fi, int64_t B, int32_t kprime, const uint
     set_error("ebt_merge_hits: null pointer");
     return EBT_EINVAL;
   }
+  if (k < 1 || k > kprime) {
+    set_error("ebt_merge_hits: k=%d outside [1, kprime=%d]", k, kprime);
+    return EBT_EINVAL;
+  }
   hipStream_t st = (hipStream_t)stream;
   if (merge_wave_fits(kprime) && n_groups <= merge_wave_max_groups() && ld_counts % 16 == 0)
-    return merge_segment_wave(fv, fi, B, kprime, cand, ld_cand, slots, counts, ld_counts,
+    return merge_segment_wave(fv, fi, B, kprime, k, cand, ld_cand, slots, counts, ld_counts,
                               n_groups, row_offset, excl_off, excl_rows, ovf, st);
   return merge_segment(fv, fi, B, kprime, cand, ld_cand, slots, counts, ld_counts, n_groups,
                        row_offset, excl_off, excl_rows, ovf, st);
@@ -522,7 +528,7 @@ static int run_screen(const PipeArgs& a, const WsLayout& L, char* ws, float* fv,
       if (rc) return rc;
     }
     StageScope s(timer, EBT_STAGE_SELECT, st);
-    rc = pilot_topk(S, L.ld_s, B, (int)L.head, 0, kprime, fv, fi, st);
+    rc = pilot_topk(S, L.ld_s, B, (int)L.head, 0, kprime, k, fv, fi, st);
   } else {
     rc = head_topk(L, ws, a.qimg, a.qscale, B, B_pad, a.cimg, a.cscale, a.img_dtype, ld_img, 0,
                    L.head, d_pad, row_offset, a.excl_off, a.excl_rows, kprime, fv, fi, kprime,
@@ -567,7 +573,7 @@ static int run_screen(const PipeArgs& a, const WsLayout& L, char* ws, float* fv,
     if (rc) return rc;
     {
       StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
-      rc = L.pilot ? merge_segment_wave(fv, fi, B, kprime, cand, L.ld_cand, slots, counts,
+      rc = L.pilot ? merge_segment_wave(fv, fi, B, kprime, k, cand, L.ld_cand, slots, counts,
                                         L.ld_counts, groups, row_offset, a.excl_off, a.excl_rows,
                                         ovf, st)
                    : merge_segment(fv, fi, B, kprime, cand, L.ld_cand, slots, counts,

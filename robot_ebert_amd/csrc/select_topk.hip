@@ -513,127 +513,145 @@ int merge_segment(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t*
 
 // ---------------------------------------------------------------------------------------------
 // The same merge with ONE WAVE per query (4 queries per workgroup, no block barriers) while
-// k' + hits <= WTOP_N: the wave holds the union in registers (WTOP_E composites per lane),
-// finds the k'-th largest by a binary search on the 32-bit key (a second one on the row part
-// when the k'-th key is tied), compacts the k' winners into LDS with ballots and writes each to
-// its rank = the number of winners above it (a broadcast scan of the k' winners). No sort
-// network: ~1.5k VALU + k' LDS broadcast reads per lane. Input either the per-group hit slots
-// of the filter GEMM plus the list fv/fi, or (the fused screen's pilot) a dense score row with
-// implicit rows idx_base + j and no list.
+// k' + hits <= WTOP_N: the wave holds the union in registers (WTOP_E composites per lane) and
+// selects with binary searches on the 32-bit key (a second one on the row part only when the
+// key at the cut is tied), counting with ballot popcounts -- uniform (scalar) loops, 32-bit
+// compares. The result is written PARTITIONED, not sorted (nothing downstream needs more):
+//   [0, k-1) the k-1 best (any order), [k-1] the k-th best,
+//   [k, n-1) the rest (any order),     [n-1] the smallest kept,   [n, k') empty (-inf / -1)
+// with n = min(k', valid entries). Every consumer reads the list as a set plus those two
+// positions: kth_threshold (the k-th), rescore (the k-th and the k'-th), the next merge (the
+// k'-th). The block merge and the streaming select write fully sorted lists, a special case.
+// Input either the per-group hit slots of the filter GEMM plus the list fv/fi, or (the fused
+// screen's pilot) a dense score row with implicit rows idx_base + j and no list.
 // ---------------------------------------------------------------------------------------------
 constexpr int WTOP_E = 16;            // composites per lane
 constexpr int WTOP_N = 64 * WTOP_E;   // union size per query
-constexpr int WMERGE_K = 512;         // largest k' (winners staged in LDS)
+constexpr int WMERGE_K = 512;         // largest k'
 constexpr int WMERGE_Q = STHREADS / 64;
 constexpr int WCNT = 4;               // 16-byte count loads per lane: n_groups <= 64 * 64
 
-// The k' largest of the wave's composites x (0 = empty), written in descending order to
-// ov/oi[0..kprime) (empty tail: -inf / -1). win: kprime u64 of LDS for this wave.
-template <int R>
-__device__ void wave_topk_write(const uint64_t (&x)[WTOP_E], int kprime, float* ov, int64_t* oi,
-                                uint64_t* win, int lane, uint32_t key_lo) {
-  int nvalid = 0;
+__device__ __forceinline__ int wave_count_ge(const uint32_t (&kx)[WTOP_E], uint32_t t) {
+  int c = 0;
 #pragma unroll
-  for (int j = 0; j < WTOP_E; ++j) nvalid += __popcll(__ballot(x[j] != 0ull));
-  const int want = nvalid < kprime ? nvalid : kprime;
-  // selected: composite >= (t << 32 | u); t = the want-th largest key, u = the row part cut
-  uint32_t t = 0u, u = 0u;
-  if (want > 0) {
-    // t = largest key with count(key >= t) >= want, searched in [key_lo, max key]: key_lo is a
-    // known lower bound (the list's k'-th key), which leaves ~20 steps for float keys
-    uint32_t kmax = 0u;
-#pragma unroll
-    for (int j = 0; j < WTOP_E; ++j) kmax = max(kmax, (uint32_t)(x[j] >> 32));
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
-    uint64_t lo = key_lo > 1u ? key_lo : 1u, hi = kmax;
-    if (lo > hi) lo = hi;
-    while (lo < hi) {
-      const uint64_t mid = lo + ((hi - lo + 1) >> 1);
-      int c = 0;  // ballot counts: scalar popcounts, no cross-lane data movement
-#pragma unroll
-      for (int j = 0; j < WTOP_E; ++j) c += __popcll(__ballot((x[j] >> 32) >= mid));
-      if (c >= want) lo = mid;
-      else hi = mid - 1;
-    }
-    t = (uint32_t)lo;
-    int gt = 0, eq = 0;
-#pragma unroll
-    for (int j = 0; j < WTOP_E; ++j) {
-      gt += __popcll(__ballot((uint32_t)(x[j] >> 32) > t));
-      eq += __popcll(__ballot((uint32_t)(x[j] >> 32) == t));
-    }
-    const int need = want - gt;  // 1 <= need <= eq entries with key == t
-    if (need < eq) {  // a tie at the cut: order the tied entries by row (rare)
-      uint64_t lo2 = 0, hi2 = 0xffffffffull;  // largest u with count(key == t, low >= u) >= need
-      while (lo2 < hi2) {
-        const uint64_t mid = lo2 + ((hi2 - lo2 + 1) >> 1);
-        int c = 0;
-#pragma unroll
-        for (int j = 0; j < WTOP_E; ++j)
-          c += __popcll(
-              __ballot(((uint32_t)(x[j] >> 32) == t) && ((x[j] & 0xffffffffull) >= mid)));
-        if (c >= need) lo2 = mid;
-        else hi2 = mid - 1;
-      }
-      u = (uint32_t)lo2;
-    }
+  for (int j = 0; j < WTOP_E; ++j) c += __popcll(__ballot(kx[j] >= t));
+  return c;
+}
+
+// The cut c (a composite) with exactly `want` entries of x >= c (1 <= want <= valid entries;
+// composites are unique). lo: a key with count(key >= lo) >= want; hi: the largest key.
+__device__ __forceinline__ uint64_t wave_cut(const uint64_t (&x)[WTOP_E],
+                                             const uint32_t (&kx)[WTOP_E], int want, uint32_t lo,
+                                             uint32_t hi) {
+  uint64_t l = __builtin_amdgcn_readfirstlane(lo), h = __builtin_amdgcn_readfirstlane(hi);
+  if (l > h) l = h;
+  while (l < h) {  // largest t with count(key >= t) >= want
+    const uint64_t mid = l + ((h - l + 1) >> 1);
+    if (wave_count_ge(kx, (uint32_t)mid) >= want) l = mid;
+    else h = mid - 1;
   }
-  const uint64_t cut = ((uint64_t)t << 32) | u;
-  int base = 0;
-  const uint64_t below = (1ull << lane) - 1ull;
+  const uint32_t t = (uint32_t)l;
+  int gt = 0, eq = 0;
 #pragma unroll
   for (int j = 0; j < WTOP_E; ++j) {
-    const bool sel = want > 0 && x[j] != 0ull && x[j] >= cut;
-    const uint64_t m = __ballot(sel);
-    if (sel) win[base + __popcll(m & below)] = x[j];
-    base += __popcll(m);
+    gt += __popcll(__ballot(kx[j] > t));
+    eq += __popcll(__ballot(kx[j] == t));
   }
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  const int nsel = base < want ? base : want;  // == want (composites are unique)
-  // rank of each winner = winners above it: every lane scans all winners (LDS broadcast reads,
-  // 8 per batch so the reads pipeline) against its own R (R * 64 >= k')
-  uint64_t mine[R];
-  int rank[R];
+  const int need = want - gt;  // 1 <= need <= eq entries with key == t
+  uint64_t u = 0;
+  if (need < eq) {  // a tie at the cut: order the tied entries by row (rare)
+    uint64_t l2 = 0, h2 = 0xffffffffull;  // largest u with count(key == t, low >= u) >= need
+    while (l2 < h2) {
+      const uint64_t mid = l2 + ((h2 - l2 + 1) >> 1);
+      int c = 0;
 #pragma unroll
-  for (int t2 = 0; t2 < R; ++t2) {
-    const int i = lane + 64 * t2;
-    mine[t2] = i < nsel ? win[i] : 0ull;
-    rank[t2] = 0;
+      for (int j = 0; j < WTOP_E; ++j)
+        c += __popcll(__ballot(kx[j] == t && (uint32_t)x[j] >= (uint32_t)mid));
+      if (c >= need) l2 = mid;
+      else h2 = mid - 1;
+    }
+    u = l2;
   }
-  for (int q = 0; q < nsel; q += 8) {
-    uint64_t w8[8];
+  return ((uint64_t)t << 32) | u;
+}
+
+// smallest nonzero composite >= cut over the wave (uniform result)
+__device__ __forceinline__ uint64_t wave_min_at_least(const uint64_t (&x)[WTOP_E], uint64_t cut) {
+  uint64_t m = ~0ull;
 #pragma unroll
-    for (int u8 = 0; u8 < 8; ++u8) w8[u8] = q + u8 < nsel ? win[q + u8] : 0ull;
+  for (int j = 0; j < WTOP_E; ++j) m = (x[j] != 0ull && x[j] >= cut && x[j] < m) ? x[j] : m;
 #pragma unroll
-    for (int u8 = 0; u8 < 8; ++u8)
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t v = ((uint64_t)(uint32_t)__shfl_xor((int)(m >> 32), o, 64) << 32) |
+                       (uint32_t)__shfl_xor((int)(uint32_t)m, o, 64);
+    m = v < m ? v : m;
+  }
+  return m;
+}
+
+// The k' largest of the wave's composites x (0 = empty), written partitioned at k (see above)
+// to ov/oi[0..kprime).
+__device__ void wave_topk_write(const uint64_t (&x)[WTOP_E], int kprime, int k, float* ov,
+                                int64_t* oi, int lane, uint32_t key_lo) {
+  uint32_t kx[WTOP_E];
+  int nvalid = 0;
+  uint32_t kmax = 0u;
 #pragma unroll
-      for (int t2 = 0; t2 < R; ++t2) rank[t2] += w8[u8] > mine[t2];
+  for (int j = 0; j < WTOP_E; ++j) {
+    kx[j] = (uint32_t)(x[j] >> 32);
+    nvalid += __popcll(__ballot(x[j] != 0ull));
+    kmax = max(kmax, kx[j]);
   }
 #pragma unroll
-  for (int t2 = 0; t2 < R; ++t2) {
-    const int i = lane + 64 * t2;
-    if (i < nsel) {
-      ov[rank[t2]] = key2f((uint32_t)(mine[t2] >> 32));
-      oi[rank[t2]] = (int64_t)(~(uint32_t)mine[t2]);
+  for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+  const int want = nvalid < kprime ? nvalid : kprime;
+  const uint64_t below = (1ull << lane) - 1ull;
+  if (want > 0) {
+    // the kept set S = {x >= cw_cut} (want entries), its smallest cw; the top kk = min(k, want)
+    // A = {x >= ck_cut}, its smallest ck (the kk-th best)
+    const uint64_t cw_cut = wave_cut(x, kx, want, key_lo > 1u ? key_lo : 1u, kmax);
+    const uint64_t cw = wave_min_at_least(x, cw_cut);
+    const int kk = k < want ? k : want;
+    uint64_t ck = cw;
+    if (kk < want) {
+      const uint64_t ck_cut = wave_cut(x, kx, kk, (uint32_t)(cw_cut >> 32), kmax);
+      ck = wave_min_at_least(x, ck_cut);
+    }
+    int na = 0, nb = kk;
+#pragma unroll
+    for (int j = 0; j < WTOP_E; ++j) {
+      const uint64_t v = x[j];
+      const bool inA = v > ck;                                  // the kk-1 best
+      const bool inB = v != 0ull && v >= cw && v < ck && v != cw;  // between
+      const uint64_t ma = __ballot(inA), mb = __ballot(inB);
+      int pos = -1;
+      if (inA) pos = na + __popcll(ma & below);
+      else if (inB) pos = nb + __popcll(mb & below);
+      else if (v == ck && v != 0ull) pos = kk - 1;
+      else if (v == cw && v != 0ull) pos = want - 1;
+      if (pos >= 0) {
+        ov[pos] = key2f((uint32_t)(v >> 32));
+        oi[pos] = (int64_t)(~(uint32_t)v);
+      }
+      na += __popcll(ma);
+      nb += __popcll(mb);
     }
   }
-  for (int i = nsel + lane; i < kprime; i += 64) {
+  for (int i = want + lane; i < kprime; i += 64) {
     ov[i] = -__builtin_inff();
     oi[i] = -1;
   }
 }
 
-template <bool DENSE, int R>
-__global__ __launch_bounds__(STHREADS) void merge_wave_kernel(
-    float* __restrict__ fv, int64_t* __restrict__ fi, int64_t B, int kprime,
+template <bool DENSE>
+__global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
+    float* __restrict__ fv, int64_t* __restrict__ fi, int64_t B, int kprime, int k,
     const uint64_t* __restrict__ cand, int64_t ld_cand, int slots,
     const uint8_t* __restrict__ counts, int64_t ld_counts, int n_groups,
     const float* __restrict__ dense, int64_t ld_dense, int n_dense, int64_t idx_base,
     int64_t row_offset, const int64_t* __restrict__ eo, const int64_t* __restrict__ er,
     int* __restrict__ ovf) {
-  __shared__ uint64_t stage[WMERGE_Q][WTOP_N];  // the union, then the winners
+  __shared__ uint64_t stage[WMERGE_Q][WTOP_N];  // the union
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t b = (int64_t)blockIdx.x * WMERGE_Q + w;
   if (b >= B) return;
@@ -674,11 +692,12 @@ __global__ __launch_bounds__(STHREADS) void merge_wave_kernel(
     const uint64_t* cb = cand + b * ld_cand;
     const int per = ((n_groups + 63) / 64 + 15) & ~15;
     const int g0 = lane * per;
+    const int nv = per / 16;  // count vectors in use (uniform)
     uint4 cv4[WCNT];
 #pragma unroll
     for (int v = 0; v < WCNT; ++v) {
       const int g = g0 + 16 * v;
-      cv4[v] = (16 * v < per && g < n_groups) ? *(const uint4*)(cr + g) : make_uint4(0, 0, 0, 0);
+      cv4[v] = (v < nv && g < n_groups) ? *(const uint4*)(cr + g) : make_uint4(0, 0, 0, 0);
     }
     auto cnt_at = [&](int v, int e) -> int {  // count of group g0 + 16 v + e (0 past the end)
       const uint32_t w4 = e < 4 ? cv4[v].x : e < 8 ? cv4[v].y : e < 12 ? cv4[v].z : cv4[v].w;
@@ -687,13 +706,15 @@ __global__ __launch_bounds__(STHREADS) void merge_wave_kernel(
     };
     int mine = 0;
 #pragma unroll
-    for (int v = 0; v < WCNT; ++v)
+    for (int v = 0; v < WCNT; ++v) {
+      if (v >= nv) break;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int c = cnt_at(v, e);
         over |= c > slots;
         mine += c < slots ? c : slots;
       }
+    }
     int incl = mine;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -707,7 +728,8 @@ __global__ __launch_bounds__(STHREADS) void merge_wave_kernel(
     int pos = kprime + incl - mine;
     if (mine > 0) {
 #pragma unroll
-      for (int v = 0; v < WCNT; ++v)
+      for (int v = 0; v < WCNT; ++v) {
+        if (v >= nv) break;
 #pragma unroll 1
         for (int e = 0; e < 16; ++e) {
           int c = cnt_at(v, e);
@@ -716,6 +738,7 @@ __global__ __launch_bounds__(STHREADS) void merge_wave_kernel(
           for (int p = 0; p < c; ++p, ++pos)
             if (pos < WTOP_N) U[pos] = (uint64_t)(g * slots + p);
         }
+      }
     }
     const int mh = kprime + m < WTOP_N ? m : WTOP_N - kprime;
     __builtin_amdgcn_wave_barrier();
@@ -744,7 +767,7 @@ __global__ __launch_bounds__(STHREADS) void merge_wave_kernel(
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
-  wave_topk_write<R>(x, kprime, fv + b * kprime, fi + b * kprime, U, lane, key_lo);
+  wave_topk_write(x, kprime, k, fv + b * kprime, fi + b * kprime, lane, key_lo);
   if (__ballot(over) != 0ull && lane == 0) ovf[b] = 1;
 }
 
@@ -752,20 +775,20 @@ bool merge_wave_fits(int kprime) { return kprime <= WMERGE_K; }
 int64_t merge_wave_max_groups() { return 64 * 16 * WCNT; }
 int merge_wave_capacity() { return WTOP_N; }
 
-int merge_segment_wave(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t* cand,
+int merge_segment_wave(float* fv, int64_t* fi, int64_t B, int kprime, int k, const uint64_t* cand,
                        int64_t ld_cand, int slots, const uint8_t* counts, int64_t ld_counts,
                        int64_t n_groups, int64_t row_offset, const int64_t* eo,
                        const int64_t* er, int* ovf, hipStream_t st) {
-  if (B < 0 || kprime < 1 || kprime > WMERGE_K || n_groups < 1 || n_groups > 64 * 16 * WCNT ||
+  if (B < 0 || kprime < 1 || kprime > WMERGE_K || k < 1 || k > kprime || n_groups < 1 ||
+      n_groups > 64 * 16 * WCNT ||
       ld_counts < n_groups || ld_counts % 16 != 0 || ((uintptr_t)counts & 15) ||
       ld_cand < n_groups * slots) {
     set_error("merge_segment_wave: bad arguments");
     return EBT_EINVAL;
   }
   if (B == 0) return EBT_OK;
-  auto kern = kprime <= 256 ? merge_wave_kernel<false, 4> : merge_wave_kernel<false, 8>;
-  hipLaunchKernelGGL(kern, dim3((unsigned)ceil_div(B, WMERGE_Q)), dim3(STHREADS), 0, st, fv, fi,
-                     B, kprime, cand, ld_cand, slots, counts, ld_counts, (int)n_groups, nullptr,
+  hipLaunchKernelGGL(merge_wave_kernel<false>, dim3((unsigned)ceil_div(B, WMERGE_Q)),
+                     dim3(STHREADS), 0, st, fv, fi, B, kprime, k, cand, ld_cand, slots, counts, ld_counts, (int)n_groups, nullptr,
                      0, 0, 0, row_offset, eo, er, ovf);
   return launch_check("merge_wave_kernel");
 }
@@ -773,15 +796,15 @@ int merge_segment_wave(float* fv, int64_t* fi, int64_t B, int kprime, const uint
 // Top-k' of a dense score block (n <= WTOP_N columns per row; masked entries -inf): the fused
 // screen's pilot rows, straight into the list fv/fi.
 int pilot_topk(const float* S, int64_t ld_s, int64_t B, int n, int64_t idx_base, int kprime,
-               float* fv, int64_t* fi, hipStream_t st) {
-  if (B < 0 || n < 1 || n > WTOP_N || kprime < 1 || kprime > WMERGE_K || ld_s < n) {
+               int k, float* fv, int64_t* fi, hipStream_t st) {
+  if (B < 0 || n < 1 || n > WTOP_N || kprime < 1 || kprime > WMERGE_K || k < 1 || k > kprime ||
+      ld_s < n) {
     set_error("pilot_topk: bad arguments");
     return EBT_EINVAL;
   }
   if (B == 0) return EBT_OK;
-  auto kern = kprime <= 256 ? merge_wave_kernel<true, 4> : merge_wave_kernel<true, 8>;
-  hipLaunchKernelGGL(kern, dim3((unsigned)ceil_div(B, WMERGE_Q)), dim3(STHREADS), 0, st, fv, fi,
-                     B, kprime, nullptr, 0, 1, nullptr, 0, 0, S, ld_s, n, idx_base, 0, nullptr,
+  hipLaunchKernelGGL(merge_wave_kernel<true>, dim3((unsigned)ceil_div(B, WMERGE_Q)),
+                     dim3(STHREADS), 0, st, fv, fi, B, kprime, k, nullptr, 0, 1, nullptr, 0, 0, S, ld_s, n, idx_base, 0, nullptr,
                      nullptr, nullptr);
   return launch_check("merge_wave_kernel");
 }

@@ -198,13 +198,31 @@ def _key_val(k):
     return float(np.array([u], dtype=np.uint32).view(np.float32)[0])
 
 
-@pytest.mark.parametrize("kp,hits,groups", [(40, 30, 7), (200, 500, 300), (200, 0, 10),
-                                            (600, 300, 50)])
-def test_merge_hits_vs_numpy(cuda_device, kp, hits, groups):
-    """ebt_merge_hits: the k' best of (sorted list + slot hits), exclusions dropped, in
-    (value desc, row asc) order -- ties included -- against numpy on the same composites."""
+def check_partitioned(gv, gi, ref_v, ref_r, k, kp):
+    """A list partitioned at k (include/ebert.h, ebt_merge_hits) against the sorted reference
+    (ref_v, ref_r) = the n <= kp best in (value desc, row asc) order."""
+    n = len(ref_r)
+    assert np.all(gi[n:] == -1) and np.all(np.isneginf(gv[n:]))
+    assert sorted(gi[:n].tolist()) == sorted(ref_r.tolist())
+    val_of = dict(zip(ref_r.tolist(), ref_v.tolist()))
+    np.testing.assert_array_equal(gv[:n], np.array([val_of[r] for r in gi[:n].tolist()],
+                                                   np.float32))
+    if n == 0:
+        return
+    kk = min(k, n)
+    assert sorted(gi[:kk].tolist()) == sorted(ref_r[:kk].tolist())
+    assert gi[kk - 1] == ref_r[kk - 1]
+    assert gi[n - 1] == ref_r[n - 1]
+
+
+@pytest.mark.parametrize("kp,k,hits,groups,shuffle", [
+    (40, 20, 30, 7, False), (200, 100, 500, 300, True), (200, 1, 0, 10, False),
+    (200, 200, 500, 300, False), (600, 100, 300, 50, True), (40, 40, 30, 7, True)])
+def test_merge_hits_vs_numpy(cuda_device, kp, k, hits, groups, shuffle):
+    """ebt_merge_hits: the k' best of (partitioned list + slot hits), exclusions dropped,
+    partitioned at k -- ties included -- against numpy on the same composites."""
     ebt, L = _ebt()
-    rng = np.random.default_rng(kp + hits)
+    rng = np.random.default_rng(kp + hits + k)
     B, slots = 9, 16
     vals = np.round(rng.standard_normal((B, kp)) * 8) / 8          # ties
     lv = -np.sort(-vals, axis=1).astype(np.float32)
@@ -214,6 +232,10 @@ def test_merge_hits_vs_numpy(cuda_device, kp, hits, groups):
     for b in range(B):                                               # (value desc, row asc)
         o = np.lexsort((np.where(lr[b] < 0, 1 << 40, lr[b]), -lv[b]))
         lv[b], lr[b] = lv[b][o], lr[b][o]
+        if shuffle:  # a partitioned input: only the last entry (the k'-th) stays in place
+            nv = int((lr[b] >= 0).sum())
+            p = np.concatenate([rng.permutation(nv - 1), np.arange(nv - 1, kp)])
+            lv[b], lr[b] = lv[b][p], lr[b][p]
     counts = np.zeros((B, (groups + 15) // 16 * 16), np.uint8)
     cand = np.zeros((B, groups * slots), np.uint64)
     hit_v, hit_r = [[] for _ in range(B)], [[] for _ in range(B)]
@@ -223,7 +245,7 @@ def test_merge_hits_vs_numpy(cuda_device, kp, hits, groups):
             if counts[b, gi] >= slots:
                 continue
             v = np.float32(np.round(rng.standard_normal() * 8) / 8)
-            r = gi * 1000 + counts[b, gi]
+            r = 1_000_000 + gi * 1000 + counts[b, gi]   # disjoint from the list's rows
             cand[b, gi * slots + counts[b, gi]] = _composite(np.array([v]), np.array([r]))[0]
             counts[b, gi] += 1
             hit_v[b].append(v)
@@ -238,7 +260,7 @@ def test_merge_hits_vs_numpy(cuda_device, kp, hits, groups):
     ct = torch.from_numpy(counts).to(dev)
     cd = torch.from_numpy(cand.view(np.int64)).to(dev)
     eot, ert = torch.from_numpy(eo).to(dev), torch.from_numpy(er).to(dev)
-    L.call("ebt_merge_hits", L.ptr(fv), L.ptr(fi), B, kp, L.ptr(cd), groups * slots, slots,
+    L.call("ebt_merge_hits", L.ptr(fv), L.ptr(fi), B, kp, k, L.ptr(cd), groups * slots, slots,
            L.ptr(ct), counts.shape[1], groups, 0, L.ptr(eot), L.ptr(ert), L.ptr(ovf),
            L.stream_of(dev))
     gv, gi_ = fv.cpu().numpy(), fi.cpu().numpy()
@@ -251,10 +273,13 @@ def test_merge_hits_vs_numpy(cuda_device, kp, hits, groups):
         allv = np.concatenate([lv[b][keep], np.array(hv, np.float32)])
         allr = np.concatenate([lr[b][keep], np.array(hr, np.int64)])
         o = np.lexsort((allr, -allv))[:kp]
-        m = len(o)
-        np.testing.assert_array_equal(gi_[b, :m], allr[o])
-        np.testing.assert_array_equal(gv[b, :m], allv[o])
-        assert np.all(gi_[b, m:] == -1)
+        if kp > 512:  # the block merge: fully sorted
+            m = len(o)
+            np.testing.assert_array_equal(gi_[b, :m], allr[o])
+            np.testing.assert_array_equal(gv[b, :m], allv[o])
+            assert np.all(gi_[b, m:] == -1)
+        else:
+            check_partitioned(gv[b], gi_[b], allv[o], allr[o], k, kp)
 
 
 def _select_ref(v, k):

@@ -100,7 +100,7 @@ def bench_merge(dev, B, kp, groups, hits, slots=16):
     def run():
         fv.copy_(fv0)
         fi.copy_(fi0)
-        L.call("ebt_merge_hits", L.ptr(fv), L.ptr(fi), B, kp, L.ptr(cand), groups * slots, slots,
+        L.call("ebt_merge_hits", L.ptr(fv), L.ptr(fi), B, kp, min(100, kp), L.ptr(cand), groups * slots, slots,
                L.ptr(counts), counts.shape[1], groups, 0, None, None, L.ptr(ovf), st)
     ms = timeit(run)
     ms_copy = timeit(lambda: (fv.copy_(fv0), fi.copy_(fi0)))
@@ -113,6 +113,7 @@ def main():
     ap.add_argument("--gemm", action="store_true")
     ap.add_argument("--select", action="store_true")
     ap.add_argument("--merge", action="store_true")
+    ap.add_argument("--merge-shape", default=None, help="B,kprime,groups,hits for --merge")
     ap.add_argument("--one", action="store_true", help="single C3-chunk GEMM config (profiling)")
     ap.add_argument("--shape", default="4096,262144,1536", help="B,N,d for --one")
     ap.add_argument("--select-shapes", default=None,
@@ -122,9 +123,11 @@ def main():
     L.load()
     res = []
     if args.merge:
-        for (B, kp, groups, hits) in [(4096, 200, 2048, 400), (4096, 200, 48, 400),
-                                      (4096, 200, 2048, 50), (4096, 200, 2048, 800),
-                                      (4096, 1016, 2048, 1000)]:
+        cfgs = [(4096, 200, 2048, 400), (4096, 200, 48, 400), (4096, 200, 2048, 50),
+                (4096, 200, 2048, 800), (4096, 1016, 2048, 1000)]
+        if args.merge_shape:
+            cfgs = [tuple(int(x) for x in args.merge_shape.split(","))]
+        for (B, kp, groups, hits) in cfgs:
             print(json.dumps(bench_merge(dev, B, kp, groups, hits)), flush=True)
         return
     if args.one:

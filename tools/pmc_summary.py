@@ -1,21 +1,22 @@
 """Summarise a tools/prof_gemm.sh run: per-dispatch averages of every counter over the screening
 GEMM dispatches, plus derived clock / MFMA utilisation / HBM bytes (FETCH_SIZE x 2 KiB-unit
-correction of the MI355X guide). Usage: python tools/pmc_summary.py gpurun_out/pmc_NAME"""
+correction of the MI355X guide). Usage: python tools/pmc_summary.py gpurun_out/pmc_NAME [REGEX]"""
 import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
 
-def main(d):
+def main(d, rx="screen_gemm"):
     acc = defaultdict(list)
     kname = None
     for f in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
         per = defaultdict(lambda: defaultdict(float))
         for r in csv.DictReader(open(f)):
-            if "screen_gemm" not in r["Kernel_Name"]:
+            if not re.search(rx, r["Kernel_Name"]):
                 continue
             kname = r["Kernel_Name"]
             per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
@@ -26,7 +27,7 @@ def main(d):
     dur = None
     for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "screen_gemm" in r["Name"]:
+            if re.search(rx, r["Name"]):
                 dur = float(r["AverageNs"])
     out["kernel"] = kname
     out["avg_ns"] = dur
@@ -45,4 +46,4 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], *(sys.argv[2:3]))
