@@ -93,64 +93,73 @@ struct EpiArgs {
   int slots;
 };
 
+// The row scales of catalog rows i0 .. i0+3 (1 past the end / without scales).
+__device__ __forceinline__ float4 row_scales4(const float* __restrict__ cscale, int64_t i0,
+                                              int64_t n_rows) {
+  float4 cs = make_float4(1.f, 1.f, 1.f, 1.f);
+  if (cscale) {
+    if (i0 + 3 < n_rows) {
+      cs = *(const float4*)(cscale + i0);
+    } else {
+      cs.x = i0 + 0 < n_rows ? cscale[i0 + 0] : 1.f;
+      cs.y = i0 + 1 < n_rows ? cscale[i0 + 1] : 1.f;
+      cs.z = i0 + 2 < n_rows ? cscale[i0 + 2] : 1.f;
+      cs.w = i0 + 3 < n_rows ? cscale[i0 + 3] : 1.f;
+    }
+  }
+  return cs;
+}
+
+// The filter's cold path: append the values >= th of rows i0 .. i0+3 (row < n_rows) to the
+// (query, group) slots.
+__device__ __forceinline__ void filter_hits(const EpiArgs& e, int64_t q, int64_t i0,
+                                            int64_t n_rows, const float (&v)[4], float th,
+                                            uint32_t* lcnt, int64_t grp) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t i = i0 + r;
+    if (i < n_rows && v[r] >= th) {
+      const uint32_t p = atomicAdd(lcnt, 1u);
+      if (p < (uint32_t)e.slots) {
+        const uint32_t row = (uint32_t)(e.idx_base + i);
+        e.cand[q * e.ld_cand + grp * e.slots + p] =
+            ((uint64_t)f2key(v[r]) << 32) | (uint64_t)(~row);
+      }
+    }
+  }
+}
+
+// One accumulator (4 consecutive catalog rows i0.. of query q) with its scales in hand.
+template <bool FILTER>
+__device__ __forceinline__ void epilogue4v(const EpiArgs& e, int64_t q, int64_t i0,
+                                           int64_t n_rows, const f32x4_t& acc, float qs,
+                                           float th, float4 cs, uint32_t* lcnt, int64_t grp) {
+  const float v[4] = {acc[0] * qs * cs.x, acc[1] * qs * cs.y, acc[2] * qs * cs.z,
+                      acc[3] * qs * cs.w};
+  if constexpr (!FILTER) {
+    float* srow = e.S + q * e.ld_s;
+    if (i0 + 3 < n_rows) {
+      *(float4*)(srow + i0) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (i0 + r < n_rows) srow[i0 + r] = v[r];
+    }
+  } else {
+    // a cheap all-miss test first: the append path is taken for ~k'/rows-so-far of the values;
+    // keeping it cold keeps the accumulators in registers
+    const bool any = (v[0] >= th && i0 < n_rows) || (v[1] >= th && i0 + 1 < n_rows) ||
+                     (v[2] >= th && i0 + 2 < n_rows) || (v[3] >= th && i0 + 3 < n_rows);
+    if (__builtin_expect(any, 0)) filter_hits(e, q, i0, n_rows, v, th, lcnt, grp);
+  }
+}
+
 template <bool FILTER>
 __device__ __forceinline__ void epilogue4(const EpiArgs& e, int64_t q, int64_t i0,
                                           int64_t n_rows, const f32x4_t& acc, float qs,
                                           float th, const float* __restrict__ cscale,
                                           uint32_t* lcnt, int64_t grp) {
-  if constexpr (!FILTER) {
-    float* srow = e.S + q * e.ld_s;
-    if (i0 + 3 < n_rows) {
-      float4 cs = cscale ? *(const float4*)(cscale + i0) : make_float4(1.f, 1.f, 1.f, 1.f);
-      float4 v;
-      v.x = acc[0] * qs * cs.x;
-      v.y = acc[1] * qs * cs.y;
-      v.z = acc[2] * qs * cs.z;
-      v.w = acc[3] * qs * cs.w;
-      *(float4*)(srow + i0) = v;
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (i0 + r < n_rows) {
-          const float cs = cscale ? cscale[i0 + r] : 1.f;
-          srow[i0 + r] = acc[r] * qs * cs;
-        }
-      }
-    }
-  } else {
-    // one vector load of the row scales and a cheap all-miss test first: the append path is
-    // taken for ~k'/rows-so-far of the values; keeping it cold keeps the accumulators in
-    // registers
-    float4 cs = make_float4(1.f, 1.f, 1.f, 1.f);
-    if (cscale) {
-      if (i0 + 3 < n_rows) {
-        cs = *(const float4*)(cscale + i0);
-      } else {
-        cs.x = i0 + 0 < n_rows ? cscale[i0 + 0] : 1.f;
-        cs.y = i0 + 1 < n_rows ? cscale[i0 + 1] : 1.f;
-        cs.z = i0 + 2 < n_rows ? cscale[i0 + 2] : 1.f;
-        cs.w = i0 + 3 < n_rows ? cscale[i0 + 3] : 1.f;
-      }
-    }
-    const float v[4] = {acc[0] * qs * cs.x, acc[1] * qs * cs.y, acc[2] * qs * cs.z,
-                        acc[3] * qs * cs.w};
-    const bool any = (v[0] >= th && i0 < n_rows) || (v[1] >= th && i0 + 1 < n_rows) ||
-                     (v[2] >= th && i0 + 2 < n_rows) || (v[3] >= th && i0 + 3 < n_rows);
-    if (__builtin_expect(any, 0)) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t i = i0 + r;
-        if (i < n_rows && v[r] >= th) {
-          const uint32_t p = atomicAdd(lcnt, 1u);
-          if (p < (uint32_t)e.slots) {
-            const uint32_t row = (uint32_t)(e.idx_base + i);
-            e.cand[q * e.ld_cand + grp * e.slots + p] =
-                ((uint64_t)f2key(v[r]) << 32) | (uint64_t)(~row);
-          }
-        }
-      }
-    }
-  }
+  epilogue4v<FILTER>(e, q, i0, n_rows, acc, qs, th, row_scales4(cscale, i0, n_rows), lcnt, grp);
 }
 
 // End of a filter-mode tile: publish the per-query hit counts of group `grp` (LDS counters of
@@ -303,11 +312,32 @@ __device__ __forceinline__ void wait_vm_halves(int halves_after) {
 // machine scheduler.
 __device__ __forceinline__ void qp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
+#if EBT_ABL_PRIO == 1
+  __builtin_amdgcn_s_setprio(0);
+#endif
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+#if EBT_ABL_PRIO == 1
+  __builtin_amdgcn_s_setprio(1);
+#endif
   __builtin_amdgcn_sched_barrier(0);
 }
+#ifndef EBT_ABL_PRIO
+#define EBT_ABL_PRIO 0
+#endif
+#ifndef EBT_ABL_NOFINISH
+#define EBT_ABL_NOFINISH 0
+#endif
+#ifndef EBT_ABL_NOEPI
+#define EBT_ABL_NOEPI 0
+#endif
+#ifndef EBT_ABL_NOWAIT
+#define EBT_ABL_NOWAIT 0
+#endif
+#ifndef EBT_ABL_SLEEP
+#define EBT_ABL_SLEEP 1
+#endif
 
 // =============================================================================================
 // Pipelined quadrant phases (qp2): ONE barrier per phase, and the fragments of the NEXT phase
@@ -342,12 +372,12 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     int64_t n_rows, int n_qtiles, int64_t n_ctiles, int ktiles,
     const float* __restrict__ qscale, const float* __restrict__ cscale, EpiArgs e) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int64_t bid = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
   const int64_t nwg = (int64_t)n_qtiles * n_ctiles;
-  const int64_t bid = blockIdx.x;
   const int64_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int64_t L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int64_t per_group = (int64_t)QP_GROUP_C * n_qtiles;
@@ -358,9 +388,23 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
   const int64_t qt = w / gc;
   const int64_t c0 = ct * 256;
   const int64_t q0 = qt * 256;
-  uint32_t* lcnt = (uint32_t*)(smem + QP_LDS);  // filter mode: hits per query of the tile
+  // after the K-tile ring: hits per query of the tile (filter mode), then the epilogue's
+  // per-query scale / threshold and per-row scale, loaded before the prologue's LDS-DMA so they
+  // retire with its first wait instead of stalling the epilogue
+  uint32_t* lcnt = (uint32_t*)(smem + QP_LDS);
+  float* lqs = (float*)(smem + QP_LDS + 1024);
+  float* lth = lqs + QP_TILE;
+  float* lcs = lth + QP_TILE;
   if constexpr (FILTER) {
     if (tid < QP_TILE) lcnt[tid] = 0u;
+  }
+  float pre_a = 1.f, pre_b = 0.f;
+  if (tid < QP_TILE) {
+    pre_a = qscale[q0 + tid];
+    if constexpr (FILTER) pre_b = e.thr[q0 + tid];
+  } else {
+    const int64_t r = c0 + tid - QP_TILE;
+    pre_a = (cscale && r < n_rows) ? cscale[r] : 1.f;
   }
 
   const int wa = wave >> 2;
@@ -449,6 +493,12 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
 #pragma unroll
   for (int idx = 0; idx < 7; ++idx) issue(idx);
   wait_for(1, 6);
+  if (tid < QP_TILE) {
+    lqs[tid] = pre_a;
+    lth[tid] = pre_b;
+  } else {
+    lcs[tid - QP_TILE] = pre_a;
+  }
   qp_barrier();
   read_a(fa0, smem + p_half_off(P_A0));
   read_b(fbx, smem + p_half_off(P_B0));
@@ -472,7 +522,7 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     const char* nbuf = smem + ((t_ + 1) & 1) * QP_BUF;                                           \
     /* Q1 (A0, B0): read B1(t) */                                                                \
     qp_barrier();                                                                                \
-    if (!(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger the SIMD's second wave */       \
+    if (EBT_ABL_SLEEP && !(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
     QP2_ISSUE(4 * t_ + 7, GUARD);                                                                \
     qp2_mma<BF16>(acc0, fa0, s0);                                                                \
     read_b(s1, buf + p_half_off(P_B1));                                                          \
@@ -495,10 +545,10 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
       }                                                                                          \
     }                                                                                            \
-    if (GUARD) wait_for(4 * t_ + 3, 4 * t_ + 7); else wait_vm<8>(); /* A1(t) for Q2 */           \
+    if (GUARD) wait_for(4 * t_ + 3, 4 * t_ + 7); else if (!EBT_ABL_NOWAIT) wait_vm<8>(); /* A1(t) for Q2 */           \
     /* Q2 (A0, B1): read A1(t) */                                                                \
     qp_barrier();                                                                                \
-    if (!(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger the SIMD's second wave */       \
+    if (EBT_ABL_SLEEP && !(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
     QP2_ISSUE(4 * t_ + 8, GUARD);                                                                \
     qp2_mma<BF16>(acc1, fa0, s1);                                                                \
     read_a(fa1, buf + p_half_off(P_A1));                                                         \
@@ -523,7 +573,7 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     }                                                                                            \
     /* Q3 (A1, B1): no reads */                                                                  \
     qp_barrier();                                                                                \
-    if (!(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger the SIMD's second wave */       \
+    if (EBT_ABL_SLEEP && !(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
     QP2_ISSUE(4 * t_ + 9, GUARD);                                                                \
     qp2_mma<BF16>(acc2, fa1, s1);                                                                \
     if (!(GUARD)) {                                                                              \
@@ -533,10 +583,10 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
       __builtin_amdgcn_sched_group_barrier(0x008, 10, 0);                                        \
     }                                                                                            \
-    if (GUARD) wait_for(4 * t_ + 5, 4 * t_ + 9); else wait_vm<8>(); /* A0(t+1), B0(t+1) for Q4 */\
+    if (GUARD) wait_for(4 * t_ + 5, 4 * t_ + 9); else if (!EBT_ABL_NOWAIT) wait_vm<8>(); /* A0(t+1), B0(t+1) for Q4 */\
     /* Q4 (A1, B0): read A0(t+1), B0(t+1) */                                                     \
     qp_barrier();                                                                                \
-    if (!(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger the SIMD's second wave */       \
+    if (EBT_ABL_SLEEP && !(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
     QP2_ISSUE(4 * t_ + 10, GUARD);                                                               \
     qp2_mma<BF16>(acc3, fa1, s0);                                                                \
     if (!(GUARD) || t_ + 1 < ktiles) {                                                           \
@@ -564,9 +614,12 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
       }                                                                                          \
     }                                                                                            \
-    if (GUARD) wait_for(4 * t_ + 6, 4 * t_ + 10); else wait_vm<8>(); /* B1(t+1) for Q1(t+1) */   \
+    if (GUARD) wait_for(4 * t_ + 6, 4 * t_ + 10); else if (!EBT_ABL_NOWAIT) wait_vm<8>(); /* B1(t+1) for Q1(t+1) */   \
   }
 
+#if EBT_ABL_PRIO == 2
+  if (wa) __builtin_amdgcn_s_setprio(1);
+#endif
   int t = 0;
   // steady state: the last half-tile issued by the pair (t, t+1) is 4 (t+1) + 10 < 4 ktiles
   for (; t + 4 < ktiles; t += 2) {
@@ -582,25 +635,104 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
 #undef QP2_ISSUE
 
   // ---- epilogue: quadrant (ah, bh) = catalog half ah x query half bh ----
-  auto store_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh) {
+  const bool full = c0 + QP_TILE <= n_rows;  // uniform
+  // filter mode, full tile: the all-miss tests of the 32 accumulators first, branch-free into
+  // a hit mask (bit 8 quadrant + 4 j + i); the append path runs only for the set bits
+  auto test_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh, int quad) {
+    uint32_t m = 0;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int64_t q = q0 + bh * 128 + wb * 32 + j * 16 + fr;
-      const float qs = qscale[q];
-      const float th = FILTER ? e.thr[q] : 0.f;
+      const int ql = bh * 128 + wb * 32 + j * 16 + fr;
+      const float qs = lqs[ql];
+      const float th = lth[ql];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int64_t i0 = c0 + ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
-        epilogue4<FILTER>(e, q, i0, n_rows, acc[i][j], qs, th, cscale, lcnt + (q - q0), ct);
+        const int il = ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
+        const f32x4_t& a = acc[i][j];
+        float mx;
+        if (cscale) {
+          const float4 cs = *(const float4*)(lcs + il);
+          mx = fmaxf(fmaxf(a[0] * qs * cs.x, a[1] * qs * cs.y),
+                     fmaxf(a[2] * qs * cs.z, a[3] * qs * cs.w));
+        } else {
+          // max_r fl(a_r qs) = fl(max_r(a_r) qs) for qs >= 0 (rounding is monotone); NaNs drop
+          // out of fmaxf as they do out of >=
+          mx = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])) * qs;
+        }
+        m |= (mx >= th ? 1u : 0u) << (quad * 8 + j * 4 + i);
+      }
+    }
+    return m;
+  };
+  auto hits_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh, int quad, uint32_t m) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ql = bh * 128 + wb * 32 + j * 16 + fr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (m & (1u << (quad * 8 + j * 4 + i))) {
+          const int il = ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
+          const float qs = lqs[ql];
+          const float4 cs = *(const float4*)(lcs + il);
+          const f32x4_t& a = acc[i][j];
+          const float v[4] = {a[0] * qs * cs.x, a[1] * qs * cs.y, a[2] * qs * cs.z,
+                              a[3] * qs * cs.w};
+          filter_hits(e, q0 + ql, c0 + il, INT64_MAX, v, lth[ql], lcnt + ql, ct);
+        }
       }
     }
   };
-  store_quadrant(acc0, 0, 0);
-  store_quadrant(acc1, 0, 1);
-  store_quadrant(acc2, 1, 1);
-  store_quadrant(acc3, 1, 0);
+  auto store_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ql = bh * 128 + wb * 32 + j * 16 + fr;
+      const float qs = lqs[ql];
+      const float th = FILTER ? lth[ql] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int il = ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
+        const float4 cs = *(const float4*)(lcs + il);
+        epilogue4v<FILTER>(e, q0 + ql, c0 + il, n_rows, acc[i][j], qs, th, cs, lcnt + ql, ct);
+      }
+    }
+  };
+#if EBT_ABL_NOEPI
+  {  // ablation: no epilogue (keeps every accumulator chain alive)
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) sum += acc0[i][j][v] + acc1[i][j][v] + acc2[i][j][v] + acc3[i][j][v];
+    if (sum == 1234.5678f) e.ovf[0] = 7;
+    (void)store_quadrant;
+    (void)lcnt;
+  }
+#else
+  if (FILTER && full) {
+    const uint32_t m = test_quadrant(acc0, 0, 0, 0) | test_quadrant(acc1, 0, 1, 1) |
+                       test_quadrant(acc2, 1, 1, 2) | test_quadrant(acc3, 1, 0, 3);
+    if (__builtin_expect(m != 0u, 0)) {
+      hits_quadrant(acc0, 0, 0, 0, m);
+      hits_quadrant(acc1, 0, 1, 1, m);
+      hits_quadrant(acc2, 1, 1, 2, m);
+      hits_quadrant(acc3, 1, 0, 3, m);
+    }
+  } else {
+    store_quadrant(acc0, 0, 0);
+    store_quadrant(acc1, 0, 1);
+    store_quadrant(acc2, 1, 1);
+    store_quadrant(acc3, 1, 0);
+  }
+#if EBT_ABL_NOFINISH
+  (void)lcnt;
+#else
   if constexpr (FILTER) filter_finish(e, lcnt, q0, QP_TILE, ct);
+#endif
+#endif
 }
+
 
 // Kernel choice: batches padded to a multiple of 256 queries take the 256 x 256 quadrant-phase
 // kernel; smaller batches (B_pad = 128) the 128 x 128 one. Measured alternatives that lost on
@@ -625,7 +757,7 @@ static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_
     dim3 grid((unsigned)nwg), block(QP_THREADS);
     auto k = img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, FILTER>
                                    : screen_gemm_qp2_kernel<false, FILTER>;
-    const int lds = QP_LDS + (FILTER ? QP_TILE * 4 : 0);
+    const int lds = QP_LDS + 1024 + 3 * QP_TILE * 4;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(k, grid, block, lds, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
                        n_ctiles, d_pad / 64, qscale, cscale, e);

@@ -186,6 +186,12 @@ def score_topk_sharded(catalog: Catalog, k: int, queries: Optional[torch.Tensor]
     return s, r
 
 
+def _gathered_floor(coll, vals: torch.Tensor, eps: torch.Tensor, k: int) -> torch.Tensor:
+    """union_floor over every shard's (k best approx, eps), in ONE all-gather ([B, k+1] f32)."""
+    g = coll.all_gather(torch.cat([vals, eps[:, None]], 1))
+    return union_floor(g[:, :, :-1], g[:, :, -1], k)
+
+
 def score_topk_sharded_local(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
                              liked: Optional[Sequence[Sequence[int]]] = None,
                              exclude=None, group: Optional[dist.ProcessGroup] = None,
@@ -196,7 +202,7 @@ def score_topk_sharded_local(catalog: Catalog, k: int, queries: Optional[torch.T
     liked_arg = counts_t = hook = None
     if liked is not None:
         liked_arg, counts_t, hook = _liked_queries(catalog, liked, coll)
-    kw.setdefault("t_floor_hook", lambda v, e: union_floor(coll.all_gather(v), coll.all_gather(e), k))
+    kw.setdefault("t_floor_hook", lambda v, e: _gathered_floor(coll, v, e, k))
     s, r = score_topk(catalog, k, queries=queries, liked=liked_arg, exclude=exclude,
                       liked_counts=counts_t, liked_sum_hook=hook, **kw)
     return merge_topk(coll.all_gather(s), coll.all_gather(r), k)
