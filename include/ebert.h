@@ -200,6 +200,15 @@ int ebt_screen_exact(const double* q64, int64_t B, int32_t d, const void* cat, i
 int ebt_cosine_topk_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
                          int64_t chunk_rows, int flags, int64_t* head_rows, int64_t* cap,
                          int64_t* chunk, int32_t* fused);
+/* The speculative fused screen ebt_cosine_topk uses for these sizes (all 0: not used).
+ * sample_tiles full 256-row tiles, tile_stride tiles apart (tiles 0, s, 2s, ...), go through the
+ * screening GEMM keeping only each query's max per 64-row subgroup; the rank-th largest of those
+ * maxima is the query's speculative threshold theta for one filter pass over the whole catalog;
+ * hits = the expected hits per query. theta is checked afterwards (theta <= the k-th best approx
+ * - 2 eps, else certified = -1: rerun unfused), so it never costs exactness. */
+int ebt_cosine_topk_spec_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
+                              int flags, int64_t* sample_tiles, int64_t* tile_stride,
+                              int32_t* rank, double* hits);
 /* Workspace bytes needed by ebt_cosine_topk for these sizes. */
 size_t ebt_cosine_topk_workspace(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
                                  int64_t chunk_rows, int flags);
@@ -208,7 +217,11 @@ size_t ebt_cosine_topk_workspace(int64_t B, int64_t B_pad, int64_t n_rows, int32
  *   unfused: for every catalog chunk of chunk_rows rows: screening GEMM -> mask excluded ->
  *   streaming select of kprime candidates; then a select across chunks; then the exact float64
  *   rescore.
- *   fused (default when n_rows >= 2*H, H = max(65536, 256*kprime)): the head rows [0, H) go
+ *   speculative fused (default for B_pad % 256 == 0, kprime <= 512 and >= 8 sample tiles, see
+ *   ebt_cosine_topk_spec_plan): a pooled sample gives each query a threshold, the whole catalog
+ *   is filtered in a few large segments (later ones at max(theta, the list's k-th - 2 eps)),
+ *   then theta is verified (failure: certified = -1).
+ *   fused (otherwise, when n_rows >= 2*H, H = max(65536, 256*kprime)): the head rows [0, H) go
  *   through the unfused path; the k'-th best head score of each query is a lower bound of its
  *   global k'-th best. The tail rows [H, n) are screened in doubling segments (each as large as
  *   all rows before it): the GEMM appends only scores >= the query's current bound to its

@@ -67,6 +67,9 @@ _SIGNATURES = {
     "ebt_cosine_topk_plan": ([_I64, _I64, _I64, _I32, _I64, _INT, ctypes.POINTER(_I64),
                               ctypes.POINTER(_I64), ctypes.POINTER(_I64),
                               ctypes.POINTER(ctypes.c_int32)], _INT),
+    "ebt_cosine_topk_spec_plan": ([_I64, _I64, _I64, _I32, _INT, ctypes.POINTER(_I64),
+                                   ctypes.POINTER(_I64), ctypes.POINTER(ctypes.c_int32),
+                                   ctypes.POINTER(ctypes.c_double)], _INT),
     "ebt_cosine_topk": ([_VP, _VP, _VP, _VP, _I64, _I64, _VP, _INT, _I64, _VP, _VP, _VP, _INT,
                          _I32, _I64, _I32, _I32, _I64, _VP, _VP, _I32, _I32, _I64, _INT, _VP, _SZ,
                          _VP, _VP, _VP, _VP, _VP], _INT),

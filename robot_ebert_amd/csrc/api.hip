@@ -30,7 +30,7 @@ int launch_check(const char* what) { return hip_check(hipGetLastError(), what); 
 
 // kernels (defined in the other translation units)
 int screen_gemm(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int, const float*,
-                const float*, float*, int64_t, hipStream_t);
+                const float*, float*, int64_t, hipStream_t, int64_t cstride = 0);
 int select_topk(const float*, const int64_t*, int64_t, int64_t, int64_t, int64_t, int32_t,
                 int32_t, float*, int64_t*, int64_t, hipStream_t);
 int row_norms(const void*, int, int64_t, int32_t, int64_t, double*, float*, hipStream_t);
@@ -52,8 +52,13 @@ int screen_gemm_filter(const void*, int64_t, const void*, int64_t, int32_t, int3
                        uint8_t*, int64_t, int*, int64_t, hipStream_t);
 int64_t filter_group_rows(int64_t);
 
+int spec_threshold(const float*, int64_t, int64_t, int64_t, int, const float*, const float*, float*,
+                   int*, int, hipStream_t);
 int kth_threshold(const float*, int64_t, int64_t, int64_t, int, const float*, float*,
                   hipStream_t);
+int pool_kth(const float*, int64_t, int64_t, int64_t, int, int, float*, hipStream_t);
+int screen_gemm_pool(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
+                     const float*, const float*, int64_t, float*, int64_t, hipStream_t);
 int merge_segment(float*, int64_t*, int64_t, int, const uint64_t*, int64_t, int, const uint8_t*,
                   int64_t, int64_t, int64_t, const int64_t*, const int64_t*, int*, hipStream_t);
 bool merge_wave_fits(int);
@@ -142,9 +147,56 @@ struct WsLayout {
   int64_t chunk, ld_s, n_chunks, head, seg_max, group_rows, ld_cand, ld_counts;
   int segs;
   bool fused, pilot;
+  // speculative fused screen: `spec_tiles` 256-row sample tiles, `spec_stride` tiles apart;
+  // threshold = the spec_j-th best sample score - 2 eps; ~spec_hits expected hits per query
+  bool spec;
+  int64_t spec_tiles, spec_stride;
+  int spec_j;
+  double spec_hits;
   size_t off_s, off_segv, off_segi, off_chv, off_chi, off_fv, off_fi, off_cand, off_counts,
-      off_thr, off_ovf, off_eps, bytes;
+      off_thr, off_ovf, off_eps, off_tspec, bytes;
 };
+
+// Speculative screen parameters (see run_screen). The sample: P evenly spaced full 256-row tiles
+// (P = min(64, tiles / 24), so at most ~4 % of the rows are screened twice); lambda = the expected
+// number of sample rows at or above the rank-k' score, taking the sample as a uniform draw of
+// the rows; j = the smallest rank with P(Poisson(lambda) >= j) <= 1e-6, so a speculative
+// threshold is too high (caught by the VERIFY check -> unfused rerun) about once per million
+// queries on data in no particular order. Expected hits per query ~ j n / m.
+static bool spec_params(int64_t B_pad, int64_t n_rows, int32_t kprime, int64_t* tiles,
+                        int64_t* stride, int* j, double* hits) {
+  static const int enabled = [] {
+    const char* v = getenv("EBT_SPEC");
+    return v ? atoi(v) : 1;
+  }();
+  if (!enabled || B_pad % 256 != 0 || !merge_wave_fits(kprime)) return false;
+  const int64_t full = n_rows / 256;
+  int64_t P = full / 24;
+  P = P > 64 ? 64 : P;
+  // whole rounds of workgroups: P x (query tiles) a multiple of 256 when that keeps >= 8 tiles
+  const int64_t per = 256 / (B_pad / 256) > 0 ? 256 / (B_pad / 256) : 1;
+  if (P / per * per >= 8) P = P / per * per;
+  if (P < 8) return false;
+  const double m = 256.0 * P;
+  const double lam = (double)kprime * m / (double)n_rows;
+  // upper tail of Poisson(lam): 1 - sum_{i<j} pmf(i)
+  double pmf = exp(-lam), cdf = 0.0;
+  int jj = 0;
+  for (; jj < 100000; ++jj) {
+    if (1.0 - cdf <= 1e-6) break;
+    cdf += pmf;
+    pmf *= lam / (jj + 1);
+  }
+  if (jj < 1) jj = 1;
+  if (jj > (int)(m / 64) / 2) return false;  // the pooled estimate: 4P maxima per query
+  *tiles = P;
+  *stride = full / P;
+  *j = jj;
+  // the j-th of the 4P pooled maxima sits ~j^2 / (2 * 4P) sample ranks lower (two of the top j
+  // sample rows in one 64-row subgroup count once)
+  *hits = ((double)jj + (double)jj * jj / (8.0 * P)) * (double)n_rows / m;
+  return true;
+}
 
 static size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 
@@ -162,26 +214,36 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
     return v ? atoll(v) : 65536LL;
   }();
   L.pilot = merge_wave_fits(kprime);
+  L.spec = !(flags & (EBT_FLAG_NO_FUSE | EBT_FLAG_EXACT)) &&
+           spec_params(B_pad, n_rows, kprime, &L.spec_tiles, &L.spec_stride, &L.spec_j,
+                       &L.spec_hits);
   int64_t H = 256LL * kprime;
   H = H < h_min ? h_min : H;
   H = (H + 255) / 256 * 256;
   if (L.pilot) H = PILOT_ROWS;
-  L.fused = !(flags & (EBT_FLAG_NO_FUSE | EBT_FLAG_EXACT)) && n_rows >= 2 * H;
+  if (L.spec) H = 256 * L.spec_tiles;  // the sample (its rows are filtered again with the rest)
+  L.fused = L.spec || (!(flags & (EBT_FLAG_NO_FUSE | EBT_FLAG_EXACT)) && n_rows >= 2 * H);
   L.head = L.fused ? H : n_rows;
   if (L.fused) {
     // hit slots: up to 1 GiB of u64 per call, never more than the whole tail at the minimum of
     // 16 slots per group (plus the pilot segment's few groups at up to 128 slots)
     L.group_rows = filter_group_rows(B_pad);
     const int64_t budget = (1LL << 30) / (B_pad * 8);
-    const int64_t need = ceil_div(n_rows - H, L.group_rows) * 16 + 8 * EBT_FILTER_SLOTS_MAX;
+    const int64_t need = ceil_div(n_rows - (L.spec ? 0 : H), L.group_rows) * 16 +
+                         8 * EBT_FILTER_SLOTS_MAX;
     L.ld_cand = budget < need ? budget : need;
     L.ld_cand = L.ld_cand < 8 * EBT_FILTER_SLOTS_MAX ? 8 * EBT_FILTER_SLOTS_MAX : L.ld_cand;
     L.seg_max = L.ld_cand / 16 * L.group_rows;
     L.ld_counts = (L.ld_cand / 16 + 15) / 16 * 16;
   }
   L.chunk = chunk_rows < L.head ? chunk_rows : L.head;
+  if (L.spec) L.chunk = L.head / 64;  // the sample's pooled maxima (4 per tile)
   if (L.chunk < 1) L.chunk = 1;
   L.ld_s = (L.chunk + 3) & ~(int64_t)3;
+  // score rows >= 4 KiB: pitch = 64 floats past a multiple of 64, so the store epilogue's 16
+  // query rows per instruction and the select's concurrent rows do not all start on the same
+  // HBM channel (a power-of-two pitch measured 5x slower writes and reads)
+  if (L.ld_s >= 1024) L.ld_s = (L.ld_s + 63) / 64 * 64 + 64;
   L.n_chunks = ceil_div(L.head, L.chunk);
   // enough select workgroups to fill the chip: >= 512 (2 per CU)
   int64_t segs = B > 0 ? ceil_div(512, B) : 1;
@@ -217,6 +279,10 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
   }
   L.off_eps = o;
   if (flags & EBT_FLAG_EXACT) o = align_up(o + (size_t)B_pad * 4);
+  if (L.spec) {
+    L.off_tspec = o;
+    o = align_up(o + (size_t)B_pad * 4);
+  }
   L.bytes = o;
   return L;
 }
@@ -426,6 +492,22 @@ int ebt_cosine_topk_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprim
   return EBT_OK;
 }
 
+int ebt_cosine_topk_spec_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
+                              int flags, int64_t* sample_tiles, int64_t* tile_stride,
+                              int32_t* rank, double* hits) {
+  if (B < 0 || B_pad < B || n_rows < 1 || kprime < 1 || !sample_tiles || !tile_stride || !rank ||
+      !hits) {
+    set_error("ebt_cosine_topk_spec_plan: bad arguments");
+    return EBT_EINVAL;
+  }
+  const WsLayout L = ws_layout(B, B_pad, n_rows, kprime, 1024, flags);
+  *sample_tiles = L.spec ? L.spec_tiles : 0;
+  *tile_stride = L.spec ? L.spec_stride : 0;
+  *rank = L.spec ? L.spec_j : 0;
+  *hits = L.spec ? L.spec_hits : 0.0;
+  return EBT_OK;
+}
+
 }  // extern "C"
 
 namespace ebt {
@@ -480,6 +562,102 @@ static int check_pipe(const PipeArgs& a, const char* who) {
   return EBT_OK;
 }
 
+// The speculative fused screen. The progressive pilot/segment screen below pays for its rising
+// threshold with ~k' ln(n / 1024) hits per query (measured ~2850 at C3 over 6 filter launches,
+// each hit a cold epilogue path while the tile's MFMAs idle). Here:
+//   1. sample: P full 256-row tiles spread evenly over the catalog through the GEMM with the
+//      POOL epilogue (strided tiles; per query only the max of each 64-row subgroup leaves the
+//      kernel); theta_spec = the j-th largest of those 4P maxima (spec_params: the rank whose
+//      estimate exceeds the k'-th best catalog score with probability <= 1e-6 on unordered data);
+//   2. the whole catalog through the filter GEMM with theta_spec in few large segments (the list
+//      starts empty; later segments raise the threshold to max(theta_spec, list k-th - 2 eps)),
+//      each followed by the wave merge (exclusions dropped there);
+//   3. VERIFY: theta_spec <= the final list's k-th - 2 eps, else ovf = 2 -> certificate -1 ->
+//      the query is rerun unfused. So theta_spec needs no proof: a wrong guess costs a rerun.
+// Sample rows are screened twice (in the sample and in the filter pass); they enter the list
+// only through the filter, so nothing is counted twice.
+static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float* fv,
+                           int64_t* fi, void* timer, hipStream_t st) {
+  int rc;
+  const int64_t B = a.B, B_pad = a.B_pad, n_rows = a.n_rows;
+  const int32_t k = a.k, kprime = a.kprime;
+  uint64_t* cand = (uint64_t*)(ws + L.off_cand);
+  uint8_t* counts = (uint8_t*)(ws + L.off_counts);
+  float* thr = (float*)(ws + L.off_thr);
+  int* ovf = (int*)(ws + L.off_ovf);
+  float* pooled = (float*)(ws + L.off_s);
+  float* tspec = (float*)(ws + L.off_tspec);
+  const int64_t m = L.head;
+  {
+    StageScope s(timer, EBT_STAGE_GEMM, st);
+    rc = screen_gemm_pool(a.qimg, B_pad, a.cimg, m, a.d_pad, a.ld_img, a.img_dtype, a.qscale,
+                          a.cscale, 256 * L.spec_stride, pooled, L.ld_s, st);
+  }
+  if (rc) return rc;
+  {
+    StageScope s(timer, EBT_STAGE_SELECT, st);
+    rc = pool_kth(pooled, L.ld_s, B, B_pad, (int)(m / 64), L.spec_j, tspec, st);
+  }
+  if (rc) return rc;
+  // empty list (-inf / -1), no overflow yet
+  const float ninf = -__builtin_inff();
+  uint32_t bits;
+  memcpy(&bits, &ninf, 4);
+  rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)fv, (int)bits, (size_t)B * kprime, st),
+                 "hipMemsetD32Async");
+  if (!rc) rc = hip_check(hipMemsetAsync(fi, 0xff, (size_t)B * kprime * 8, st), "hipMemsetAsync");
+  if (!rc) rc = hip_check(hipMemsetAsync(ovf, 0, (size_t)B_pad * 4, st), "hipMemsetAsync");
+  if (rc) return rc;
+  // hits per 256-row group ~ H 256 / n: slots for 4x that (+8)
+  const double per_group = L.spec_hits * (double)L.group_rows / (double)n_rows;
+  int slots = 8;
+  while (slots < 4.0 * per_group + 8.0 && slots < EBT_FILTER_SLOTS_MAX) slots *= 2;
+  int64_t seg_cap = L.ld_cand / slots;
+  seg_cap = seg_cap < merge_wave_max_groups() ? seg_cap : merge_wave_max_groups();
+  seg_cap *= L.group_rows;
+  const double cap = (double)merge_wave_capacity();
+  int64_t r0 = 0;
+  while (r0 < n_rows) {
+    // expected hits <= 0.4 of the merge's room beside the list (the hit count has a relative
+    // spread of ~1/sqrt(j): an overflow, i.e. an unfused rerun, stays rare). Hits per row: at
+    // theta_spec H / n; after r0 rows the raised threshold (the list's k-th - 2 eps) keeps at
+    // most ~k' / r0 of the rows. A remainder of less than half a segment joins the last one.
+    const double room = 0.4 * (cap - kprime);
+    double rate = L.spec_hits / (double)n_rows;
+    if (r0 > 0 && (double)kprime / (double)r0 < rate) rate = (double)kprime / (double)r0;
+    int64_t seg = (int64_t)(room / (rate > 1e-12 ? rate : 1e-12));
+    seg = (seg + 255) / 256 * 256;
+    seg = seg < 256 ? 256 : seg;
+    seg = seg < seg_cap ? seg : seg_cap;
+    if (r0 > 0 && n_rows - r0 - seg < seg / 2) seg = n_rows - r0;
+    if (seg > seg_cap) seg = seg_cap;
+    if (seg > n_rows - r0) seg = n_rows - r0;
+    const float* t = tspec;
+    if (r0 > 0) {
+      rc = spec_threshold(fv, kprime, B, B_pad, k, a.eps, tspec, thr, ovf, 0, st);
+      if (rc) return rc;
+      t = thr;
+    }
+    {
+      StageScope s(timer, EBT_STAGE_GEMM_FILTER, st);
+      rc = screen_gemm_filter(a.qimg, B_pad, (const char*)a.cimg + r0 * a.ld_img * 2, seg,
+                              a.d_pad, a.ld_img, a.img_dtype, a.qscale,
+                              a.cscale ? a.cscale + r0 : nullptr, t, cand, L.ld_cand, slots,
+                              counts, L.ld_counts, ovf, r0, st);
+    }
+    if (rc) return rc;
+    {
+      StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
+      rc = merge_segment_wave(fv, fi, B, kprime, k, cand, L.ld_cand, slots, counts, L.ld_counts,
+                              ceil_div(seg, L.group_rows), a.row_offset, a.excl_off, a.excl_rows,
+                              ovf, st);
+    }
+    if (rc) return rc;
+    r0 += seg;
+  }
+  return spec_threshold(fv, kprime, B, B_pad, k, a.eps, tspec, nullptr, ovf, 1, st);
+}
+
 // The screen: the k' best approx candidates per query into fv/fi (LOCAL rows, sorted), by the
 // exact (float64) screen, the unfused chunked screen or the fused pilot/segment screen.
 static int run_screen(const PipeArgs& a, const WsLayout& L, char* ws, float* fv, int64_t* fi,
@@ -512,6 +690,7 @@ static int run_screen(const PipeArgs& a, const WsLayout& L, char* ws, float* fv,
   float* thr = (float*)(ws + L.off_thr);
   int* ovf = (int*)(ws + L.off_ovf);
   so->ovf = ovf;
+  if (L.spec) return run_screen_spec(a, L, ws, fv, fi, timer, st);
   // 1. head rows [0, H): exact top-k' per query (the list fv/fi)
   if (L.pilot) {
     float* S = (float*)(ws + L.off_s);

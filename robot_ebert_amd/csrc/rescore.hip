@@ -425,7 +425,7 @@ __global__ void export_list_kernel(int64_t* __restrict__ rows, int64_t B, int kp
     rows[b * kprime + j] = r >= 0 ? r + row_offset : -1;
   }
   if (threadIdx.x == 0) {
-    ovf_out[b] = ovf ? (ovf[b] > 0 ? 1 : 0) : 0;
+    ovf_out[b] = ovf ? (ovf[b] > 0 ? ovf[b] : 0) : 0;  // 1 overflow, 2 speculation failed
     eps_out[b] = eps[b];
   }
 }

@@ -366,11 +366,18 @@ __device__ __forceinline__ void qp2_mma(f32x4_t (&acc)[4][2], const u16x8_t (&a)
       for (int j = 0; j < 2; ++j) acc[i][j] = mfma16<BF16>(a[i][ks], b[j][ks], acc[i][j]);
 }
 
-template <bool BF16, bool FILTER>
+// Epilogue modes of the quadrant-phase kernel: EPI_STORE (score rows), EPI_FILTER (the fused
+// screen's hit slots), EPI_POOL (the speculative screen's sample: per query and 64-row subgroup
+// only the MAX score, S[q][4 ct + 2 ah + wa] -- 64x less output than the scores).
+enum { EPI_STORE = 0, EPI_FILTER = 1, EPI_POOL = 2 };
+
+template <bool BF16, int EPI>
 __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ C, int64_t ld_img,
     int64_t n_rows, int n_qtiles, int64_t n_ctiles, int ktiles,
-    const float* __restrict__ qscale, const float* __restrict__ cscale, EpiArgs e) {
+    const float* __restrict__ qscale, const float* __restrict__ cscale, EpiArgs e,
+    int64_t cstride) {
+  constexpr bool FILTER = EPI == EPI_FILTER;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int64_t bid = blockIdx.x;
   const int tid = threadIdx.x;
@@ -387,6 +394,9 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
   const int64_t ct = g * QP_GROUP_C + w % gc;
   const int64_t qt = w / gc;
   const int64_t c0 = ct * 256;
+  // catalog row of the tile's first row: c0, or ct * cstride for a strided sample of full tiles
+  // (store mode; n_rows then counts the sample's rows and the scores stay dense)
+  const int64_t c0s = ct * cstride;
   const int64_t q0 = qt * 256;
   // after the K-tile ring: hits per query of the tile (filter mode), then the epilogue's
   // per-query scale / threshold and per-row scale, loaded before the prologue's LDS-DMA so they
@@ -403,8 +413,8 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     pre_a = qscale[q0 + tid];
     if constexpr (FILTER) pre_b = e.thr[q0 + tid];
   } else {
-    const int64_t r = c0 + tid - QP_TILE;
-    pre_a = (cscale && r < n_rows) ? cscale[r] : 1.f;
+    const int64_t r = tid - QP_TILE;
+    pre_a = (cscale && c0 + r < n_rows) ? cscale[c0s + r] : 1.f;
   }
 
   const int wa = wave >> 2;
@@ -442,7 +452,8 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
   const int64_t row_bytes = ld_img * 2;
   const int64_t c_rem = (n_rows - c0) * row_bytes;
   const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(C + c0 * ld_img), 0, (int)(c_rem < 0x7fffffffLL ? c_rem : 0x7fffffffLL), 0x00020000);
+      (void*)(C + c0s * ld_img), 0, (int)(c_rem < 0x7fffffffLL ? c_rem : 0x7fffffffLL),
+      0x00020000);
   const __amdgpu_buffer_rsrc_t rsQ = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(Q + q0 * ld_img), 0, (int)(256 * row_bytes), 0x00020000);
   // lane: row (wave*16 + (lane>>3)) of the half, 16-byte chunk (lane&7)^(lane>>3)
@@ -710,7 +721,35 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     (void)lcnt;
   }
 #else
-  if (FILTER && full) {
+  // pool mode: max over the 64 rows (ah, wa) of each query: 4 accumulators x 4 values in the
+  // lane, then the 4 lanes of the same fr (lane ^ 16, ^ 32); rows past n_rows are skipped
+  auto pool_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ql = bh * 128 + wb * 32 + j * 16 + fr;
+      const float qs = lqs[ql];
+      float mx = -__builtin_inff();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int il = ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
+        const float4 cs = *(const float4*)(lcs + il);
+        const f32x4_t& a = acc[i][j];
+        const float v[4] = {a[0] * qs * cs.x, a[1] * qs * cs.y, a[2] * qs * cs.z, a[3] * qs * cs.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (c0 + il + r < n_rows) mx = fmaxf(mx, v[r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if ((lane >> 4) == 0) e.S[(q0 + ql) * e.ld_s + ct * 4 + ah * 2 + wa] = mx;
+    }
+  };
+  if constexpr (EPI == EPI_POOL) {
+    pool_quadrant(acc0, 0, 0);
+    pool_quadrant(acc1, 0, 1);
+    pool_quadrant(acc2, 1, 1);
+    pool_quadrant(acc3, 1, 0);
+  } else if (FILTER && full) {
     const uint32_t m = test_quadrant(acc0, 0, 0, 0) | test_quadrant(acc1, 0, 1, 1) |
                        test_quadrant(acc2, 1, 1, 2) | test_quadrant(acc3, 1, 0, 3);
     if (__builtin_expect(m != 0u, 0)) {
@@ -739,11 +778,13 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
 // MI355X ("screening GEMM"): a 4-slot ring with k32 slices, one barrier per phase
 // with two barriers (qp), a persistent one-workgroup-per-CU walk of the same tiles, and a
 // 4-wave 128 x 128-per-wave tile (LDS-DMA issue cost with one wave per SIMD).
-template <bool FILTER>
+template <int EPI>
 static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
                        int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
-                       const float* cscale, const EpiArgs& e, hipStream_t stream) {
+                       const float* cscale, const EpiArgs& e, hipStream_t stream,
+                       int64_t cstride = 0) {
   const bool big = B_pad % QP_TILE == 0;
+  if (cstride == 0) cstride = big ? QP_TILE : GBM;
   const int n_qtiles = (int)(B_pad / (big ? QP_TILE : GBN));
   const int64_t n_ctiles = ceil_div(n_rows, big ? QP_TILE : GBM);
   const int64_t nwg = n_ctiles * n_qtiles;
@@ -755,14 +796,19 @@ static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_
   const uint16_t* C = (const uint16_t*)cimg;
   if (big) {
     dim3 grid((unsigned)nwg), block(QP_THREADS);
-    auto k = img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, FILTER>
-                                   : screen_gemm_qp2_kernel<false, FILTER>;
+    auto k = img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, EPI>
+                                   : screen_gemm_qp2_kernel<false, EPI>;
     const int lds = QP_LDS + 1024 + 3 * QP_TILE * 4;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(k, grid, block, lds, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
-                       n_ctiles, d_pad / 64, qscale, cscale, e);
+                       n_ctiles, d_pad / 64, qscale, cscale, e, cstride);
     return launch_check("screen_gemm_qp2_kernel");
   }
+  if (cstride != GBM || EPI == EPI_POOL) {
+    set_error("screen gemm: strided tiles / pooled scores need a batch padded to 256");
+    return EBT_EINVAL;
+  }
+  constexpr bool FILTER = EPI == EPI_FILTER;
   dim3 grid((unsigned)nwg), block(GTHREADS);
   auto k = img_dtype == EBT_BF16 ? screen_gemm_kernel<true, FILTER>
                                  : screen_gemm_kernel<false, FILTER>;
@@ -772,6 +818,8 @@ static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_
                      n_ctiles, d_pad / GBK, qscale, cscale, e);
   return launch_check("screen_gemm_kernel");
 }
+
+int64_t filter_group_rows(int64_t B_pad);
 
 static int check_gemm_args(const char* who, const void* qimg, int64_t B_pad, const void* cimg,
                            int64_t n_rows, int32_t d_pad, int32_t ld_img, int img_dtype,
@@ -795,7 +843,7 @@ static int check_gemm_args(const char* who, const void* qimg, int64_t B_pad, con
 
 int screen_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows, int32_t d_pad,
                 int32_t ld_img, int img_dtype, const float* qscale, const float* cscale,
-                float* scores, int64_t ld_scores, hipStream_t stream) {
+                float* scores, int64_t ld_scores, hipStream_t stream, int64_t cstride) {
   int rc = check_gemm_args("ebt_screen_scores", qimg, B_pad, cimg, n_rows, d_pad, ld_img,
                            img_dtype, qscale, cscale);
   if (rc) return rc;
@@ -806,8 +854,34 @@ int screen_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_row
   EpiArgs e{};
   e.S = scores;
   e.ld_s = ld_scores;
-  return launch_gemm<false>(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale, cscale,
-                            e, stream);
+  if (cstride == 0) cstride = filter_group_rows(B_pad);
+  if (cstride != filter_group_rows(B_pad) && (cstride < QP_TILE || n_rows % QP_TILE != 0)) {
+    set_error("ebt_screen_scores: strided tiles must be full and non-overlapping");
+    return EBT_EINVAL;
+  }
+  return launch_gemm<EPI_STORE>(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale,
+                                cscale, e, stream, cstride);
+}
+
+// The speculative screen's sample: P full 256-row tiles, cstride rows apart (P = n_rows / 256),
+// -> pooled[q][g] = max score of query q over the sample's 64-row subgroup g (4P per query).
+int screen_gemm_pool(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
+                     int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
+                     const float* cscale, int64_t cstride, float* pooled, int64_t ld_pooled,
+                     hipStream_t stream) {
+  int rc = check_gemm_args("screen_gemm_pool", qimg, B_pad, cimg, n_rows, d_pad, ld_img,
+                           img_dtype, qscale, cscale);
+  if (rc) return rc;
+  if (!pooled || B_pad % QP_TILE != 0 || n_rows % QP_TILE != 0 || cstride < QP_TILE ||
+      ld_pooled < n_rows / 64) {
+    set_error("screen_gemm_pool: bad arguments");
+    return EBT_EINVAL;
+  }
+  EpiArgs e{};
+  e.S = pooled;
+  e.ld_s = ld_pooled;
+  return launch_gemm<EPI_POOL>(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale,
+                               cscale, e, stream, cstride);
 }
 
 int64_t filter_group_rows(int64_t B_pad) { return B_pad % QP_TILE == 0 ? QP_TILE : GBM; }
@@ -837,8 +911,8 @@ int screen_gemm_filter(const void* qimg, int64_t B_pad, const void* cimg, int64_
   e.ovf = ovf;
   e.idx_base = idx_base;
   e.slots = slots;
-  return launch_gemm<true>(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale, cscale,
-                           e, stream);
+  return launch_gemm<EPI_FILTER>(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale,
+                                 cscale, e, stream);
 }
 
 }  // namespace ebt

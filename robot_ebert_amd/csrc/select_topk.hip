@@ -837,4 +837,96 @@ int kth_threshold(const float* vals, int64_t ld, int64_t B, int64_t B_pad, int k
   return launch_check("kth_threshold_kernel");
 }
 
+// The speculative fused screen (api.hip, run_screen): a threshold theta_spec[b] estimated from a
+// sample of the catalog filters the whole catalog in one pass. theta_spec is NOT a proven lower
+// bound of T - 2 eps (T = the final list's k-th approx), so it is checked afterwards:
+//   RAISE:  thr[b] = max(theta_spec[b], the list's k-th - 2 eps rounded down) for the next
+//           segment (the second term is the rigorous kth_threshold value; padding rows +inf);
+//   VERIFY: theta_spec[b] > the list's k-th - 2 eps (rounded down) sets ovf[b]: a row the filter
+//           dropped might belong to the top k, so the query loses its certificate (-1) and is
+//           rerun unfused. A list with fewer than k entries (-inf) or a NaN fails the test too.
+//   INIT:   theta_spec[b] = vals[b][k-1] (the sample's j-th best as it is: the check is
+//           theta_spec <= T - 2 eps, so no margin is subtracted here); padding rows +inf.
+enum { SPEC_RAISE = 0, SPEC_VERIFY = 1, SPEC_INIT = 2 };
+__global__ void spec_threshold_kernel(const float* __restrict__ vals, int64_t ld, int64_t B,
+                                      int64_t B_pad, int k, const float* __restrict__ eps,
+                                      const float* __restrict__ thr_spec, float* __restrict__ thr,
+                                      int* __restrict__ ovf, int mode) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (mode == SPEC_INIT) {
+    if (b < B_pad) thr[b] = b < B ? vals[b * ld + k - 1] : __builtin_inff();
+    return;
+  }
+  if (b < B) {
+    const double t = (double)vals[b * ld + k - 1] - 2.0 * (double)eps[b];
+    float f = (float)t;
+    if ((double)f > t && f == f && f != -__builtin_inff()) {  // one float step down
+      const uint32_t u = __float_as_uint(f);
+      f = f == 0.f ? -__uint_as_float(1u) : __uint_as_float(f > 0.f ? u - 1u : u + 1u);
+    }
+    const float s = thr_spec[b];
+    if (mode == SPEC_RAISE) thr[b] = f > s ? f : s;  // NaN f keeps s
+    else if (!(s <= f)) ovf[b] = 2;
+  } else if (b < B_pad && mode == SPEC_RAISE) {
+    thr[b] = __builtin_inff();
+  }
+}
+// theta_spec[b] = the j-th largest of query b's G <= 256 pooled sample maxima (one wave per
+// query; the largest key t with count(key >= t) >= j, by bisection with ballot counts). A 64-row
+// subgroup's max is >= x only if one of its rows is, so P(theta_spec > x) <= P(>= j sample rows
+// >= x): spec_params' Poisson bound holds for the pooled estimate too. Fewer than j valid maxima
+// -> -inf (keep everything: the merge overflows and the query is rerun unfused).
+__global__ __launch_bounds__(256) void pool_kth_kernel(const float* __restrict__ pool, int64_t ld,
+                                                       int64_t B, int64_t B_pad, int G, int j,
+                                                       float* __restrict__ thr) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B_pad) return;
+  if (b >= B) {
+    if (lane == 0) thr[b] = __builtin_inff();
+    return;
+  }
+  uint32_t kx[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int g = lane + 64 * e;
+    kx[e] = g < G ? f2key(pool[b * ld + g]) : 0u;
+  }
+  auto count_ge = [&](uint32_t t) {
+    int c = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) c += __popcll(__ballot(kx[e] >= t));
+    return c;
+  };
+  uint64_t lo = 1, hi = 0xffffffffull;  // largest t with count(key >= t) >= j
+  if (count_ge(1u) < j) {
+    if (lane == 0) thr[b] = -__builtin_inff();
+    return;
+  }
+  while (lo < hi) {
+    const uint64_t mid = lo + ((hi - lo + 1) >> 1);
+    if (count_ge((uint32_t)mid) >= j) lo = mid;
+    else hi = mid - 1;
+  }
+  if (lane == 0) thr[b] = key2f((uint32_t)lo);
+}
+int pool_kth(const float* pool, int64_t ld, int64_t B, int64_t B_pad, int G, int j, float* thr,
+             hipStream_t st) {
+  if (G < 1 || G > 256 || j < 1 || ld < G) {
+    set_error("pool_kth: bad arguments (G=%d j=%d)", G, j);
+    return EBT_EINVAL;
+  }
+  hipLaunchKernelGGL(pool_kth_kernel, dim3((unsigned)ceil_div(B_pad, 4)), dim3(256), 0, st, pool,
+                     ld, B, B_pad, G, j, thr);
+  return launch_check("pool_kth_kernel");
+}
+
+int spec_threshold(const float* vals, int64_t ld, int64_t B, int64_t B_pad, int k,
+                   const float* eps, const float* thr_spec, float* thr, int* ovf, int mode,
+                   hipStream_t st) {
+  hipLaunchKernelGGL(spec_threshold_kernel, dim3((unsigned)ceil_div(B_pad, 256)), dim3(256), 0,
+                     st, vals, ld, B, B_pad, k, eps, thr_spec, thr, ovf, mode);
+  return launch_check("spec_threshold_kernel");
+}
+
 }  // namespace ebt

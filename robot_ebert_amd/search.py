@@ -180,8 +180,24 @@ def plan(catalog: Catalog, B: int, k: int, kprime: Optional[int] = None,
     call("ebt_cosine_topk_plan", B, B_pad, catalog.n, kp, chunk,
          0 if fuse else _lib.EBT_FLAG_NO_FUSE, ctypes.byref(h), ctypes.byref(c), ctypes.byref(ch),
          ctypes.byref(f))
-    return {"kprime": kp, "B_pad": B_pad, "fused": bool(f.value), "head_rows": h.value,
-            "segment_rows_max": c.value, "chunk_rows": ch.value}
+    out = {"kprime": kp, "B_pad": B_pad, "fused": bool(f.value), "head_rows": h.value,
+           "segment_rows_max": c.value, "chunk_rows": ch.value}
+    out["spec"] = spec_plan(B, catalog.n, kp, fuse)
+    return out
+
+
+def spec_plan(B: int, n: int, kprime: int, fuse: bool = True) -> Optional[dict]:
+    """The speculative screen's sample (ebt_cosine_topk_spec_plan) or None when not used:
+    tiles (256 rows each), stride (tiles apart, from tile 0), rank (j) and expected hits."""
+    import ctypes
+    t, st, h = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double()
+    j = ctypes.c_int32()
+    call("ebt_cosine_topk_spec_plan", B, pad_batch(B), n, kprime,
+         0 if fuse else _lib.EBT_FLAG_NO_FUSE, ctypes.byref(t), ctypes.byref(st), ctypes.byref(j),
+         ctypes.byref(h))
+    if t.value == 0:
+        return None
+    return {"tiles": t.value, "stride": st.value, "rank": j.value, "hits": round(h.value, 1)}
 
 
 def run_pipeline(catalog: Catalog, qb: QueryBatch, k: int, kprime: int,

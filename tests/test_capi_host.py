@@ -122,3 +122,34 @@ def test_torch_ops_registered_with_fake_kernels():
     ms, mr = torch.ops.ebert.merge_topk(torch.empty(3, 7, 5, dtype=torch.float64, device="meta"),
                                         torch.empty(3, 7, 5, dtype=torch.int64, device="meta"), 5)
     assert ms.shape == (7, 5)
+
+
+def test_spec_plan_poisson_rank():
+    """The speculative screen's sample (ebt_cosine_topk_spec_plan): P evenly spaced tiles and the
+    smallest rank j with P(Poisson(k' m / n) >= j) <= 1e-6 (api.hip:spec_params)."""
+    import ctypes
+    from scipy.stats import poisson
+    from robot_ebert_amd import _lib
+    lib = _lib.load()
+
+    def sp(B, n, kp, flags=0):
+        t, s, h = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double()
+        j = ctypes.c_int32()
+        assert lib.ebt_cosine_topk_spec_plan(B, (B + 255) // 256 * 256 if B > 128 else 128, n,
+                                             kp, flags, ctypes.byref(t), ctypes.byref(s),
+                                             ctypes.byref(j), ctypes.byref(h)) == 0
+        return t.value, s.value, j.value, h.value
+
+    for (B, n, kp) in [(4096, 1_000_000, 200), (4096, 125_000, 200), (1024, 100_000, 120),
+                       (4096, 250_000, 200)]:
+        P, S, j, H = sp(B, n, kp)
+        assert P >= 8 and P <= 64 and (P - 1) * S * 256 + 256 <= n
+        lam = kp * 256 * P / n
+        assert poisson.sf(j - 1, lam) <= 1e-6 < poisson.sf(j - 2, lam), (n, P, j)
+        assert H >= j * n / (256 * P)
+    assert sp(4096, 1_000_000, 200)[:3] == (64, 61, 16)
+    assert sp(4096, 125_000, 200)[0] == 16          # one round of 256 workgroups
+    assert sp(100, 1_000_000, 104)[0] == 0          # B_pad = 128: the 128-tile kernel, no spec
+    assert sp(4096, 1_000_000, 1016)[0] == 0        # k' > 512: block merges, no spec
+    assert sp(4096, 20_000, 200)[0] == 0            # too few tiles for a sample
+    assert sp(4096, 1_000_000, 200, _lib.EBT_FLAG_NO_FUSE)[0] == 0

@@ -475,6 +475,59 @@ def test_fused_large_kprime_block_path(cuda_device):
     assert_topk_equal(s1[sample], r1[sample], s_ref, r_ref)
 
 
+def test_speculative_screen_matches_oracle(cuda_device):
+    """The speculative fused screen (pooled sample threshold, one filter pass, verify) on a
+    shape where it is the default: bit-exact rows vs the oracle, equal to the unfused path."""
+    ebt, L = _ebt()
+    n, d, B, k = 98_304, 96, 300, 20
+    c = gaussian(21, n, d, "f32")
+    q = gaussian(22, B, d, "f32")
+    rng = np.random.default_rng(23)
+    excl = [np.sort(rng.choice(n, 40, replace=False)) for _ in range(B)]
+    cat = ebt.Catalog(_t(c, "f32", cuda_device))
+    qt = _t(q, "f32", cuda_device)
+    pl = ebt.search.plan(cat, B, k)
+    assert pl["fused"] and pl["spec"] is not None and pl["spec"]["tiles"] >= 8, pl
+    timer = ebt.Timer()
+    s1, r1 = ebt.score_topk(cat, k, queries=qt, exclude=[list(e) for e in excl], timer=timer)
+    assert timer.query("gemm_filter")[1] >= 1
+    s2, r2 = ebt.score_topk(cat, k, queries=qt, exclude=[list(e) for e in excl], fuse=False)
+    assert torch.equal(r1, r2)
+    torch.testing.assert_close(s1, s2, rtol=0, atol=0)
+    s_ref, r_ref = R.cosine_topk(q.astype(np.float64), c.astype(np.float64), k,
+                                 [list(e) for e in excl])
+    assert_topk_equal(s1, r1, s_ref, r_ref)
+
+
+def test_speculative_threshold_failure_reruns(cuda_device):
+    """Near-duplicates of query 0 placed only in the SAMPLE tiles make its speculative
+    threshold (the sample's j-th best) exceed T - 2 eps: the verify step flags it (ovf = 2, cert
+    -1), the query is rerun unfused, and the result is still exact."""
+    ebt, L = _ebt()
+    from robot_ebert_amd.search import prepare_queries, run_screen
+    n, d, B, k = 98_304, 64, 256, 10
+    c = gaussian(31, n, d, "f32")
+    q = gaussian(32, B, d, "f32")
+    cat0 = ebt.Catalog(_t(c, "f32", cuda_device))
+    sp = ebt.search.plan(cat0, B, k)["spec"]
+    assert sp is not None
+    rng = np.random.default_rng(33)
+    for t in range(sp["tiles"]):
+        for r in range(4):  # 4 near-duplicates per sample tile: >> the rank j in the sample
+            c[t * sp["stride"] * 256 + 17 * r] = q[0] + 1e-3 * rng.standard_normal(d)
+    c = c.astype(np.float32)  # the oracle sees the values the GPU catalog holds
+    cat = ebt.Catalog(_t(c, "f32", cuda_device))
+    qt = _t(q, "f32", cuda_device)
+    qb = prepare_queries(cat, queries=qt)
+    kp = ebt.search.plan(cat, B, k)["kprime"]
+    lv, lr, ovf, eps = run_screen(cat, qb, k, kp)
+    assert int(ovf[0]) == 2, "the verify step did not catch the bad speculative threshold"
+    s, r = ebt.score_topk(cat, k, queries=qt)
+    sample = [0, 1, 100, 255]
+    s_ref, r_ref = R.cosine_topk(q[sample].astype(np.float64), c.astype(np.float64), k)
+    assert_topk_equal(s[sample], r[sample], s_ref, r_ref)
+
+
 def test_fused_overflow_falls_back(cuda_device):
     """Scores that grow with the row index make the head threshold useless: every tail row
     passes, the candidate list overflows, and the query must be redone unfused -- exactly."""
