@@ -154,7 +154,8 @@ def main() -> None:
     dev = torch.device("cuda", local_rank)
 
     import robot_ebert_amd as ebt
-    from robot_ebert_amd.distributed import score_topk_sharded_local, shard_range
+    from robot_ebert_amd.distributed import (score_topk_sharded_local_finish,
+                                             score_topk_sharded_local_submit, shard_range)
     ebt.load()
 
     begin, end = shard_range(cfg["n"], rank, world)
@@ -166,14 +167,33 @@ def main() -> None:
     timer = ebt.Timer()
     k = cfg["k"]
 
-    def step():
+    # A step is submitted (all of its kernels and collectives enqueued) before the previous
+    # step is finished (its certificates checked on the host, retries run): the GPU never waits
+    # for the host between batches. Every step is a complete batch through the whole path.
+    def submit():
         if world > 1:  # per-shard exact top-k, one RCCL all-gather, merge
-            return score_topk_sharded_local(cat, k, queries=q, timer=timer)
-        return ebt.score_topk(cat, k, queries=q, timer=timer)
+            return score_topk_sharded_local_submit(cat, k, queries=q, timer=timer)
+        return ebt.score_topk_submit(cat, k, queries=q, timer=timer)
+
+    def finish(p):
+        if world > 1:
+            return score_topk_sharded_local_finish(p)
+        return ebt.score_topk_finish(p)
+
+    def run_steps(n, log_every=0):
+        pending, out = None, None
+        for i in range(n):
+            p = submit()
+            if pending is not None:
+                out = finish(pending)
+            pending = p
+            if log_every and (i + 1) % log_every == 0:
+                log(f"step {i + 1}/{n} submitted")
+        return finish(pending) if pending is not None else out
 
     for i in range(args.warmup):
         t0 = time.perf_counter()
-        step()
+        run_steps(1)
         torch.cuda.synchronize(dev)
         log(f"warmup {i + 1}/{args.warmup}: {time.perf_counter() - t0:.3f} s")
     timer.reset()
@@ -181,10 +201,7 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        s, r = step()
-        if (i + 1) % max(1, args.steps // 5) == 0:
-            log(f"step {i + 1}/{args.steps} enqueued")
+    s, r = run_steps(args.steps, max(1, args.steps // 5))
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()

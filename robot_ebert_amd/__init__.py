@@ -6,7 +6,8 @@ ctypes). Python keeps the reference's call surface: ``lib.get_user_recs`` and fr
 """
 from ._lib import EbertError, Timer, load  # noqa: F401
 from .catalog import Catalog  # noqa: F401
-from .search import merge_topk, prepare_queries, rescore_rows, score_topk  # noqa: F401
+from .search import (merge_topk, prepare_queries, rescore_rows, score_topk,  # noqa: F401
+                     score_topk_finish, score_topk_submit)
 from . import ops  # noqa: F401,E402  (registers torch.ops.ebert.*)
 
 __version__ = "0.1.0"

@@ -34,7 +34,8 @@ from . import _lib
 from ._lib import EbertError, call, ptr, stream_of
 from .catalog import Catalog
 from .search import (KPRIME_MAX, _round_up, csr_from_lists, csr_subset, default_kprime,
-                     merge_topk, prepare_queries, run_screen, score_topk, union_floor)
+                     merge_topk, prepare_queries, run_screen, score_topk, score_topk_finish,
+                     score_topk_submit, union_floor)
 
 
 def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
@@ -197,12 +198,31 @@ def score_topk_sharded_local(catalog: Catalog, k: int, queries: Optional[torch.T
                              exclude=None, group: Optional[dist.ProcessGroup] = None,
                              collectives=None, **kw) -> Tuple[torch.Tensor, torch.Tensor]:
     """Per-shard exact top-k (the single-GPU path on each shard) + all-gather + merge."""
+    return score_topk_sharded_local_finish(score_topk_sharded_local_submit(
+        catalog, k, queries=queries, liked=liked, exclude=exclude, group=group,
+        collectives=collectives, **kw))
+
+
+def score_topk_sharded_local_submit(catalog: Catalog, k: int,
+                                    queries: Optional[torch.Tensor] = None,
+                                    liked: Optional[Sequence[Sequence[int]]] = None,
+                                    exclude=None, group: Optional[dist.ProcessGroup] = None,
+                                    collectives=None, **kw):
+    """Enqueue a batch of score_topk_sharded_local (its screen and the floor all-gather) and
+    return without waiting; score_topk_sharded_local_finish completes it (retries, all-gather,
+    merge). Every rank must submit and finish its batches in the same order: the collectives
+    are issued in program order, so ranks stay in lockstep."""
     coll = collectives if collectives is not None else TorchCollectives(group)
-    dev = catalog.device
     liked_arg = counts_t = hook = None
     if liked is not None:
         liked_arg, counts_t, hook = _liked_queries(catalog, liked, coll)
     kw.setdefault("t_floor_hook", lambda v, e: _gathered_floor(coll, v, e, k))
-    s, r = score_topk(catalog, k, queries=queries, liked=liked_arg, exclude=exclude,
-                      liked_counts=counts_t, liked_sum_hook=hook, **kw)
+    pending = score_topk_submit(catalog, k, queries=queries, liked=liked_arg, exclude=exclude,
+                                liked_counts=counts_t, liked_sum_hook=hook, **kw)
+    return pending, coll, k
+
+
+def score_topk_sharded_local_finish(sub) -> Tuple[torch.Tensor, torch.Tensor]:
+    pending, coll, k = sub
+    s, r = score_topk_finish(pending)
     return merge_topk(coll.all_gather(s), coll.all_gather(r), k)

@@ -255,14 +255,18 @@ def run_screen(catalog: Catalog, qb: QueryBatch, k: int, kprime: int,
     return lv, lr, ovf, eps
 
 
-def score_topk(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
+def score_topk_submit(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
                liked: Optional[Union[Tuple[torch.Tensor, torch.Tensor], Sequence[Sequence[int]]]] = None,
                exclude: Optional[Union[Tuple[torch.Tensor, torch.Tensor], Sequence[Sequence[int]]]] = None,
                kprime: Optional[int] = None, chunk_rows: Optional[int] = None,
                timer: Optional[_lib.Timer] = None, liked_counts: Optional[torch.Tensor] = None,
                liked_sum_hook=None, fuse: bool = True,
-               t_floor_hook=None) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Top-k by cosine (mean cosine over liked rows) with exclusions.
+               t_floor_hook=None) -> "PendingTopk":
+    """Enqueue the first pass of score_topk (see there) on the catalog's device and return
+    without waiting for it: score_topk_finish(pending) waits, retries the queries whose
+    certificate needs it and returns (scores, rows). Submitting batch i+1 before finishing
+    batch i keeps the GPU busy while the host checks certificates (bench.py's step loop).
+    Top-k by cosine (mean cosine over liked rows) with exclusions.
 
     Returns (scores float64 [B, k], rows int64 [B, k]) on the catalog's device, ordered by
     (score desc, row asc); rows are GLOBAL row ids; missing entries (fewer than k candidates)
@@ -299,16 +303,36 @@ def score_topk(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
     else:
         s, r, cert = _screen_global_cut(catalog, qb, k_eff, k, kp, exclude, chunk_rows, timer,
                                         flags, t_floor_hook)
+    # the certificates travel to pinned host memory right behind this batch's kernels, so
+    # finishing it waits for this batch only, not for batches submitted after it
+    cert_host = torch.empty(cert.shape, dtype=cert.dtype, pin_memory=True)
+    cert_host.copy_(cert, non_blocking=True)
+    ready = torch.cuda.Event()
+    ready.record(torch.cuda.current_stream(dev))
+    return PendingTopk(catalog, qb, k, k_eff, kp, exclude, chunk_rows, timer, flags, n_cap,
+                       s, r, cert, cert_host, ready)
+
+
+def score_topk_finish(p: "PendingTopk") -> Tuple[torch.Tensor, torch.Tensor]:
+    """Wait for a submitted batch, run its retries, return (scores f64 [B, k], rows i64 [B, k])."""
+    catalog, qb, k, k_eff, kp = p.catalog, p.qb, p.k, p.k_eff, p.kprime
+    exclude, chunk_rows, timer, flags, n_cap = p.exclude, p.chunk_rows, p.timer, p.flags, p.n_cap
+    s, r, cert = p.s, p.r, p.cert
+    dev = catalog.device
+    p.ready.synchronize()
+    flat = p.cert_host
     # retries, only for the queries that need one: a fused candidate list that overflowed
     # (cert -1: rerun unfused) or a candidate set that is not provably complete (cert 0: widen k')
     while True:
-        flat = cert.cpu()
+        if flat is None:
+            flat = cert.cpu()
         if bool((flat == -2).any()):
             raise EbertError("internal error: candidate row out of range (libebert bug)")
         over = torch.nonzero(flat == -1).flatten().to(dev)
         bad = torch.nonzero(flat == 0).flatten().to(dev)
         if over.numel() == 0 and bad.numel() == 0:
             break
+        flat = None
         if over.numel():
             sub_ex = csr_subset(exclude[0], exclude[1], over) if exclude is not None else None
             s2, r2, c2 = run_pipeline(catalog, qb.subset(over), k_eff, kp, sub_ex, chunk_rows,
@@ -337,6 +361,41 @@ def score_topk(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
         pad_r = torch.full((qb.B, k - k_eff), -1, dtype=torch.int64, device=dev)
         s, r = torch.cat([s, pad_s], 1), torch.cat([r, pad_r], 1)
     return s, r
+
+
+def score_topk(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
+               liked: Optional[Union[Tuple[torch.Tensor, torch.Tensor], Sequence[Sequence[int]]]] = None,
+               exclude: Optional[Union[Tuple[torch.Tensor, torch.Tensor], Sequence[Sequence[int]]]] = None,
+               kprime: Optional[int] = None, chunk_rows: Optional[int] = None,
+               timer: Optional[_lib.Timer] = None, liked_counts: Optional[torch.Tensor] = None,
+               liked_sum_hook=None, fuse: bool = True,
+               t_floor_hook=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Top-k by cosine (mean cosine over liked rows) with exclusions: score_topk_submit +
+    score_topk_finish (arguments and results as documented there)."""
+    return score_topk_finish(score_topk_submit(
+        catalog, k, queries=queries, liked=liked, exclude=exclude, kprime=kprime,
+        chunk_rows=chunk_rows, timer=timer, liked_counts=liked_counts,
+        liked_sum_hook=liked_sum_hook, fuse=fuse, t_floor_hook=t_floor_hook))
+
+
+@dataclass
+class PendingTopk:
+    """A submitted score_topk batch: its first pass is enqueued, retries not yet decided."""
+    catalog: Catalog
+    qb: QueryBatch
+    k: int
+    k_eff: int
+    kprime: int
+    exclude: Optional[Tuple[torch.Tensor, torch.Tensor]]
+    chunk_rows: Optional[int]
+    timer: Optional[_lib.Timer]
+    flags: int
+    n_cap: int
+    s: torch.Tensor
+    r: torch.Tensor
+    cert: torch.Tensor
+    cert_host: torch.Tensor          # pinned copy of cert, valid once `ready` has completed
+    ready: torch.cuda.Event
 
 
 def union_floor(vals: torch.Tensor, eps: torch.Tensor, k: int) -> torch.Tensor:

@@ -528,6 +528,30 @@ def test_speculative_threshold_failure_reruns(cuda_device):
     assert_topk_equal(s[sample], r[sample], s_ref, r_ref)
 
 
+def test_submit_finish_pipelined_equals_sync(cuda_device):
+    """score_topk_submit of batch i+1 before score_topk_finish of batch i (bench.py's step
+    loop): each batch's result equals its synchronous score_topk, including a batch whose
+    queries need retries (near-duplicates: certificate 0 -> widened k')."""
+    ebt, L = _ebt()
+    n, d, k = 70_000, 64, 16
+    c = gaussian(41, n, d, "f32")
+    qa = gaussian(42, 300, d, "f32")
+    qb = gaussian(43, 300, d, "f32")
+    c[1000:1400] = (qb[0] + 1e-7 * np.arange(400)[:, None]).astype(np.float32)  # a near-tie wall
+    cat = ebt.Catalog(_t(c, "f32", cuda_device))
+    ta, tb = _t(qa, "f32", cuda_device), _t(qb, "f32", cuda_device)
+    pa = ebt.score_topk_submit(cat, k, queries=ta)
+    pb = ebt.score_topk_submit(cat, k, queries=tb)
+    sa, ra = ebt.score_topk_finish(pa)
+    sb, rb = ebt.score_topk_finish(pb)
+    for (s, r, t) in ((sa, ra, ta), (sb, rb, tb)):
+        s2, r2 = ebt.score_topk(cat, k, queries=t)
+        assert torch.equal(r, r2)
+        torch.testing.assert_close(s, s2, rtol=0, atol=0)
+    s_ref, r_ref = R.cosine_topk(qb[:4].astype(np.float64), c.astype(np.float64), k)
+    assert_topk_equal(sb[:4], rb[:4], s_ref, r_ref)
+
+
 def test_fused_overflow_falls_back(cuda_device):
     """Scores that grow with the row index make the head threshold useless: every tail row
     passes, the candidate list overflows, and the query must be redone unfused -- exactly."""

@@ -77,12 +77,22 @@ def one_rank(args):
                           "rescored_nocut": float((lv0 >= cut0[:, None]).sum(1).double().mean()),
                           "rescored_cut": float((lv0 >= cut1[:, None]).sum(1).double().mean())}),
               flush=True)
-        for name, hook in (("cut", lambda v, e: t_glob.clone()), ("nocut", None)):
+        variants = (("cut", lambda v, e: t_glob.clone()), ("nocut", None))
+        if args.only:
+            variants = [v for v in variants if v[0] == args.only]
+        for name, hook in variants:
+            pending = None  # pipelined as bench.py does: submit step i+1, then finish step i
             for i in range(args.steps + 1):
                 if i == 1:
+                    search.score_topk_finish(pending)
+                    pending = None
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
-                search.score_topk(cat0, k, queries=q, t_floor_hook=hook)
+                p = search.score_topk_submit(cat0, k, queries=q, t_floor_hook=hook)
+                if pending is not None:
+                    search.score_topk_finish(pending)
+                pending = p
+            search.score_topk_finish(pending)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) * 1e3 / args.steps
             tm = ebt.Timer()
@@ -102,6 +112,8 @@ def main():
     ap.add_argument("--one-rank", action="store_true",
                     help="time rank 0's own work alone (the floor all-reduce replaced by its "
                          "precomputed result) with and without the global cut")
+    ap.add_argument("--only", default=None, choices=["cut", "nocut"],
+                    help="--one-rank: time only this variant (profiling)")
     args = ap.parse_args()
     if args.one_rank:
         return one_rank(args)
