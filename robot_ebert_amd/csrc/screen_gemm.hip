@@ -339,6 +339,7 @@ __device__ __forceinline__ void qp_barrier() {
 #define EBT_ABL_SLEEP 1
 #endif
 
+
 // =============================================================================================
 // Pipelined quadrant phases (qp2): ONE barrier per phase, and the fragments of the NEXT phase
 // are read while the current phase's 16 MFMAs run (interleaved by sched_group_barrier), so LDS
@@ -647,49 +648,144 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
 
   // ---- epilogue: quadrant (ah, bh) = catalog half ah x query half bh ----
   const bool full = c0 + QP_TILE <= n_rows;  // uniform
-  // filter mode, full tile: the all-miss tests of the 32 accumulators first, branch-free into
-  // a hit mask (bit 8 quadrant + 4 j + i); the append path runs only for the set bits
-  auto test_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh, int quad) {
+  // Filter mode, register-resident: the epilogue constants of this lane (query scale
+  // and threshold per (bh, j), row scales per (ah, i)) are read from LDS ONCE; the hit path then
+  // runs on registers only. Per (bh, j) each lane builds the bit mask of its hits among its 32
+  // values of query ql (2 catalog halves x 4 accumulators x 4 rows), the 4 lanes of the query
+  // (lane ^ 16, ^ 32) take exclusive prefixes of their counts, the 4 slot claims of the wave
+  // (one LDS atomic per query) are issued together, and each lane writes its hits. The earlier
+  // per-hit form (LDS reads + a returned-value atomic per hit, all dependent) cost ~5 us per
+  // tile at ~40 hits per wave.
+  auto filter_tile = [&]() {
+    float qs_r[2][2], th_r[2][2];
+    float4 cs_r[2][4];
+#pragma unroll
+    for (int bh = 0; bh < 2; ++bh)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ql = bh * 128 + wb * 32 + j * 16 + fr;
+        qs_r[bh][j] = lqs[ql];
+        th_r[bh][j] = lth[ql];
+      }
+#pragma unroll
+    for (int ah = 0; ah < 2; ++ah)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        cs_r[ah][i] = *(const float4*)(lcs + ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4));
+    // quadrant q = (ah, bh): acc0 (0, 0), acc1 (0, 1), acc2 (1, 1), acc3 (1, 0)
+    auto acc_of = [&](int ah, int bh) -> const f32x4_t (&)[4][2] {
+      return ah == 0 ? (bh == 0 ? acc0 : acc1) : (bh == 0 ? acc3 : acc2);
+    };
+    auto val4 = [&](int ah, int bh, int i, int j, float (&v)[4]) {
+      const f32x4_t& a = acc_of(ah, bh)[i][j];
+      const float qs = qs_r[bh][j];
+      const float4 cs = cs_r[ah][i];
+      v[0] = a[0] * qs * cs.x;
+      v[1] = a[1] * qs * cs.y;
+      v[2] = a[2] * qs * cs.z;
+      v[3] = a[3] * qs * cs.w;
+    };
+    // all-miss test: bit (4 (2 bh + j) ... ) -> m bit (bh * 2 + j) * 8 + ah * 4 + i
     uint32_t m = 0;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int ql = bh * 128 + wb * 32 + j * 16 + fr;
-      const float qs = lqs[ql];
-      const float th = lth[ql];
+    for (int bh = 0; bh < 2; ++bh)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int il = ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
-        const f32x4_t& a = acc[i][j];
-        float mx;
-        if (cscale) {
-          const float4 cs = *(const float4*)(lcs + il);
-          mx = fmaxf(fmaxf(a[0] * qs * cs.x, a[1] * qs * cs.y),
-                     fmaxf(a[2] * qs * cs.z, a[3] * qs * cs.w));
-        } else {
-          // max_r fl(a_r qs) = fl(max_r(a_r) qs) for qs >= 0 (rounding is monotone); NaNs drop
-          // out of fmaxf as they do out of >=
-          mx = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])) * qs;
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ah = 0; ah < 2; ++ah)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float mx;
+            if (cscale || !full) {
+              float v[4];
+              val4(ah, bh, i, j, v);
+              if (!full) {  // the catalog's last tile: rows past n_rows never hit
+                const int64_t i0 = c0 + ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                  if (i0 + r >= n_rows) v[r] = -__builtin_inff();
+              }
+              mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+            } else {
+              // max_r fl(a_r qs) = fl(max_r(a_r) qs) for qs >= 0 (rounding is monotone); NaNs
+              // drop out of fmaxf as they do out of >=
+              const f32x4_t& a = acc_of(ah, bh)[i][j];
+              mx = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])) * qs_r[bh][j];
+            }
+            m |= (mx >= th_r[bh][j] ? 1u : 0u) << ((bh * 2 + j) * 8 + ah * 4 + i);
+          }
+    if (__builtin_expect(__ballot(m != 0u) == 0ull, 1)) return;
+    uint32_t hm[4];
+    int xs[4], cnt[4], tot[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int bh = c >> 1, j = c & 1;
+      uint32_t h = 0;
+#pragma unroll
+      for (int ah = 0; ah < 2; ++ah)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (m & (1u << (c * 8 + ah * 4 + i))) {
+            float v[4];
+            val4(ah, bh, i, j, v);
+            const int64_t i0 = c0 + ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              h |= (v[r] >= th_r[bh][j] && (full || i0 + r < n_rows) ? 1u : 0u)
+                   << (ah * 16 + i * 4 + r);
+          }
         }
-        m |= (mx >= th ? 1u : 0u) << (quad * 8 + j * 4 + i);
-      }
+      hm[c] = h;
+      cnt[c] = __popc(h);
+      int x = cnt[c];  // inclusive prefix over lanes fr, fr + 16, fr + 32, fr + 48
+      int y = __shfl_up(x, 16, 64);
+      if (lane >= 16) x += y;
+      y = __shfl_up(x, 32, 64);
+      if (lane >= 32) x += y;
+      xs[c] = x;
+      tot[c] = __shfl(x, 48 + fr, 64);
     }
-    return m;
-  };
-  auto hits_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh, int quad, uint32_t m) {
+    uint32_t base[4];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int ql = bh * 128 + wb * 32 + j * 16 + fr;
+    for (int c = 0; c < 4; ++c) {
+      const int ql = (c >> 1) * 128 + wb * 32 + (c & 1) * 16 + fr;
+      base[c] = (lane < 16 && tot[c] > 0) ? atomicAdd(lcnt + ql, (uint32_t)tot[c]) : 0u;
+    }
+    // the writes: per (bh, j) with hits in the wave, the lane's 32 values go to its staging
+    // slots in the (dead) K-tile ring -- every wave passed the last tile's final barrier after
+    // its last LDS read of the ring -- as 8 float4 planes, and a ROLLED loop over the set bits
+    // reads them back. (Fully unrolled per-bit code made the kernel ~84 KB: the hit path then
+    // ran from instruction-cache misses, ~2x the cost of the hits themselves.)
+    float4* stg = (float4*)(smem + wave * 8192);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (m & (1u << (quad * 8 + j * 4 + i))) {
-          const int il = ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
-          const float qs = lqs[ql];
-          const float4 cs = *(const float4*)(lcs + il);
-          const f32x4_t& a = acc[i][j];
-          const float v[4] = {a[0] * qs * cs.x, a[1] * qs * cs.y, a[2] * qs * cs.z,
-                              a[3] * qs * cs.w};
-          filter_hits(e, q0 + ql, c0 + il, INT64_MAX, v, lth[ql], lcnt + ql, ct);
+    for (int c = 0; c < 4; ++c) {
+      const int bh = c >> 1, j = c & 1;
+      if (__ballot(hm[c] != 0u) == 0ull) continue;
+#pragma unroll
+      for (int ah = 0; ah < 2; ++ah)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v[4];
+          val4(ah, bh, i, j, v);
+          stg[(ah * 4 + i) * 64 + lane] = make_float4(v[0], v[1], v[2], v[3]);
         }
+      const int ql = bh * 128 + wb * 32 + j * 16 + fr;
+      uint32_t p = (uint32_t)__shfl((int)base[c], fr, 64) + (uint32_t)(xs[c] - cnt[c]);
+      uint64_t* dst = e.cand + (q0 + ql) * e.ld_cand + ct * e.slots;
+      const float* sf = (const float*)stg;
+      uint32_t h = hm[c];
+#pragma unroll 1
+      while (h) {
+        const int bit = __builtin_ctz(h);
+        h &= h - 1u;
+        if (p < (uint32_t)e.slots) {
+          const float v = sf[((bit >> 2) * 64 + lane) * 4 + (bit & 3)];
+          const int il = (bit >> 4) * 128 + wa * 64 + ((bit >> 2) & 3) * 16 + 4 * (lane >> 4) +
+                         (bit & 3);
+          const uint32_t row = (uint32_t)(e.idx_base + c0 + il);
+          dst[p] = ((uint64_t)f2key(v) << 32) | (uint64_t)(~row);
+        }
+        ++p;
       }
     }
   };
@@ -749,15 +845,8 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     pool_quadrant(acc1, 0, 1);
     pool_quadrant(acc2, 1, 1);
     pool_quadrant(acc3, 1, 0);
-  } else if (FILTER && full) {
-    const uint32_t m = test_quadrant(acc0, 0, 0, 0) | test_quadrant(acc1, 0, 1, 1) |
-                       test_quadrant(acc2, 1, 1, 2) | test_quadrant(acc3, 1, 0, 3);
-    if (__builtin_expect(m != 0u, 0)) {
-      hits_quadrant(acc0, 0, 0, 0, m);
-      hits_quadrant(acc1, 0, 1, 1, m);
-      hits_quadrant(acc2, 1, 1, 2, m);
-      hits_quadrant(acc3, 1, 0, 3, m);
-    }
+  } else if constexpr (FILTER) {
+    filter_tile();
   } else {
     store_quadrant(acc0, 0, 0);
     store_quadrant(acc1, 0, 1);

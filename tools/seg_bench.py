@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--d", type=int, default=1536)
     ap.add_argument("--kprime", type=int, default=200)
     ap.add_argument("--segs", default=None, help="r:s,... (default: 3x growth from 1024, cap 524288)")
+    ap.add_argument("--no-inf", action="store_true", help="skip the no-hit comparison launch")
     ap.add_argument("--hits", default=None, help="h1,h2,...: one launch over --n rows per target "
                     "hits/query (Gaussian quantile threshold)")
     a = ap.parse_args()
@@ -66,7 +67,7 @@ def main():
         ms = timeit(lambda: run(thr))
         hits = float(counts.float().sum(1).mean())
         inf = torch.full_like(thr, float("inf"))
-        ms0 = timeit(lambda: run(inf))
+        ms0 = timeit(lambda: run(inf)) if not a.no_inf else float("nan")
         total_ms += ms
         total_ms0 += ms0
         tf = 2.0 * B * s * d / (ms * 1e-3) / 1e12
