@@ -14,7 +14,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DOMINANT = "screen_gemm_qp2_kernel<false, true>"  # f16 image, filter epilogue
+DOMINANT = "screen_gemm_qp2_kernel<false, 1>"  # f16 image, EPI_FILTER epilogue
 
 
 def per_kernel(path, counter):
