@@ -146,15 +146,16 @@ int ebt_select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B
  * best by (score desc, row asc) go to out_scores/out_rows[b*k + j] (rows + row_offset; empty
  * slots NaN / -1). certified[b] = 1 iff the candidate set provably contains the exact top-k:
  * kprime >= n_rows (every row is a candidate),
- * fewer than kprime valid candidates, or approx[kprime-1] < approx[k-1] - 2*eps[b].
+ * fewer than kprime valid candidates, or approx[kprime-1] < cut[b] (below).
  * n_rows is the catalog's row count; a candidate row >= n_rows is never read and gives
  * certified[b] = -2 (corrupt candidate list).
- * Candidates with approx < max(approx[k-1] - 2*eps[b], t_floor[b] - eps[b]) cannot be in the
- * top k and are not gathered (equal cand_vals and eps = 0 rescore every candidate). t_floor
+ * Candidates with approx < cut[b] = max(approx[k-1] - 2*eps[b], t_floor[b] - eps[b]) cannot
+ * be in the top k and are not gathered (equal cand_vals and eps = 0 rescore every candidate). t_floor
  * (float64 [B], NULL = none) is a lower bound of the k-th best EXACT score over the whole
  * (sharded) catalog, e.g. the all-reduced max over shards of approx[k-1] - eps: a shard then
  * rescores only rows that can enter the GLOBAL top k, and the slots of its top k that such a
- * cut leaves empty read NaN / -1. The certificate is unchanged (it is about this list). */
+ * cut leaves empty read NaN / -1: the certificate is then about the GLOBAL top k (a row
+ * dropped below approx[kprime-1] < t_floor - eps has exact < t_floor). */
 int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype, int64_t ld,
                 const double* gnorm64, int64_t row_offset, const float* cand_vals,
                 const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
@@ -194,6 +195,7 @@ int ebt_screen_exact(const double* q64, int64_t B, int32_t d, const void* cat, i
  * kprime = 4096, certified with eps = EBT_EXACT_EPS (|q64| <= 1 as the ebt_query_* make it). */
 #define EBT_FLAG_NO_FUSE 1
 #define EBT_FLAG_EXACT 2
+#define EBT_FLAG_THETA 4 /* internal: set by ebt_cosine_screen_at (workspace sizing only) */
 #define EBT_EXACT_EPS 1.1920928955078125e-07f /* 2^-23 >= f32 rounding of |s| <= 1 + f64 error */
 /* How ebt_cosine_topk will run these sizes (host pointers out): head rows screened unfused,
  * the largest fused tail segment in rows (cap; 0 = not fused), score chunk rows, fused flag. */
@@ -264,6 +266,38 @@ int ebt_cosine_screen(const double* q64, const void* qimg, const float* qscale, 
                       int64_t chunk_rows, int flags, void* workspace, size_t ws_bytes,
                       float* list_vals, int64_t* list_rows, int32_t* ovf_out, float* eps_out,
                       void* timer, void* stream);
+/* ---- shared screening threshold over a row-sharded catalog (distributed.py) -------------
+ * The per-shard path (every rank: its exact top-k, then one all-gather + ebt_merge_topk)
+ * screens every shard at ONE catalog-wide threshold instead of each shard's own:
+ *   1. ebt_cosine_sample: `tiles` full 256-row tiles of this shard, `tile_stride` tiles apart
+ *      from tile 0, through the screening GEMM keeping only the max of every 64-row subgroup:
+ *      pooled[b * ld_pooled + 4 t + s] (B_pad rows, 4 * tiles maxima each; B_pad % 256 == 0).
+ *   2. the ranks all-gather the maxima; ebt_pool_kth: theta[b] = the j-th largest of the G
+ *      values pooled[b * ld + 0 .. G) (G <= 2048), -inf when fewer than j are >= -inf;
+ *      theta[b] = +inf for B <= b < B_pad.
+ *   3. ebt_cosine_screen_at = ebt_cosine_screen with the filter threshold theta[b] (device,
+ *      [B]) instead of the shard's own sample estimate, `hits` = the expected hits per query on
+ *      this shard (segment sizing). The list then holds this shard's rows with approx >= theta
+ *      (and >= the list's own k-th - 2 eps once it has k rows): often fewer than k. Rows below
+ *      theta are not screened out silently: theta is NOT checked here -- the caller must
+ *      verify theta[b] <= t_floor[b] - eps[b] with the catalog-wide floor it passes to
+ *      ebt_rescore, and rerun a query that fails (unfused, locally). kprime <= 512.
+ * Replaces nothing in the reference (no sharding there). */
+int ebt_cosine_sample(const void* qimg, const float* qscale, int64_t B_pad, const void* cimg,
+                      const float* cscale, int img_dtype, int32_t ld_img, int64_t n_rows,
+                      int32_t d_pad, int64_t tiles, int64_t tile_stride, float* pooled,
+                      int64_t ld_pooled, void* timer, void* stream);
+int ebt_pool_kth(const float* pooled, int64_t ld, int64_t B, int64_t B_pad, int32_t G, int32_t j,
+                 float* theta, void* stream);
+int ebt_cosine_screen_at(const double* q64, const void* qimg, const float* qscale,
+                         const float* eps, int64_t B, int64_t B_pad, const void* cat, int dtype,
+                         int64_t ld, const double* gnorm64, const void* cimg, const float* cscale,
+                         int img_dtype, int32_t ld_img, int64_t n_rows, int32_t d, int32_t d_pad,
+                         int64_t row_offset, const int64_t* excl_off, const int64_t* excl_rows,
+                         int32_t k, int32_t kprime, int64_t chunk_rows, int flags,
+                         void* workspace, size_t ws_bytes, float* list_vals, int64_t* list_rows,
+                         int32_t* ovf_out, float* eps_out, const float* theta, double hits,
+                         void* timer, void* stream);
 int ebt_rescore_owned(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
                       int64_t ld, const double* gnorm64, int64_t row_offset, int64_t n_rows,
                       const float* cand_vals, const int64_t* cand_rows, int32_t kprime, int32_t k,

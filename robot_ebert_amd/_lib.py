@@ -22,6 +22,7 @@ DTYPE_CODE = {torch.float32: EBT_F32, torch.bfloat16: EBT_BF16, torch.float16: E
 STAGES = {"gemm": 0, "mask": 1, "select": 2, "merge_select": 3, "rescore": 4, "gemm_filter": 5}
 EBT_FLAG_NO_FUSE = 1
 EBT_FLAG_EXACT = 2
+EBT_FLAG_THETA = 4
 EBT_FILTER_SLOTS_MAX = 128
 
 
@@ -50,6 +51,13 @@ _SIGNATURES = {
     "ebt_cosine_screen": ([_VP, _VP, _VP, _VP, _I64, _I64, _VP, _INT, _I64, _VP, _VP, _VP, _INT,
                            _I32, _I64, _I32, _I32, _I64, _VP, _VP, _I32, _I32, _I64, _INT, _VP,
                            ctypes.c_size_t, _VP, _VP, _VP, _VP, _VP, _VP], _INT),
+    "ebt_cosine_screen_at": ([_VP, _VP, _VP, _VP, _I64, _I64, _VP, _INT, _I64, _VP, _VP, _VP,
+                              _INT, _I32, _I64, _I32, _I32, _I64, _VP, _VP, _I32, _I32, _I64,
+                              _INT, _VP, ctypes.c_size_t, _VP, _VP, _VP, _VP, _VP,
+                              ctypes.c_double, _VP, _VP], _INT),
+    "ebt_cosine_sample": ([_VP, _VP, _I64, _VP, _VP, _INT, _I32, _I64, _I32, _I64, _I64, _VP,
+                           _I64, _VP, _VP], _INT),
+    "ebt_pool_kth": ([_VP, _I64, _I64, _I64, _I32, _I32, _VP, _VP], _INT),
     "ebt_rescore_owned": ([_VP, _I64, _I32, _VP, _INT, _I64, _VP, _I64, _I64, _VP, _VP, _I32,
                            _I32, _VP, _VP, _VP], _INT),
     "ebt_finalize_topk": ([_VP, _VP, _VP, _I64, _I32, _I32, _I64, _VP, _VP, _VP, _VP, _VP, _VP],

@@ -217,6 +217,13 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
   L.spec = !(flags & (EBT_FLAG_NO_FUSE | EBT_FLAG_EXACT)) &&
            spec_params(B_pad, n_rows, kprime, &L.spec_tiles, &L.spec_stride, &L.spec_j,
                        &L.spec_hits);
+  if ((flags & EBT_FLAG_THETA) && !(flags & (EBT_FLAG_NO_FUSE | EBT_FLAG_EXACT)) &&
+      merge_wave_fits(kprime)) {
+    // the caller's threshold (ebt_cosine_screen_at): no sample of our own; the spec layout
+    // (hit slots, threshold buffer) is kept, the sample scores buffer shrinks to one tile
+    if (!L.spec) L.spec_tiles = 1;
+    L.spec = true;
+  }
   int64_t H = 256LL * kprime;
   H = H < h_min ? h_min : H;
   H = (H + 255) / 256 * 256;
@@ -541,6 +548,9 @@ struct PipeArgs {
   int32_t k, kprime;
   int64_t chunk_rows;
   int flags;
+  // ebt_cosine_screen_at: the caller's per-query threshold [B] and expected hits per query
+  const float* theta = nullptr;
+  double hits = 0.0;
 };
 
 static int check_pipe(const PipeArgs& a, const char* who) {
@@ -588,17 +598,31 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
   float* pooled = (float*)(ws + L.off_s);
   float* tspec = (float*)(ws + L.off_tspec);
   const int64_t m = L.head;
-  {
-    StageScope s(timer, EBT_STAGE_GEMM, st);
-    rc = screen_gemm_pool(a.qimg, B_pad, a.cimg, m, a.d_pad, a.ld_img, a.img_dtype, a.qscale,
-                          a.cscale, 256 * L.spec_stride, pooled, L.ld_s, st);
+  const bool given = a.theta != nullptr;  // ebt_cosine_screen_at: the caller's threshold
+  if (given) {
+    const float inf = __builtin_inff();
+    uint32_t bits;
+    memcpy(&bits, &inf, 4);
+    rc = hip_check(hipMemcpyAsync(tspec, a.theta, (size_t)B * 4, hipMemcpyDeviceToDevice, st),
+                   "hipMemcpyAsync");
+    if (!rc && B_pad > B)
+      rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)(tspec + B), (int)bits,
+                                       (size_t)(B_pad - B), st), "hipMemsetD32Async");
+    if (rc) return rc;
+  } else {
+    {
+      StageScope s(timer, EBT_STAGE_GEMM, st);
+      rc = screen_gemm_pool(a.qimg, B_pad, a.cimg, m, a.d_pad, a.ld_img, a.img_dtype, a.qscale,
+                            a.cscale, 256 * L.spec_stride, pooled, L.ld_s, st);
+    }
+    if (rc) return rc;
+    {
+      StageScope s(timer, EBT_STAGE_SELECT, st);
+      rc = pool_kth(pooled, L.ld_s, B, B_pad, (int)(m / 64), L.spec_j, tspec, st);
+    }
+    if (rc) return rc;
   }
-  if (rc) return rc;
-  {
-    StageScope s(timer, EBT_STAGE_SELECT, st);
-    rc = pool_kth(pooled, L.ld_s, B, B_pad, (int)(m / 64), L.spec_j, tspec, st);
-  }
-  if (rc) return rc;
+  const double spec_hits = given ? (a.hits > 0.0 ? a.hits : 1.0) : L.spec_hits;
   // empty list (-inf / -1), no overflow yet
   const float ninf = -__builtin_inff();
   uint32_t bits;
@@ -609,7 +633,7 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
   if (!rc) rc = hip_check(hipMemsetAsync(ovf, 0, (size_t)B_pad * 4, st), "hipMemsetAsync");
   if (rc) return rc;
   // hits per 256-row group ~ H 256 / n: slots for 4x that (+8)
-  const double per_group = L.spec_hits * (double)L.group_rows / (double)n_rows;
+  const double per_group = spec_hits * (double)L.group_rows / (double)n_rows;
   int slots = 8;
   while (slots < 4.0 * per_group + 8.0 && slots < EBT_FILTER_SLOTS_MAX) slots *= 2;
   int64_t seg_cap = L.ld_cand / slots;
@@ -623,7 +647,7 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
     // theta_spec H / n; after r0 rows the raised threshold (the list's k-th - 2 eps) keeps at
     // most ~k' / r0 of the rows. A remainder of less than half a segment joins the last one.
     const double room = 0.4 * (cap - kprime);
-    double rate = L.spec_hits / (double)n_rows;
+    double rate = spec_hits / (double)n_rows;
     if (r0 > 0 && (double)kprime / (double)r0 < rate) rate = (double)kprime / (double)r0;
     int64_t seg = (int64_t)(room / (rate > 1e-12 ? rate : 1e-12));
     seg = (seg + 255) / 256 * 256;
@@ -655,6 +679,9 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
     if (rc) return rc;
     r0 += seg;
   }
+  // a caller's threshold is verified by the caller against the catalog-wide floor (the local
+  // list may hold fewer than k rows: most of the global top k live on other shards)
+  if (given) return EBT_OK;
   return spec_threshold(fv, kprime, B, B_pad, k, a.eps, tspec, nullptr, ovf, 1, st);
 }
 
@@ -831,6 +858,66 @@ int ebt_cosine_screen(const double* q64, const void* qimg, const float* qscale, 
   rc = run_screen(a, L, ws, list_vals, list_rows, timer, st, &so);
   if (rc) return rc;
   return export_list(list_rows, B, kprime, row_offset, so.ovf, so.eps, ovf_out, eps_out, st);
+}
+
+int ebt_cosine_screen_at(const double* q64, const void* qimg, const float* qscale,
+                         const float* eps, int64_t B, int64_t B_pad, const void* cat, int dtype,
+                         int64_t ld, const double* gnorm64, const void* cimg, const float* cscale,
+                         int img_dtype, int32_t ld_img, int64_t n_rows, int32_t d, int32_t d_pad,
+                         int64_t row_offset, const int64_t* excl_off, const int64_t* excl_rows,
+                         int32_t k, int32_t kprime, int64_t chunk_rows, int flags,
+                         void* workspace, size_t ws_bytes, float* list_vals, int64_t* list_rows,
+                         int32_t* ovf_out, float* eps_out, const float* theta, double hits,
+                         void* timer, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  flags |= EBT_FLAG_THETA;
+  PipeArgs a{q64, qimg, qscale, eps, B, B_pad, cat, dtype, ld, gnorm64, cimg, cscale,
+             img_dtype, ld_img, n_rows, d, d_pad, row_offset, excl_off, excl_rows, k, kprime,
+             chunk_rows, flags};
+  a.theta = theta;
+  a.hits = hits;
+  int rc = check_pipe(a, "ebt_cosine_screen_at");
+  if (rc) return rc;
+  if (!workspace || !list_vals || !list_rows || !ovf_out || !eps_out || !theta) {
+    set_error("ebt_cosine_screen_at: null pointer");
+    return EBT_EINVAL;
+  }
+  if ((flags & (EBT_FLAG_NO_FUSE | EBT_FLAG_EXACT)) || !merge_wave_fits(kprime) ||
+      !(hits >= 0.0)) {
+    set_error("ebt_cosine_screen_at: needs the fused screen with kprime <= 512 (kprime=%d, "
+              "flags=%d, hits=%g)", kprime, flags, hits);
+    return EBT_EINVAL;
+  }
+  const WsLayout L = ws_layout(B, B_pad, n_rows, kprime, chunk_rows, flags);
+  if (ws_bytes < L.bytes) {
+    set_error("ebt_cosine_screen_at: workspace %zu < %zu bytes", ws_bytes, L.bytes);
+    return EBT_ENOMEM;
+  }
+  char* ws = (char*)workspace;
+  ScreenOut so{};
+  rc = run_screen(a, L, ws, list_vals, list_rows, timer, st, &so);
+  if (rc) return rc;
+  return export_list(list_rows, B, kprime, row_offset, so.ovf, so.eps, ovf_out, eps_out, st);
+}
+
+int ebt_cosine_sample(const void* qimg, const float* qscale, int64_t B_pad, const void* cimg,
+                      const float* cscale, int img_dtype, int32_t ld_img, int64_t n_rows,
+                      int32_t d_pad, int64_t tiles, int64_t tile_stride, float* pooled,
+                      int64_t ld_pooled, void* timer, void* stream) {
+  if (tiles < 1 || tile_stride < 1 || (tiles - 1) * tile_stride * 256 + 256 > n_rows) {
+    set_error("ebt_cosine_sample: %lld tiles %lld apart do not fit %lld rows", (long long)tiles,
+              (long long)tile_stride, (long long)n_rows);
+    return EBT_EINVAL;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  StageScope s(timer, EBT_STAGE_GEMM, st);
+  return screen_gemm_pool(qimg, B_pad, cimg, 256 * tiles, d_pad, ld_img, img_dtype, qscale, cscale,
+                          256 * tile_stride, pooled, ld_pooled, st);
+}
+
+int ebt_pool_kth(const float* pooled, int64_t ld, int64_t B, int64_t B_pad, int32_t G, int32_t j,
+                 float* theta, void* stream) {
+  return pool_kth(pooled, ld, B, B_pad, G, j, theta, (hipStream_t)stream);
 }
 
 int ebt_rescore_owned(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,

@@ -201,9 +201,10 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
   if (tid == 0) {
     int ok = 1;
     if (nvalid >= kprime && n_rows > kprime) {  // kprime >= n_rows: every row is a candidate
-      const double T = (double)cv[k - 1];
+      // rows below the k'-th candidate have approx <= amin; none of them can enter the top k
+      // when amin < cut (the local k-th - 2 eps, or t_floor - eps when that is higher)
       const double amin = (double)cv[kprime - 1];
-      ok = amin < T - 2.0 * (double)eps[b];
+      ok = amin < cut;
     }
     if (ovf_cnt && ovf_cnt[b] > ovf_cap) ok = -1;  // fused screen dropped candidates
     if (corrupt) ok = -2;                           // internal error: row out of range

@@ -871,11 +871,14 @@ __global__ void spec_threshold_kernel(const float* __restrict__ vals, int64_t ld
     thr[b] = __builtin_inff();
   }
 }
-// theta_spec[b] = the j-th largest of query b's G <= 256 pooled sample maxima (one wave per
+// theta_spec[b] = the j-th largest of query b's G <= 2048 pooled sample maxima (one wave per
 // query; the largest key t with count(key >= t) >= j, by bisection with ballot counts). A 64-row
 // subgroup's max is >= x only if one of its rows is, so P(theta_spec > x) <= P(>= j sample rows
 // >= x): spec_params' Poisson bound holds for the pooled estimate too. Fewer than j valid maxima
-// -> -inf (keep everything: the merge overflows and the query is rerun unfused).
+// -> -inf (keep everything: the merge overflows and the query is rerun unfused). E = maxima per
+// lane (G <= 64 E): 4 for one shard's sample, up to 32 for the maxima of all shards
+// (ebt_pool_kth over the all-gathered samples of a row-sharded catalog).
+template <int E>
 __global__ __launch_bounds__(256) void pool_kth_kernel(const float* __restrict__ pool, int64_t ld,
                                                        int64_t B, int64_t B_pad, int G, int j,
                                                        float* __restrict__ thr) {
@@ -886,16 +889,16 @@ __global__ __launch_bounds__(256) void pool_kth_kernel(const float* __restrict__
     if (lane == 0) thr[b] = __builtin_inff();
     return;
   }
-  uint32_t kx[4];
+  uint32_t kx[E];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < E; ++e) {
     const int g = lane + 64 * e;
     kx[e] = g < G ? f2key(pool[b * ld + g]) : 0u;
   }
   auto count_ge = [&](uint32_t t) {
     int c = 0;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) c += __popcll(__ballot(kx[e] >= t));
+    for (int e = 0; e < E; ++e) c += __popcll(__ballot(kx[e] >= t));
     return c;
   };
   uint64_t lo = 1, hi = 0xffffffffull;  // largest t with count(key >= t) >= j
@@ -912,12 +915,15 @@ __global__ __launch_bounds__(256) void pool_kth_kernel(const float* __restrict__
 }
 int pool_kth(const float* pool, int64_t ld, int64_t B, int64_t B_pad, int G, int j, float* thr,
              hipStream_t st) {
-  if (G < 1 || G > 256 || j < 1 || ld < G) {
-    set_error("pool_kth: bad arguments (G=%d j=%d)", G, j);
+  if (!pool || !thr || B < 0 || B_pad < B || G < 1 || G > 2048 || j < 1 || ld < G) {
+    set_error("pool_kth: bad arguments (G=%d j=%d ld=%lld)", G, j, (long long)ld);
     return EBT_EINVAL;
   }
-  hipLaunchKernelGGL(pool_kth_kernel, dim3((unsigned)ceil_div(B_pad, 4)), dim3(256), 0, st, pool,
-                     ld, B, B_pad, G, j, thr);
+  const dim3 grid((unsigned)ceil_div(B_pad, 4)), block(256);
+  if (G <= 256)
+    hipLaunchKernelGGL(pool_kth_kernel<4>, grid, block, 0, st, pool, ld, B, B_pad, G, j, thr);
+  else
+    hipLaunchKernelGGL(pool_kth_kernel<32>, grid, block, 0, st, pool, ld, B, B_pad, G, j, thr);
   return launch_check("pool_kth_kernel");
 }
 

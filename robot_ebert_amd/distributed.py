@@ -34,8 +34,11 @@ from . import _lib
 from ._lib import EbertError, call, ptr, stream_of
 from .catalog import Catalog
 from .search import (KPRIME_MAX, _round_up, csr_from_lists, csr_subset, default_kprime,
-                     merge_topk, prepare_queries, run_screen, score_topk, score_topk_finish,
-                     score_topk_submit, union_floor)
+                     merge_topk, pad_batch, pool_kth, prepare_queries, run_screen,
+                     sample_maxima, score_topk, score_topk_finish, score_topk_submit, spec_rank,
+                     union_floor)
+
+SAMPLE_TILES_MAX = 64   # per shard, as the single-GPU speculative screen (api.hip spec_params)
 
 
 def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
@@ -193,6 +196,57 @@ def _gathered_floor(coll, vals: torch.Tensor, eps: torch.Tensor, k: int) -> torc
     return union_floor(g[:, :, :-1], g[:, :, -1], k)
 
 
+def shared_sample_tiles(n_global: int, world: int, B_pad: int) -> int:
+    """256-row sample tiles per shard for the shared screening threshold, 0 = not used. Depends
+    only on (n_global, world, B_pad), so every rank takes the same decision (the threshold's
+    all-gather is a collective). The single-GPU rule (api.hip spec_params: <= 64 tiles, <= 1/24
+    of the rows, whole rounds of 256 workgroups when that keeps >= 8) on the largest shard."""
+    if world < 2 or B_pad % 256 != 0:
+        return 0
+    full = -(-n_global // world) // 256
+    P = min(SAMPLE_TILES_MAX, full // 24)
+    per = max(1, 256 // (B_pad // 256))
+    if P // per * per >= 8:
+        P = P // per * per
+    return P if P >= 1 and world * P >= 8 else 0
+
+
+def _shared_theta(coll, catalog: Catalog, qb, kprime: int, tiles: int, timer=None):
+    """Catalog-wide screening threshold: every shard's sample maxima (ebt_cosine_sample), ONE
+    all-gather ([R, B, 4 tiles] f32), theta = the j-th largest of all R * 4 tiles maxima
+    (ebt_pool_kth), j from the Poisson bound of spec_params with the k'-th best of the WHOLE
+    catalog as the target. Each shard then keeps ~(its share of) k' j / lambda rows per query
+    instead of ~k' j / lambda of its own, and one filter launch covers it. Returns
+    (theta [B_pad], expected hits per query on this shard) or None (every rank alike)."""
+    g = coll.all_gather(local_sample(catalog, qb, tiles, timer))   # [R, B, 4 tiles]
+    return theta_from_samples(g, qb, kprime, tiles, catalog.n_global, catalog.n)
+
+
+def local_sample(catalog: Catalog, qb, tiles: int, timer=None) -> torch.Tensor:
+    """This shard's part of the shared threshold: [B, 4 tiles] f32 sample maxima (-inf where a
+    shard too small for `tiles` full tiles has none)."""
+    B, G = qb.B, 4 * tiles
+    pooled = torch.full((B, G), float("-inf"), dtype=torch.float32, device=catalog.device)
+    own = min(tiles, catalog.n // 256)
+    if own >= 1:
+        pooled[:, :4 * own] = sample_maxima(catalog, qb, own, timer)[:B]
+    return pooled
+
+
+def theta_from_samples(g: torch.Tensor, qb, kprime: int, tiles: int, n_global: int,
+                       n_local: int):
+    """(theta [B_pad], expected hits per query on an n_local-row shard) from the gathered
+    [R, B, 4 tiles] maxima, or None when the sample is too small to say anything."""
+    R, B, G = g.shape
+    m_total = 256 * tiles * R
+    j = spec_rank(kprime * m_total / max(n_global, 1))
+    if j > R * G // 2:
+        return None
+    theta = pool_kth(g.permute(1, 0, 2).reshape(B, R * G), B, qb.B_pad, j)
+    hits = (j + j * j / (2.0 * R * G)) * n_local / m_total
+    return theta, hits
+
+
 def score_topk_sharded_local(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
                              liked: Optional[Sequence[Sequence[int]]] = None,
                              exclude=None, group: Optional[dist.ProcessGroup] = None,
@@ -207,16 +261,24 @@ def score_topk_sharded_local_submit(catalog: Catalog, k: int,
                                     queries: Optional[torch.Tensor] = None,
                                     liked: Optional[Sequence[Sequence[int]]] = None,
                                     exclude=None, group: Optional[dist.ProcessGroup] = None,
-                                    collectives=None, **kw):
+                                    collectives=None, shared_threshold: bool = True, **kw):
     """Enqueue a batch of score_topk_sharded_local (its screen and the floor all-gather) and
     return without waiting; score_topk_sharded_local_finish completes it (retries, all-gather,
     merge). Every rank must submit and finish its batches in the same order: the collectives
-    are issued in program order, so ranks stay in lockstep."""
+    are issued in program order, so ranks stay in lockstep. shared_threshold: screen every
+    shard at one catalog-wide threshold (_shared_theta) when the batch allows it."""
     coll = collectives if collectives is not None else TorchCollectives(group)
     liked_arg = counts_t = hook = None
     if liked is not None:
         liked_arg, counts_t, hook = _liked_queries(catalog, liked, coll)
     kw.setdefault("t_floor_hook", lambda v, e: _gathered_floor(coll, v, e, k))
+    B = int(queries.shape[0]) if queries is not None else len(liked)
+    tiles = shared_sample_tiles(catalog.n_global, coll.world, pad_batch(B)) \
+        if shared_threshold and kw.get("fuse", True) else 0
+    if tiles:
+        timer = kw.get("timer")
+        kw.setdefault("theta_hook", lambda qb, kp: _shared_theta(coll, catalog, qb, kp, tiles,
+                                                                 timer))
     pending = score_topk_submit(catalog, k, queries=queries, liked=liked_arg, exclude=exclude,
                                 liked_counts=counts_t, liked_sum_hook=hook, **kw)
     return pending, coll, k

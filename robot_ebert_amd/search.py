@@ -29,6 +29,7 @@ from ._lib import DTYPE_CODE, EbertError, call, ptr, require_cuda, stream_of
 from .catalog import Catalog
 
 KPRIME_MAX = 4096
+MERGE_WAVE_KMAX = 512   # largest k' of the fused wave-merge screen (select_topk.hip WMERGE_K)
 DEFAULT_SCORE_BUDGET = int(os.environ.get("EBT_SCORE_BUDGET", str(4 << 30)))  # bytes of f32 scores
 
 
@@ -255,13 +256,75 @@ def run_screen(catalog: Catalog, qb: QueryBatch, k: int, kprime: int,
     return lv, lr, ovf, eps
 
 
+def spec_rank(lam: float, tail: float = 1e-6) -> int:
+    """The smallest j with P(Poisson(lam) >= j) <= tail (api.hip spec_params): the rank of the
+    sample maxima whose value exceeds the k'-th best catalog score with probability <= tail."""
+    import math
+    pmf, cdf, j = math.exp(-lam), 0.0, 0
+    while j < 100000 and 1.0 - cdf > tail:
+        cdf += pmf
+        pmf *= lam / (j + 1)
+        j += 1
+    return max(j, 1)
+
+
+def sample_maxima(catalog: Catalog, qb: QueryBatch, tiles: int,
+                  timer: Optional[_lib.Timer] = None) -> torch.Tensor:
+    """ebt_cosine_sample: `tiles` evenly spaced full 256-row tiles of this catalog (shard)
+    through the screening GEMM, keeping the max of every 64-row subgroup: [B_pad, 4 tiles] f32."""
+    stride = (catalog.n // 256) // tiles
+    out = torch.empty((qb.B_pad, 4 * tiles), dtype=torch.float32, device=catalog.device)
+    call("ebt_cosine_sample", ptr(qb.qimg), ptr(qb.qscale), qb.B_pad, ptr(catalog.image),
+         ptr(catalog.cscale), catalog.img_dtype, catalog.ld_img, catalog.n, catalog.d_pad, tiles,
+         stride, ptr(out), 4 * tiles, timer.handle if timer is not None else None,
+         stream_of(catalog.device))
+    return out
+
+
+def pool_kth(pooled: torch.Tensor, B: int, B_pad: int, j: int) -> torch.Tensor:
+    """ebt_pool_kth: theta[b] = the j-th largest of pooled[b, :] ([B, G] f32, G <= 2048);
+    +inf for the padding rows B <= b < B_pad."""
+    pooled = pooled.contiguous()
+    theta = torch.empty(B_pad, dtype=torch.float32, device=pooled.device)
+    call("ebt_pool_kth", ptr(pooled), pooled.shape[1], B, B_pad, pooled.shape[1], j, ptr(theta),
+         stream_of(pooled.device))
+    return theta
+
+
+def screen_at(catalog: Catalog, qb: QueryBatch, k: int, kprime: int, theta: torch.Tensor,
+              hits: float, exclude: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+              chunk_rows: Optional[int] = None, timer: Optional[_lib.Timer] = None):
+    """ebt_cosine_screen_at: run_screen at the caller's threshold theta [B_pad] f32 (see
+    include/ebert.h: the caller verifies theta against the catalog-wide floor)."""
+    dev = catalog.device
+    B, B_pad = qb.B, qb.B_pad
+    chunk = chunk_rows or _chunk_rows(catalog, B_pad, DEFAULT_SCORE_BUDGET)
+    need = _lib.load().ebt_cosine_topk_workspace(B, B_pad, catalog.n, kprime, chunk,
+                                                 _lib.EBT_FLAG_THETA)
+    if need == 0:
+        raise EbertError("invalid workspace request")
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    lv = torch.empty((B, kprime), dtype=torch.float32, device=dev)
+    lr = torch.empty((B, kprime), dtype=torch.int64, device=dev)
+    ovf = torch.empty(B, dtype=torch.int32, device=dev)
+    eps = torch.empty(B, dtype=torch.float32, device=dev)
+    eo, er = (exclude if exclude is not None else (None, None))
+    call("ebt_cosine_screen_at", ptr(qb.q64), ptr(qb.qimg), ptr(qb.qscale), ptr(qb.eps), B,
+         B_pad, ptr(catalog.data), catalog.dtype_code, catalog.ld, ptr(catalog.gnorm),
+         ptr(catalog.image), ptr(catalog.cscale), catalog.img_dtype, catalog.ld_img, catalog.n,
+         catalog.d, catalog.d_pad, catalog.row_offset, ptr(eo), ptr(er), k, kprime, chunk, 0,
+         ptr(ws), int(ws.numel()), ptr(lv), ptr(lr), ptr(ovf), ptr(eps), ptr(theta.contiguous()),
+         float(hits), timer.handle if timer is not None else None, stream_of(dev))
+    return lv, lr, ovf, eps
+
+
 def score_topk_submit(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
                liked: Optional[Union[Tuple[torch.Tensor, torch.Tensor], Sequence[Sequence[int]]]] = None,
                exclude: Optional[Union[Tuple[torch.Tensor, torch.Tensor], Sequence[Sequence[int]]]] = None,
                kprime: Optional[int] = None, chunk_rows: Optional[int] = None,
                timer: Optional[_lib.Timer] = None, liked_counts: Optional[torch.Tensor] = None,
                liked_sum_hook=None, fuse: bool = True,
-               t_floor_hook=None) -> "PendingTopk":
+               t_floor_hook=None, theta_hook=None) -> "PendingTopk":
     """Enqueue the first pass of score_topk (see there) on the catalog's device and return
     without waiting for it: score_topk_finish(pending) waits, retries the queries whose
     certificate needs it and returns (scores, rows). Submitting batch i+1 before finishing
@@ -281,6 +344,12 @@ def score_topk_submit(catalog: Catalog, k: int, queries: Optional[torch.Tensor] 
     t_floor); slots that cut empties read NaN / -1, which merge_topk sorts last. The hook runs
     exactly once per call on every shard (retries below are local, no collective), so shards
     cannot fall out of step.
+
+    theta_hook (with t_floor_hook): hook(qb, kprime) -> (theta f32 [B_pad], hits) or None, a
+    catalog-wide screening threshold (distributed.py: the all-gathered sample maxima of every
+    shard). Called exactly once per call, before the screen; when it returns a threshold and
+    the fused wave-merge screen applies (k' <= 512), the shard is screened at theta
+    (ebt_cosine_screen_at) and a query whose theta exceeds t_floor - eps is rerun unfused.
     """
     if k < 1:
         raise EbertError("k must be >= 1")
@@ -298,11 +367,13 @@ def score_topk_submit(catalog: Catalog, k: int, queries: Optional[torch.Tensor] 
     kp = kprime or default_kprime(catalog, k_eff)
     kp = max(_round_up(k_eff, 4), min(_round_up(kp, 4), n_cap, KPRIME_MAX))
     flags = 0 if fuse else _lib.EBT_FLAG_NO_FUSE
+    if theta_hook is not None and t_floor_hook is None:
+        raise EbertError("theta_hook needs t_floor_hook (the threshold is verified against it)")
     if t_floor_hook is None:
         s, r, cert = run_pipeline(catalog, qb, k_eff, kp, exclude, chunk_rows, timer, flags=flags)
     else:
         s, r, cert = _screen_global_cut(catalog, qb, k_eff, k, kp, exclude, chunk_rows, timer,
-                                        flags, t_floor_hook)
+                                        flags, t_floor_hook, theta_hook)
     # the certificates travel to pinned host memory right behind this batch's kernels, so
     # finishing it waits for this batch only, not for batches submitted after it
     cert_host = torch.empty(cert.shape, dtype=cert.dtype, pin_memory=True)
@@ -369,13 +440,14 @@ def score_topk(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
                kprime: Optional[int] = None, chunk_rows: Optional[int] = None,
                timer: Optional[_lib.Timer] = None, liked_counts: Optional[torch.Tensor] = None,
                liked_sum_hook=None, fuse: bool = True,
-               t_floor_hook=None) -> Tuple[torch.Tensor, torch.Tensor]:
+               t_floor_hook=None, theta_hook=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Top-k by cosine (mean cosine over liked rows) with exclusions: score_topk_submit +
     score_topk_finish (arguments and results as documented there)."""
     return score_topk_finish(score_topk_submit(
         catalog, k, queries=queries, liked=liked, exclude=exclude, kprime=kprime,
         chunk_rows=chunk_rows, timer=timer, liked_counts=liked_counts,
-        liked_sum_hook=liked_sum_hook, fuse=fuse, t_floor_hook=t_floor_hook))
+        liked_sum_hook=liked_sum_hook, fuse=fuse, t_floor_hook=t_floor_hook,
+        theta_hook=theta_hook))
 
 
 @dataclass
@@ -408,12 +480,19 @@ def union_floor(vals: torch.Tensor, eps: torch.Tensor, k: int) -> torch.Tensor:
 
 
 def _screen_global_cut(catalog: Catalog, qb: QueryBatch, k: int, k_req: int, kprime: int,
-                       exclude, chunk_rows, timer, flags, t_floor_hook):
-    """score_topk's first pass under a catalog-wide cut: screen, t_floor_hook, rescore. A shard
-    with fewer rows than the requested k_req pads its bounds with -inf."""
+                       exclude, chunk_rows, timer, flags, t_floor_hook, theta_hook=None):
+    """score_topk's first pass under a catalog-wide cut: [theta_hook,] screen, t_floor_hook,
+    rescore. A shard with fewer rows than the requested k_req pads its bounds with -inf."""
     dev = catalog.device
     B = qb.B
-    lv, lr, ovf, eps = run_screen(catalog, qb, k, kprime, exclude, chunk_rows, timer, flags)
+    # the hook is a collective: called on every shard whether or not this one uses its result
+    th = theta_hook(qb, kprime) if theta_hook is not None else None
+    use_theta = th is not None and flags == 0 and kprime <= MERGE_WAVE_KMAX
+    if use_theta:
+        lv, lr, ovf, eps = screen_at(catalog, qb, k, kprime, th[0], th[1], exclude, chunk_rows,
+                                     timer)
+    else:
+        lv, lr, ovf, eps = run_screen(catalog, qb, k, kprime, exclude, chunk_rows, timer, flags)
     vals = lv[:, :k]
     if k < k_req:
         vals = torch.cat([vals, torch.full((B, k_req - k), float("-inf"), device=dev)], 1)
@@ -428,8 +507,13 @@ def _screen_global_cut(catalog: Catalog, qb: QueryBatch, k: int, k_req: int, kpr
          catalog.ld, ptr(catalog.gnorm), catalog.row_offset, ptr(lv), ptr(local.contiguous()),
          kprime, k, catalog.n, ptr(eps), ptr(t_floor), ptr(out_s), ptr(out_r), ptr(cert),
          stream_of(dev))
-    # an overflowed fused list is rerun unfused (cert -1), unless a row is corrupt (-2)
-    cert = torch.where((ovf != 0) & (cert != -2), torch.full_like(cert, -1), cert)
+    # an overflowed fused list is rerun unfused (cert -1), unless a row is corrupt (-2); so is a
+    # query whose shared threshold may have dropped a row of the global top k: every top-k row
+    # has approx >= t_floor - eps, so theta <= t_floor - eps keeps them all
+    drop = ovf != 0
+    if use_theta:
+        drop |= ~(th[0][:B].double() <= t_floor - eps[:B].double())
+    cert = torch.where(drop & (cert != -2), torch.full_like(cert, -1), cert)
     return out_s, out_r, cert
 
 

@@ -216,3 +216,76 @@ def test_per_shard_global_cut_overflow_retry(cuda_device):
     s_ref, r_ref = R.cosine_topk(q, c, k)
     for s, r in res:
         assert_topk_equal(s, r, s_ref, r_ref)
+
+
+def _spy(monkeypatch, module, name, log):
+    orig = getattr(module, name)
+
+    def wrapper(*a, **kw):
+        log.append(kw.get("flags", a[8] if name == "run_pipeline" and len(a) > 8 else None))
+        return orig(*a, **kw)
+    monkeypatch.setattr(module, name, wrapper)
+
+
+@pytest.mark.parametrize("world,dt", [(2, "f32"), (4, "bf16")])
+def test_shared_threshold_matches_single(cuda_device, monkeypatch, world, dt):
+    """score_topk_sharded_local screens every shard at ONE catalog-wide threshold (the
+    all-gathered sample maxima of all shards, ebt_cosine_sample + ebt_pool_kth +
+    ebt_cosine_screen_at): the merged answer equals the single-GPU one and the oracle."""
+    import robot_ebert_amd as ebt
+    from robot_ebert_amd import search
+    from robot_ebert_amd.distributed import score_topk_sharded_local, shared_sample_tiles
+    from test_gpu_parity import _t, assert_topk_equal
+    n, d, B, k = 400_000, 128, 300, 50
+    assert shared_sample_tiles(n, world, search.pad_batch(B)) > 0
+    c = gaussian(71, n, d, dt)
+    q = gaussian(72, B, d, dt)
+    rng = np.random.default_rng(73)
+    excl = [sorted(rng.choice(n, 100, replace=False).tolist()) for _ in range(B)]
+    full = _t(c, dt, cuda_device)
+    qt = _t(q, dt, cuda_device)
+    calls = []
+    _spy(monkeypatch, search, "screen_at", calls)
+    res = _run_sharded(full, world, lambda r, cat, coll: score_topk_sharded_local(
+        cat, k, queries=qt, exclude=excl, collectives=coll))
+    assert len(calls) == world          # every shard screened at the shared threshold
+    single = ebt.score_topk(ebt.Catalog(full), k, queries=qt, exclude=excl)
+    for s, r in res:
+        assert torch.equal(r, single[1])
+        torch.testing.assert_close(s, single[0], rtol=0, atol=0)
+    sample = [0, 150, 299]
+    s_ref, r_ref = R.cosine_topk(q[sample].astype(np.float64), c.astype(np.float64), k,
+                                 [excl[i] for i in sample])
+    assert_topk_equal(res[0][0][sample], res[0][1][sample], s_ref, r_ref)
+
+
+def test_shared_threshold_too_high_reruns(cuda_device, monkeypatch):
+    """An adversarial catalog whose only high rows sit exactly in the sampled subgroups (20 of
+    them, k = 50): the shared threshold lands above the k-th score, every query fails the
+    theta <= t_floor - eps check and is rerun unfused on its shard; the answer stays exact."""
+    from robot_ebert_amd import search
+    from robot_ebert_amd.distributed import score_topk_sharded_local, shared_sample_tiles
+    from test_gpu_parity import _t, assert_topk_equal
+    n, d, B, k, world = 200_000, 64, 256, 50, 2
+    tiles = shared_sample_tiles(n, world, search.pad_batch(B))
+    assert tiles > 0
+    rng = np.random.default_rng(81)
+    q0 = rng.standard_normal(d)
+    c = rng.standard_normal((n, d))
+    stride = (n // world // 256) // tiles
+    boosted = [t * stride * 256 + 64 * s for t in range(5) for s in range(4)]   # shard 0
+    c[boosted] = q0[None, :] + 0.3 * rng.standard_normal((len(boosted), d))
+    q = q0[None, :] + 0.05 * rng.standard_normal((B, d))
+    full = _t(c, "f64", cuda_device)
+    qt = _t(q, "f64", cuda_device)
+    reruns = []
+    _spy(monkeypatch, search, "run_pipeline", reruns)
+    res = _run_sharded(full, world, lambda r, cat, coll: score_topk_sharded_local(
+        cat, k, queries=qt, collectives=coll))
+    assert reruns, "the too-high threshold was not caught"
+    sample = [0, 77, 255]
+    s_ref, r_ref = R.cosine_topk(q[sample], c, k)
+    for s, r in res:
+        assert_topk_equal(s[sample], r[sample], s_ref, r_ref)
+    s_all, r_all = R.cosine_topk(q, c, k)
+    assert np.array_equal(res[0][1].cpu().numpy(), r_all)

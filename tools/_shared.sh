@@ -1,0 +1,4 @@
+set -e
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -1 gpurun_out/gpu_tests.log
+cd tools && timeout -k 10 400 python shard_sim.py --one-rank --ranks 2 4 8 --steps 10 2>&1 | grep -v amdgpu.ids

@@ -51,9 +51,12 @@ def one_rank(args):
     dev = torch.device("cuda:0")
     q = bench.make_queries(cfg, dev)
     k = cfg["k"]
+    from robot_ebert_amd.distributed import (local_sample, shared_sample_tiles,
+                                             theta_from_samples)
     for R in args.ranks:
-        floors = []
+        floors, samples = [], []
         cat0 = None
+        tiles = shared_sample_tiles(cfg["n"], R, search.pad_batch(q.shape[0]))
         for r in range(R):
             a, b = shard_range(cfg["n"], r, R)
             cat = ebt.Catalog(bench.make_catalog_shard(cfg, a, b, dev), row_offset=a,
@@ -62,6 +65,8 @@ def one_rank(args):
             kp = search.default_kprime(cat, k)
             lv, _, _, eps = search.run_screen(cat, qb, k, kp)
             floors.append((lv[:, :k].clone(), eps[:qb.B].clone()))
+            if tiles:
+                samples.append(local_sample(cat, qb, tiles))
             if r == 0:
                 cat0, lv0, eps0 = cat, lv.double(), eps[:qb.B].double()
             else:
@@ -77,10 +82,22 @@ def one_rank(args):
                           "rescored_nocut": float((lv0 >= cut0[:, None]).sum(1).double().mean()),
                           "rescored_cut": float((lv0 >= cut1[:, None]).sum(1).double().mean())}),
               flush=True)
-        variants = (("cut", lambda v, e: t_glob.clone()), ("nocut", None))
+        variants = [("cut", lambda v, e: t_glob.clone(), None), ("nocut", None, None)]
+        if tiles:  # rank 0 screened at the catalog-wide threshold of all shards' samples
+            g = torch.stack(samples)
+            variants.insert(0, ("shared", lambda v, e: t_glob.clone(),
+                                lambda qb, kp: theta_from_samples(g, qb, kp, tiles, cfg["n"],
+                                                                  cat0.n)))
+            qb0 = search.prepare_queries(cat0, queries=q)
+            th, hits = theta_from_samples(g, qb0, search.default_kprime(cat0, k), tiles,
+                                          cfg["n"], cat0.n)
+            fails = int((th[:qb0.B].double() > t_glob - eps0).sum())
+            print(json.dumps({"ranks": R, "shared_tiles": tiles, "expected_hits": round(hits, 1),
+                              "theta_failures": fails}), flush=True)
         if args.only:
             variants = [v for v in variants if v[0] == args.only]
-        for name, hook in variants:
+        ref = None
+        for name, hook, th_hook in variants:
             pending = None  # pipelined as bench.py does: submit step i+1, then finish step i
             for i in range(args.steps + 1):
                 if i == 1:
@@ -88,7 +105,8 @@ def one_rank(args):
                     pending = None
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
-                p = search.score_topk_submit(cat0, k, queries=q, t_floor_hook=hook)
+                p = search.score_topk_submit(cat0, k, queries=q, t_floor_hook=hook,
+                                             theta_hook=th_hook)
                 if pending is not None:
                     search.score_topk_finish(pending)
                 pending = p
@@ -96,9 +114,18 @@ def one_rank(args):
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) * 1e3 / args.steps
             tm = ebt.Timer()
-            search.score_topk(cat0, k, queries=q, t_floor_hook=hook, timer=tm)
+            s_, r_ = search.score_topk(cat0, k, queries=q, t_floor_hook=hook, theta_hook=th_hook,
+                                       timer=tm)
             torch.cuda.synchronize()
+            same = None
+            if name == "shared" or ref is not None:
+                if ref is None:
+                    ref = (s_, r_)
+                else:
+                    same = bool(torch.equal(r_, ref[1]) and torch.allclose(s_, ref[0], rtol=0, atol=0,
+                                                                           equal_nan=True))
             print(json.dumps({"ranks": R, "path": "one_rank_" + name, "ms_per_step": round(ms, 3),
+                              "same_as_shared": same,
                               "stages_ms": {kk: round(tm.query(kk)[0], 3) for kk in _lib.STAGES}}),
                   flush=True)
         del cat0
@@ -112,7 +139,7 @@ def main():
     ap.add_argument("--one-rank", action="store_true",
                     help="time rank 0's own work alone (the floor all-reduce replaced by its "
                          "precomputed result) with and without the global cut")
-    ap.add_argument("--only", default=None, choices=["cut", "nocut"],
+    ap.add_argument("--only", default=None, choices=["shared", "cut", "nocut"],
                     help="--one-rank: time only this variant (profiling)")
     args = ap.parse_args()
     if args.one_rank:
