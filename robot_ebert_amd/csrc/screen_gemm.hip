@@ -21,6 +21,7 @@
 // groups of 8 (128-kernel) / 4 (256-kernel) catalog tiles walked query-tile-major, so a catalog
 // tile is fetched from HBM about once per XCD and re-read from L2 by the query tiles that use it.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -166,7 +167,16 @@ __device__ __forceinline__ void epilogue4(const EpiArgs& e, int64_t q, int64_t i
 // queries q0 .. q0 + nq - 1), after every wave's epilogue.
 __device__ __forceinline__ void filter_finish(const EpiArgs& e, const uint32_t* lcnt, int64_t q0,
                                               int nq, int64_t grp) {
+  // LDS-only barrier: the counters are LDS atomics, the hits are read by a later kernel, so
+  // the waves need not wait for their hit stores here (__syncthreads() adds vmcnt(0); measured
+  // no difference either way on MI355X -- the hit path's cost is its instructions)
+#if EBT_ABL_SYNCFIN
   __syncthreads();
+#else
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#endif
   for (int t = threadIdx.x; t < nq; t += blockDim.x) {
     const uint32_t c = lcnt[t];
     const int64_t q = q0 + t;
@@ -648,17 +658,23 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
 
   // ---- epilogue: quadrant (ah, bh) = catalog half ah x query half bh ----
   const bool full = c0 + QP_TILE <= n_rows;  // uniform
-  // Filter mode, register-resident: the epilogue constants of this lane (query scale
-  // and threshold per (bh, j), row scales per (ah, i)) are read from LDS ONCE; the hit path then
-  // runs on registers only. Per (bh, j) each lane builds the bit mask of its hits among its 32
-  // values of query ql (2 catalog halves x 4 accumulators x 4 rows), the 4 lanes of the query
-  // (lane ^ 16, ^ 32) take exclusive prefixes of their counts, the 4 slot claims of the wave
-  // (one LDS atomic per query) are issued together, and each lane writes its hits. The earlier
-  // per-hit form (LDS reads + a returned-value atomic per hit, all dependent) cost ~5 us per
-  // tile at ~40 hits per wave.
-  auto filter_tile = [&]() {
+  // Filter mode. Each lane holds 4 query columns (bh, j) x 32 catalog rows (2 halves x 4
+  // accumulators x 4 rows); a block is one accumulator (4 consecutive rows of one query).
+  //   1. column test (every tile): the max of each column's 32 values against the query's
+  //      threshold -- 4 compares per lane, no per-block branches. SIMPLE (no row scales, a full
+  //      tile): max_r fl(a_r qs) = fl(max_r(a_r) qs) for qs >= 0 (rounding is monotone), so the
+  //      scale is applied once per column; NaNs drop out of fmaxf as they do out of >=.
+  //   2. only if some lane of the wave passed: block bits m (bit c*8 + ah*4 + i) for the flagged
+  //      columns.
+  //   3. the lane's flagged blocks go to its 8 LDS slots in the dead K-tile ring (rounds of 8
+  //      when a lane has more; only the wave's flagged columns are visited), and a ROLLED loop over the lane's own blocks computes the exact
+  //      values, claims slots with one LDS atomic per block and writes the hits: the work
+  //      follows the lane's hits, not the union of the wave's blocks (the earlier form executed
+  //      every block any lane had flagged: ~600 VALU per wave with 2 hits, ~1500 with 60).
+  // Every wave passed the last tile's final barrier after its last LDS read of the ring.
+  auto filter_tile = [&](auto simple_tag) {
+    constexpr bool SIMPLE = decltype(simple_tag)::value;
     float qs_r[2][2], th_r[2][2];
-    float4 cs_r[2][4];
 #pragma unroll
     for (int bh = 0; bh < 2; ++bh)
 #pragma unroll
@@ -667,15 +683,22 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
         qs_r[bh][j] = lqs[ql];
         th_r[bh][j] = lth[ql];
       }
-#pragma unroll
-    for (int ah = 0; ah < 2; ++ah)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        cs_r[ah][i] = *(const float4*)(lcs + ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4));
     // quadrant q = (ah, bh): acc0 (0, 0), acc1 (0, 1), acc2 (1, 1), acc3 (1, 0)
     auto acc_of = [&](int ah, int bh) -> const f32x4_t (&)[4][2] {
       return ah == 0 ? (bh == 0 ? acc0 : acc1) : (bh == 0 ? acc3 : acc2);
     };
+    // row scales, register-resident (read from LDS once; 1 without scales)
+    float4 cs_r[2][4];
+    if constexpr (!SIMPLE) {
+#pragma unroll
+      for (int ah = 0; ah < 2; ++ah)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          cs_r[ah][i] = *(const float4*)(lcs + ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4));
+    }
+    // the exact epilogue values of block (ah, bh, i, j). Rows past n_rows are NOT masked here
+    // (they read 0 through the buffer descriptor): the block bits are a superset, the exact
+    // per-row test in the hit loop drops them.
     auto val4 = [&](int ah, int bh, int i, int j, float (&v)[4]) {
       const f32x4_t& a = acc_of(ah, bh)[i][j];
       const float qs = qs_r[bh][j];
@@ -685,108 +708,111 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
       v[2] = a[2] * qs * cs.z;
       v[3] = a[3] * qs * cs.w;
     };
-    // all-miss test: bit (4 (2 bh + j) ... ) -> m bit (bh * 2 + j) * 8 + ah * 4 + i
+    auto max4 = [](float a, float b, float c, float d) { return fmaxf(fmaxf(a, b), fmaxf(c, d)); };
     uint32_t m = 0;
+    if constexpr (SIMPLE) {
+      uint32_t colm = 0;
 #pragma unroll
-    for (int bh = 0; bh < 2; ++bh)
+      for (int bh = 0; bh < 2; ++bh)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j) {
+          float mx = -__builtin_inff();
+#pragma unroll
+          for (int ah = 0; ah < 2; ++ah)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const f32x4_t& a = acc_of(ah, bh)[i][j];
+              mx = fmaxf(mx, max4(a[0], a[1], a[2], a[3]));
+            }
+          colm |= (mx * qs_r[bh][j] >= th_r[bh][j] ? 1u : 0u) << (bh * 2 + j);
+        }
+      if (__builtin_expect(__ballot(colm != 0u) == 0ull, 1)) return;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int bh = c >> 1, j = c & 1;
+        if (__ballot((colm >> c) & 1u) == 0ull) continue;
 #pragma unroll
         for (int ah = 0; ah < 2; ++ah)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            float mx;
-            if (cscale || !full) {
-              float v[4];
-              val4(ah, bh, i, j, v);
-              if (!full) {  // the catalog's last tile: rows past n_rows never hit
-                const int64_t i0 = c0 + ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                  if (i0 + r >= n_rows) v[r] = -__builtin_inff();
-              }
-              mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
-            } else {
-              // max_r fl(a_r qs) = fl(max_r(a_r) qs) for qs >= 0 (rounding is monotone); NaNs
-              // drop out of fmaxf as they do out of >=
-              const f32x4_t& a = acc_of(ah, bh)[i][j];
-              mx = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])) * qs_r[bh][j];
-            }
-            m |= (mx >= th_r[bh][j] ? 1u : 0u) << ((bh * 2 + j) * 8 + ah * 4 + i);
+            const f32x4_t& a = acc_of(ah, bh)[i][j];
+            const float mx = max4(a[0], a[1], a[2], a[3]) * qs_r[bh][j];
+            m |= (mx >= th_r[bh][j] ? 1u : 0u) << (c * 8 + ah * 4 + i);
           }
-    if (__builtin_expect(__ballot(m != 0u) == 0ull, 1)) return;
-    uint32_t hm[4];
-    int xs[4], cnt[4], tot[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int bh = c >> 1, j = c & 1;
-      uint32_t h = 0;
-#pragma unroll
-      for (int ah = 0; ah < 2; ++ah)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (m & (1u << (c * 8 + ah * 4 + i))) {
-            float v[4];
-            val4(ah, bh, i, j, v);
-            const int64_t i0 = c0 + ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              h |= (v[r] >= th_r[bh][j] && (full || i0 + r < n_rows) ? 1u : 0u)
-                   << (ah * 16 + i * 4 + r);
-          }
-        }
-      hm[c] = h;
-      cnt[c] = __popc(h);
-      int x = cnt[c];  // inclusive prefix over lanes fr, fr + 16, fr + 32, fr + 48
-      int y = __shfl_up(x, 16, 64);
-      if (lane >= 16) x += y;
-      y = __shfl_up(x, 32, 64);
-      if (lane >= 32) x += y;
-      xs[c] = x;
-      tot[c] = __shfl(x, 48 + fr, 64);
-    }
-    uint32_t base[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int ql = (c >> 1) * 128 + wb * 32 + (c & 1) * 16 + fr;
-      base[c] = (lane < 16 && tot[c] > 0) ? atomicAdd(lcnt + ql, (uint32_t)tot[c]) : 0u;
-    }
-    // the writes: per (bh, j) with hits in the wave, the lane's 32 values go to its staging
-    // slots in the (dead) K-tile ring -- every wave passed the last tile's final barrier after
-    // its last LDS read of the ring -- as 8 float4 planes, and a ROLLED loop over the set bits
-    // reads them back. (Fully unrolled per-bit code made the kernel ~84 KB: the hit path then
-    // ran from instruction-cache misses, ~2x the cost of the hits themselves.)
-    float4* stg = (float4*)(smem + wave * 8192);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int bh = c >> 1, j = c & 1;
-      if (__ballot(hm[c] != 0u) == 0ull) continue;
-#pragma unroll
-      for (int ah = 0; ah < 2; ++ah)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float v[4];
-          val4(ah, bh, i, j, v);
-          stg[(ah * 4 + i) * 64 + lane] = make_float4(v[0], v[1], v[2], v[3]);
-        }
-      const int ql = bh * 128 + wb * 32 + j * 16 + fr;
-      uint32_t p = (uint32_t)__shfl((int)base[c], fr, 64) + (uint32_t)(xs[c] - cnt[c]);
-      uint64_t* dst = e.cand + (q0 + ql) * e.ld_cand + ct * e.slots;
-      const float* sf = (const float*)stg;
-      uint32_t h = hm[c];
-#pragma unroll 1
-      while (h) {
-        const int bit = __builtin_ctz(h);
-        h &= h - 1u;
-        if (p < (uint32_t)e.slots) {
-          const float v = sf[((bit >> 2) * 64 + lane) * 4 + (bit & 3)];
-          const int il = (bit >> 4) * 128 + wa * 64 + ((bit >> 2) & 3) * 16 + 4 * (lane >> 4) +
-                         (bit & 3);
-          const uint32_t row = (uint32_t)(e.idx_base + c0 + il);
-          dst[p] = ((uint64_t)f2key(v) << 32) | (uint64_t)(~row);
-        }
-        ++p;
       }
+    } else {
+      // row scales or a partial tile: the block bits directly (each block's values are used
+      // at once; a column pass first would keep all 128 values live and spill)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int ah = 0; ah < 2; ++ah)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float v[4];
+            val4(ah, c >> 1, i, c & 1, v);
+            m |= (max4(v[0], v[1], v[2], v[3]) >= th_r[c >> 1][c & 1] ? 1u : 0u)
+                 << (c * 8 + ah * 4 + i);
+          }
+      if (__builtin_expect(__ballot(m != 0u) == 0ull, 1)) return;
+    }
+    char* stg = smem + wave * 8192 + lane * 128;  // this lane's 8 slots of 16 B
+    // columns with a flagged block in some lane of the wave (uniform): only their 8 blocks are
+    // visited when staging
+    uint32_t cols = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      cols |= (__ballot(((m >> (8 * c)) & 0xffu) != 0u) != 0ull ? 1u : 0u) << c;
+    const int nblk = __popc(m);
+    uint32_t rest = m;
+#pragma unroll 1
+    for (int round = 0;; ++round) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (!((cols >> c) & 1u)) continue;
+#pragma unroll
+        for (int ah = 0; ah < 2; ++ah)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int g = c * 8 + ah * 4 + i;
+            const int rank = __popc(m & ((1u << g) - 1u));
+            if (((m >> g) & 1u) && (rank >> 3) == round)
+              *(f32x4_t*)(stg + (rank & 7) * 16) = acc_of(ah, c >> 1)[i][c & 1];
+          }
+      }
+#pragma unroll 1
+      for (int s2 = 0; s2 < 8; ++s2) {
+        if (__ballot(rest != 0u) == 0ull) break;
+        if (rest != 0u && (nblk - __popc(rest)) >> 3 == round) {
+          const int g = __builtin_ctz(rest);
+          rest &= rest - 1u;
+          const f32x4_t a = *(const f32x4_t*)(stg + s2 * 16);
+          const int c = g >> 3, ah = (g >> 2) & 1, i = g & 3;
+          const int ql = (c >> 1) * 128 + wb * 32 + (c & 1) * 16 + fr;
+          const int il = ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
+          const float qs = lqs[ql], th = lth[ql];
+          const float4 cs = *(const float4*)(lcs + il);
+          const float v[4] = {a[0] * qs * cs.x, a[1] * qs * cs.y, a[2] * qs * cs.z,
+                              a[3] * qs * cs.w};
+          uint32_t hb = 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            hb |= (v[r] >= th && (full || c0 + il + r < n_rows) ? 1u : 0u) << r;
+          if (hb) {
+            const uint32_t base = atomicAdd(lcnt + ql, (uint32_t)__popc(hb));
+            uint64_t* dst = e.cand + (q0 + ql) * e.ld_cand + ct * e.slots;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const uint32_t p = base + (uint32_t)__popc(hb & ((1u << r) - 1u));
+              if (((hb >> r) & 1u) && p < (uint32_t)e.slots) {
+                const uint32_t row = (uint32_t)(e.idx_base + c0 + il + r);
+                dst[p] = ((uint64_t)f2key(v[r]) << 32) | (uint64_t)(~row);
+              }
+            }
+          }
+        }
+      }
+      if (__ballot(nblk > 8 * (round + 1)) == 0ull) break;
     }
   };
   auto store_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh) {
@@ -846,7 +872,8 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     pool_quadrant(acc2, 1, 1);
     pool_quadrant(acc3, 1, 0);
   } else if constexpr (FILTER) {
-    filter_tile();
+    if (!cscale && full) filter_tile(std::true_type{});
+    else filter_tile(std::false_type{});
   } else {
     store_quadrant(acc0, 0, 0);
     store_quadrant(acc1, 0, 1);
