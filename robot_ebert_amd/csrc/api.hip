@@ -63,6 +63,7 @@ int merge_segment(float*, int64_t*, int64_t, int, const uint64_t*, int64_t, int,
                   int64_t, int64_t, int64_t, const int64_t*, const int64_t*, int*, hipStream_t);
 bool merge_wave_fits(int);
 int merge_wave_capacity();
+int merge_block_capacity(int);
 int64_t merge_wave_max_groups();
 int merge_segment_wave(float*, int64_t*, int64_t, int, int, const uint64_t*, int64_t, int,
                        const uint8_t*, int64_t, int64_t, int64_t, const int64_t*, const int64_t*,
@@ -157,6 +158,8 @@ struct WsLayout {
       off_thr, off_ovf, off_eps, off_tspec, bytes;
 };
 
+constexpr int SPEC_KPRIME_MAX = 2048;
+
 // Speculative screen parameters (see run_screen). The sample: P evenly spaced full 256-row tiles
 // (P = min(64, tiles / 24), so at most ~4 % of the rows are screened twice); lambda = the expected
 // number of sample rows at or above the rank-k' score, taking the sample as a uniform draw of
@@ -169,7 +172,8 @@ static bool spec_params(int64_t B_pad, int64_t n_rows, int32_t kprime, int64_t* 
     const char* v = getenv("EBT_SPEC");
     return v ? atoi(v) : 1;
   }();
-  if (!enabled || B_pad % 256 != 0 || !merge_wave_fits(kprime)) return false;
+  // k' <= 512: one wave per query merges the hits; up to 2048: the block merge
+  if (!enabled || B_pad % 256 != 0 || kprime > SPEC_KPRIME_MAX) return false;
   const int64_t full = n_rows / 256;
   int64_t P = full / 24;
   P = P > 64 ? 64 : P;
@@ -235,13 +239,19 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
     // hit slots: up to 1 GiB of u64 per call, never more than the whole tail at the minimum of
     // 16 slots per group (plus the pilot segment's few groups at up to 128 slots)
     L.group_rows = filter_group_rows(B_pad);
-    const int64_t budget = (1LL << 30) / (B_pad * 8);
+    // 1 GiB at B_pad <= 4096, growing with the batch up to 8 GiB (C5: 16384 queries): larger
+    // segments, fewer merges
+    int64_t bytes = B_pad * (512LL << 10);
+    bytes = bytes < (1LL << 30) ? (1LL << 30) : (bytes > (8LL << 30) ? (8LL << 30) : bytes);
+    if (B_pad <= 4096) bytes = 1LL << 30;
+    const int64_t budget = bytes / (B_pad * 8);
     const int64_t need = ceil_div(n_rows - (L.spec ? 0 : H), L.group_rows) * 16 +
                          8 * EBT_FILTER_SLOTS_MAX;
     L.ld_cand = budget < need ? budget : need;
     L.ld_cand = L.ld_cand < 8 * EBT_FILTER_SLOTS_MAX ? 8 * EBT_FILTER_SLOTS_MAX : L.ld_cand;
     L.seg_max = L.ld_cand / 16 * L.group_rows;
-    L.ld_counts = (L.ld_cand / 16 + 15) / 16 * 16;
+    // the speculative screen may use 8 slots per group: counts for ld_cand / 8 groups
+    L.ld_counts = (L.ld_cand / 8 + 15) / 16 * 16;
   }
   L.chunk = chunk_rows < L.head ? chunk_rows : L.head;
   if (L.spec) L.chunk = L.head / 64;  // the sample's pooled maxima (4 per tile)
@@ -632,14 +642,16 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
   if (!rc) rc = hip_check(hipMemsetAsync(fi, 0xff, (size_t)B * kprime * 8, st), "hipMemsetAsync");
   if (!rc) rc = hip_check(hipMemsetAsync(ovf, 0, (size_t)B_pad * 4, st), "hipMemsetAsync");
   if (rc) return rc;
-  // hits per 256-row group ~ H 256 / n: slots for 4x that (+8)
+  // hits per 256-row group ~ H 256 / n: slots for 4x that (+4; a group overflow only costs
+  // its query an unfused rerun)
   const double per_group = spec_hits * (double)L.group_rows / (double)n_rows;
   int slots = 8;
-  while (slots < 4.0 * per_group + 8.0 && slots < EBT_FILTER_SLOTS_MAX) slots *= 2;
+  while (slots < 4.0 * per_group + 4.0 && slots < EBT_FILTER_SLOTS_MAX) slots *= 2;
+  const bool wave = merge_wave_fits(kprime);
   int64_t seg_cap = L.ld_cand / slots;
-  seg_cap = seg_cap < merge_wave_max_groups() ? seg_cap : merge_wave_max_groups();
+  if (wave) seg_cap = seg_cap < merge_wave_max_groups() ? seg_cap : merge_wave_max_groups();
   seg_cap *= L.group_rows;
-  const double cap = (double)merge_wave_capacity();
+  const double cap = (double)(wave ? merge_wave_capacity() : merge_block_capacity(kprime));
   int64_t r0 = 0;
   while (r0 < n_rows) {
     // expected hits <= 0.4 of the merge's room beside the list (the hit count has a relative
@@ -672,9 +684,14 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
     if (rc) return rc;
     {
       StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
-      rc = merge_segment_wave(fv, fi, B, kprime, k, cand, L.ld_cand, slots, counts, L.ld_counts,
-                              ceil_div(seg, L.group_rows), a.row_offset, a.excl_off, a.excl_rows,
-                              ovf, st);
+      if (wave)
+        rc = merge_segment_wave(fv, fi, B, kprime, k, cand, L.ld_cand, slots, counts,
+                                L.ld_counts, ceil_div(seg, L.group_rows), a.row_offset,
+                                a.excl_off, a.excl_rows, ovf, st);
+      else  // sorted lists (the block merge sorts the union)
+        rc = merge_segment(fv, fi, B, kprime, cand, L.ld_cand, slots, counts, L.ld_counts,
+                           ceil_div(seg, L.group_rows), a.row_offset, a.excl_off, a.excl_rows,
+                           ovf, st);
     }
     if (rc) return rc;
     r0 += seg;

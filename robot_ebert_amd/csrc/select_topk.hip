@@ -772,6 +772,8 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
 }
 
 bool merge_wave_fits(int kprime) { return kprime <= WMERGE_K; }
+// entries the block merge holds (list + hits) for this k'
+int merge_block_capacity(int kprime) { return merge_entries(kprime); }
 int64_t merge_wave_max_groups() { return 64 * 16 * WCNT; }
 int merge_wave_capacity() { return WTOP_N; }
 

@@ -154,8 +154,11 @@ def prepare_queries(catalog: Catalog, queries: Optional[torch.Tensor] = None,
 
 
 def default_kprime(catalog: Catalog, k: int) -> int:
-    """Screening width: native images have a tiny error bound, f16 images need more slack."""
-    kp = k + 16 if catalog.native else max(2 * k, k + 32)
+    """Screening width: native images have a tiny error bound, f16 images need more slack.
+    The rows inside the 2 eps band around the k-th score grow with k (Gaussian tail: about
+    2 eps k z sqrt(d) of them, z ~ 4): at C5 (k = 1000, d = 1536, native f16) ~55, so the
+    native slack is k / 4, at least 16."""
+    kp = k + max(16, k // 4) if catalog.native else max(2 * k, k + 32)
     return min(_round_up(kp, 8), KPRIME_MAX)
 
 

@@ -450,11 +450,13 @@ def test_fused_screen_equals_unfused_and_oracle(cuda_device, dt):
     assert_topk_equal(s1[sample], r1[sample], s_ref, r_ref)
 
 
-def test_fused_large_kprime_block_path(cuda_device):
-    """k' > 512 (C5's k = 1000 class) takes the 256 k'-row head + block-level merges: equal to
-    the unfused path and to the oracle on sampled queries, with exclusions."""
+@pytest.mark.parametrize("B", [100, 300])
+def test_fused_large_kprime_block_path(cuda_device, B):
+    """k' > 512 (C5's k = 1000 class) with block-level merges: B = 100 (B_pad 128, no sample)
+    takes the 256 k'-row head; B = 300 the speculative screen (sample threshold). Both equal
+    the unfused path and the oracle on sampled queries, with exclusions."""
     ebt, L = _ebt()
-    n, d, B, k = 400_000, 128, 130, 600
+    n, d, k = 400_000, 128, 600
     c = gaussian(4, n, d, "f16")
     q = gaussian(5, B, d, "f16")
     rng = np.random.default_rng(6)
@@ -462,14 +464,18 @@ def test_fused_large_kprime_block_path(cuda_device):
     cat = ebt.Catalog(_t(c, "f16", cuda_device))
     qt = _t(q, "f16", cuda_device)
     pl = ebt.search.plan(cat, B, k)
-    assert pl["fused"] and pl["kprime"] > 512 and pl["head_rows"] >= 256 * pl["kprime"]
+    assert pl["fused"] and pl["kprime"] > 512
+    if B <= 128:
+        assert pl["spec"] is None and pl["head_rows"] >= 256 * pl["kprime"], pl
+    else:
+        assert pl["spec"] is not None, pl
     timer = ebt.Timer()
     s1, r1 = ebt.score_topk(cat, k, queries=qt, exclude=[list(e) for e in excl], timer=timer)
     assert timer.query("gemm_filter")[1] >= 1, "fused path not taken"
     s2, r2 = ebt.score_topk(cat, k, queries=qt, exclude=[list(e) for e in excl], fuse=False)
     assert torch.equal(r1, r2)
     torch.testing.assert_close(s1, s2, rtol=0, atol=0)
-    sample = [0, 64, 129]
+    sample = [0, 64, B - 1]
     s_ref, r_ref = R.cosine_topk(q[sample].astype(np.float64), c.astype(np.float64), k,
                                  [excl[i] for i in sample])
     assert_topk_equal(s1[sample], r1[sample], s_ref, r_ref)
