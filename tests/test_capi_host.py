@@ -154,3 +154,32 @@ def test_spec_plan_poisson_rank():
     assert sp(4096, 1_000_000, 2052)[0] == 0        # k' > 2048: no spec
     assert sp(4096, 20_000, 200)[0] == 0            # too few tiles for a sample
     assert sp(4096, 1_000_000, 200, _lib.EBT_FLAG_NO_FUSE)[0] == 0
+
+
+def test_shared_threshold_plan():
+    """The row-sharded path's shared threshold: spec_rank (Python) is the C rank rule, the
+    sample size depends only on (n_global, world, B_pad) -- every rank takes the same decision
+    before the all-gather -- and small batches / single ranks do not use it."""
+    import ctypes
+    from robot_ebert_amd import _lib
+    from robot_ebert_amd.distributed import shard_range, shared_sample_tiles
+    from robot_ebert_amd.search import spec_rank
+    lib = _lib.load()
+    for (n, kp) in [(1_000_000, 200), (125_000, 200), (6_250_000, 1256)]:
+        t, s, h = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double()
+        j = ctypes.c_int32()
+        assert lib.ebt_cosine_topk_spec_plan(4096, 4096, n, kp, 0, ctypes.byref(t),
+                                             ctypes.byref(s), ctypes.byref(j),
+                                             ctypes.byref(h)) == 0
+        assert spec_rank(kp * 256 * t.value / n) == j.value
+    assert shared_sample_tiles(1_000_000, 8, 4096) == 16
+    assert shared_sample_tiles(1_000_000, 2, 4096) == 64
+    assert shared_sample_tiles(1_000_000, 1, 4096) == 0      # one rank: its own sample
+    assert shared_sample_tiles(1_000_000, 8, 128) == 0       # B_pad 128: no pool epilogue
+    assert shared_sample_tiles(20_000, 8, 4096) == 0         # shards too small to sample
+    # every shard of shard_range holds the sample's tiles (stride >= 1)
+    for world in (2, 3, 8):
+        P = shared_sample_tiles(1_000_003, world, 4096)
+        for r in range(world):
+            a, b = shard_range(1_000_003, r, world)
+            assert (b - a) // 256 >= P
