@@ -39,6 +39,10 @@ from .search import (KPRIME_MAX, _round_up, csr_from_lists, csr_subset, default_
                      union_floor)
 
 SAMPLE_TILES_MAX = 64   # per shard, as the single-GPU speculative screen (api.hip spec_params)
+# Larger shards screen at their own sample threshold: there the shard's first segment raises
+# its threshold (list k-th - 2 eps) soon enough, and the shared threshold's uniform hits cost
+# as much as they save (tools/shard_sim.py at C3: 2 ranks +2.5 %, 4 ranks +-0, 8 ranks -3 %).
+SHARED_MAX_SHARD_ROWS = 200_000
 
 
 def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
@@ -201,7 +205,7 @@ def shared_sample_tiles(n_global: int, world: int, B_pad: int) -> int:
     only on (n_global, world, B_pad), so every rank takes the same decision (the threshold's
     all-gather is a collective). The single-GPU rule (api.hip spec_params: <= 64 tiles, <= 1/24
     of the rows, whole rounds of 256 workgroups when that keeps >= 8) on the largest shard."""
-    if world < 2 or B_pad % 256 != 0:
+    if world < 2 or B_pad % 256 != 0 or -(-n_global // world) > SHARED_MAX_SHARD_ROWS:
         return 0
     full = -(-n_global // world) // 256
     P = min(SAMPLE_TILES_MAX, full // 24)
