@@ -322,6 +322,8 @@ int ebt_finalize_topk(const float* cand_vals, const int64_t* cand_rows, const do
 void* ebt_timer_create(void);
 void ebt_timer_destroy(void* timer);
 int ebt_timer_reset(void* timer);
+/* Record only the stages whose bit (1 << EBT_STAGE_*) is set (default: all). */
+int ebt_timer_set_mask(void* timer, uint32_t stage_mask);
 int ebt_timer_query(void* timer, int stage, double* total_ms, int64_t* launches);
 
 #ifdef __cplusplus

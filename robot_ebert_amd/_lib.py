@@ -84,6 +84,7 @@ _SIGNATURES = {
     "ebt_timer_create": ([], _VP),
     "ebt_timer_destroy": ([_VP], None),
     "ebt_timer_reset": ([_VP], _INT),
+    "ebt_timer_set_mask": ([_VP, ctypes.c_uint32], _INT),
     "ebt_timer_query": ([_VP, _INT, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64)], _INT),
 }
 
@@ -150,6 +151,11 @@ class Timer:
 
     def reset(self) -> None:
         call("ebt_timer_reset", self._h)
+
+    def only(self, *stages: str) -> None:
+        """Record only these stages from now on (all of them when none are given)."""
+        mask = 0xffffffff if not stages else sum(1 << STAGES[s] for s in stages)
+        call("ebt_timer_set_mask", self._h, mask)
 
     def query(self, stage: str):
         tot = ctypes.c_double(0.0)

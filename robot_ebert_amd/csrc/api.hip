@@ -103,6 +103,7 @@ struct Timer {
   size_t used = 0;
   std::vector<Rec> recs;
   std::mutex mu;
+  uint32_t mask = 0xffffffffu;  // stages recorded (ebt_timer_set_mask)
 
   hipEvent_t get() {
     if (used == pool.size()) {
@@ -123,6 +124,8 @@ struct StageScope {
   hipStream_t st;
   hipEvent_t a = nullptr, b = nullptr;
   StageScope(void* timer, int s, hipStream_t stream) : t((Timer*)timer), stage(s), st(stream) {
+    // an unrecorded stage adds no event (each recorded pair costs the stream ~5 us of gaps)
+    if (t && !((t->mask >> s) & 1u)) t = nullptr;
     if (t) {
       std::lock_guard<std::mutex> g(t->mu);
       a = t->get();
@@ -956,6 +959,14 @@ int ebt_finalize_topk(const float* cand_vals, const int64_t* cand_rows, const do
 void* ebt_timer_create(void) { return new (std::nothrow) Timer(); }
 
 void ebt_timer_destroy(void* timer) { delete (Timer*)timer; }
+
+int ebt_timer_set_mask(void* timer, uint32_t stage_mask) {
+  if (!timer) return EBT_EINVAL;
+  Timer* t = (Timer*)timer;
+  std::lock_guard<std::mutex> g(t->mu);
+  t->mask = stage_mask;
+  return EBT_OK;
+}
 
 int ebt_timer_reset(void* timer) {
   if (!timer) return EBT_EINVAL;
