@@ -66,6 +66,16 @@ __device__ __forceinline__ float key2f(uint32_t k) {
   return __uint_as_float(u);
 }
 
+// Workgroup barrier for LDS traffic only. __syncthreads() also waits for the wave's outstanding
+// GLOBAL loads (its release fence is s_waitcnt vmcnt(0)), which empties a register prefetch
+// pipeline at every barrier; LDS ops complete in order, so lgkmcnt(0) + s_barrier suffices when
+// the barrier protects LDS only.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // ---- wave reductions -----------------------------------------------------------------------
 __device__ __forceinline__ double wave_sum_f64(double v) {
 #pragma unroll

@@ -38,6 +38,8 @@ struct SelLayout {
 
 __host__ __device__ inline SelLayout sel_layout(int kprime) {
   SelLayout L;
+  // two tiles of room: with one, every tile that admits anything past k' forces a compaction
+  // (measured 1.7x slower on 1M-entry rows)
   L.cap = kprime + 2 * STILE;
   L.kpp = next_pow2(kprime);
   L.off_key = 0;
@@ -64,12 +66,12 @@ __device__ __forceinline__ void block_minmax_u64(uint64_t& mn, uint64_t& mx, uin
     mx = b > mx ? b : mx;
   }
   const int w = threadIdx.x >> 6;
-  __syncthreads();
+  lds_barrier();
   if ((threadIdx.x & 63) == 0) {
     red[w] = mn;
     red[4 + w] = mx;
   }
-  __syncthreads();
+  lds_barrier();
   mn = red[0];
   mx = red[4];
 #pragma unroll
@@ -101,12 +103,12 @@ __device__ uint64_t select_rank(const uint32_t* bkey, const uint32_t* bidx, int 
     const int shift = bits > 11 ? bits - 11 : 0;
 #pragma unroll
     for (int j = 0; j < SHIST / STHREADS; ++j) hist[tid * (SHIST / STHREADS) + j] = 0;
-    __syncthreads();
+    lds_barrier();
     for (int i = tid; i < n; i += STHREADS) {
       const uint64_t c = comp_of(bkey[i], bidx[i]);
       if (c >= mn && c <= mx) atomicAdd(&hist[(uint32_t)((c - mn) >> shift)], 1u);
     }
-    __syncthreads();
+    lds_barrier();
     // suffix scan: thread t owns bins [8t, 8t+8)
     uint32_t hv[SHIST / STHREADS];
     uint32_t s = 0;
@@ -124,7 +126,7 @@ __device__ uint64_t select_rank(const uint32_t* bkey, const uint32_t* bidx, int 
     }
     uint32_t* wtot = misc + 8;
     if (lane == 0) wtot[tid >> 6] = x;
-    __syncthreads();
+    lds_barrier();
     uint32_t above = x - s;
     for (int w2 = (tid >> 6) + 1; w2 < 4; ++w2) above += wtot[w2];
     if (above < (uint32_t)r && (uint32_t)r <= above + s) {
@@ -138,10 +140,10 @@ __device__ uint64_t select_rank(const uint32_t* bkey, const uint32_t* bidx, int 
         cum += hv[j];
       }
     }
-    __syncthreads();
+    lds_barrier();
     const uint32_t b = misc[0];
     r -= (int)misc[1];
-    __syncthreads();  // misc reused next iteration
+    lds_barrier();  // misc reused next iteration
     lo = mn + ((uint64_t)b << shift);
     const uint64_t w = (shift >= 64) ? ~0ull : ((1ull << shift) - 1);
     hi = (mx - lo) < w ? mx : lo + w;
@@ -157,7 +159,7 @@ __device__ uint64_t compact(uint32_t* bkey, uint32_t* bidx, int n, int rank, uin
   const uint64_t theta = select_rank(bkey, bidx, n, rank, hist, red, misc);
   const int tid = threadIdx.x, lane = tid & 63;
   if (tid == 0) misc[2] = 0;
-  __syncthreads();  // hist (aliased with keep) is dead from here
+  lds_barrier();  // hist (aliased with keep) is dead from here
   for (int base = 0; base < n; base += STHREADS) {
     const int i = base + tid;
     uint64_t c = 0;
@@ -177,13 +179,13 @@ __device__ uint64_t compact(uint32_t* bkey, uint32_t* bidx, int n, int rank, uin
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   for (int i = tid; i < rank; i += STHREADS) {
     const uint64_t c = keep[i];
     bkey[i] = (uint32_t)(c >> 32);
     bidx[i] = ~(uint32_t)c;
   }
-  __syncthreads();
+  lds_barrier();
   return theta;
 }
 
@@ -202,7 +204,7 @@ __device__ void bitonic_desc(uint64_t* keep, int P) {
           keep[hi] = a;
         }
       }
-      __syncthreads();
+      lds_barrier();
     }
   }
 }
@@ -231,10 +233,18 @@ __global__ __launch_bounds__(STHREADS, 2) void select_topk_kernel(
   const int64_t* irow = HAS_IDX ? idxs + row * ld : nullptr;
 
   if (tid == 0) misc[3] = 0;  // nbuf counter
-  __syncthreads();
+  lds_barrier();
   uint32_t thr = 1;
   int nbuf = 0;
+  // float form of "key >= thr" for the per-tile fast test: keys up to f2key(-FLT_MAX) admit
+  // every finite value (-inf and NaN have key 0); above that key2f(thr) is a float (or a NaN
+  // that admits nothing, as no float has such a key)
+  auto thr_f = [](uint32_t t) {
+    return t <= 0x00800000u ? -3.402823466e38f : key2f(t);
+  };
+  float tf = thr_f(thr);
 
+  // one tile in flight (a second one, 32 KiB per workgroup, measured 20 % slower)
   float cur[SE], nxt[SE];
   int64_t curi[SE], nxti[SE];
   auto load_tile = [&](int64_t t0, float* v, int64_t* ix) {
@@ -280,10 +290,18 @@ __global__ __launch_bounds__(STHREADS, 2) void select_topk_kernel(
       nbuf = kprime;
       const uint32_t tau = (uint32_t)(theta >> 32);
       thr = HAS_IDX ? tau : tau + 1u;
+      tf = thr_f(thr);
       if (tid == 0) misc[3] = (uint32_t)nbuf;
-      __syncthreads();
+      lds_barrier();
     }
     if (t + 1 < ntiles) load_tile(t0 + STILE, nxt, nxti);
+    // fast test: once the threshold has risen, almost no tile has a value to admit; the wave
+    // then skips the per-value ballots (a superset test: entries past the segment read -inf,
+    // excluded (idx < 0) ones are dropped below)
+    bool any = false;
+#pragma unroll
+    for (int e = 0; e < SE; ++e) any |= cur[e] >= tf;
+    if (__ballot(any) != 0ull)
 #pragma unroll
     for (int e = 0; e < SE; ++e) {
       const int64_t p = t0 + (e >> 2) * (STHREADS * 4) + tid * 4 + (e & 3);
@@ -308,7 +326,7 @@ __global__ __launch_bounds__(STHREADS, 2) void select_topk_kernel(
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     nbuf = (int)misc[3];
     if (t + 1 < ntiles) {
 #pragma unroll
@@ -327,7 +345,7 @@ __global__ __launch_bounds__(STHREADS, 2) void select_topk_kernel(
   }
   const int P = Lo.kpp;
   for (int i = tid; i < P; i += STHREADS) keep[i] = i < nk ? comp_of(bkey[i], bidx[i]) : 0ull;
-  __syncthreads();
+  lds_barrier();
   bitonic_desc(keep, P);
   float* ov = out_vals + row * ld_out + (int64_t)seg * kprime;
   int64_t* oi = out_idx + row * ld_out + (int64_t)seg * kprime;
