@@ -170,8 +170,8 @@ def main() -> None:
     dev = torch.device("cuda", local_rank)
 
     import robot_ebert_amd as ebt
-    from robot_ebert_amd.distributed import (score_topk_sharded_local_finish,
-                                             score_topk_sharded_local_submit, shard_range)
+    from robot_ebert_amd.distributed import (run_sharded_steps, score_topk_sharded_local_stages,
+                                             shard_range)
     ebt.load()
 
     begin, end = shard_range(cfg["n"], rank, world)
@@ -186,17 +186,19 @@ def main() -> None:
     # A step is submitted (all of its kernels and collectives enqueued) before the previous
     # step is finished (its certificates checked on the host, retries run): the GPU never waits
     # for the host between batches. Every step is a complete batch through the whole path.
+    # N > 1: per-shard exact top-k with the shared threshold and the floor cut, all-gather,
+    # merge; two batches in flight so that each collective runs under the other batch's kernels
+    # (distributed.run_sharded_steps).
     def submit():
-        if world > 1:  # per-shard exact top-k, one RCCL all-gather, merge
-            return score_topk_sharded_local_submit(cat, k, queries=q, timer=timer)
         return ebt.score_topk_submit(cat, k, queries=q, timer=timer)
 
     def finish(p):
-        if world > 1:
-            return score_topk_sharded_local_finish(p)
         return ebt.score_topk_finish(p)
 
     def run_steps(n, log_every=0):
+        if world > 1:
+            return run_sharded_steps(
+                lambda: score_topk_sharded_local_stages(cat, k, queries=q, timer=timer), n)
         pending, out = None, None
         for i in range(n):
             p = submit()

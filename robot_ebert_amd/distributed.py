@@ -35,8 +35,8 @@ from ._lib import EbertError, call, ptr, stream_of
 from .catalog import Catalog
 from .search import (KPRIME_MAX, _round_up, csr_from_lists, csr_subset, default_kprime,
                      merge_topk, pad_batch, pool_kth, prepare_queries, run_screen,
-                     sample_maxima, score_topk, score_topk_finish, score_topk_submit, spec_rank,
-                     union_floor)
+                     sample_maxima, score_topk, score_topk_finish, score_topk_stages,
+                     score_topk_submit, spec_rank, union_floor)
 
 SAMPLE_TILES_MAX = 64   # per shard, as the single-GPU speculative screen (api.hip spec_params)
 # Larger shards screen at their own sample threshold: there the shard's first segment raises
@@ -86,6 +86,22 @@ class TorchCollectives:
                           device=t.device)
         dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
         return out.view((self.world,) + tuple(t.shape))
+
+    def all_gather_start(self, t: torch.Tensor):
+        """Start an all-gather without making the stream wait for it; the returned callable
+        makes the CURRENT stream wait (work.wait()) and returns the [R, ...] result. Kernels
+        enqueued in between run while the collective is in flight."""
+        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
+                          device=t.device)
+        src = t.contiguous()
+        work = dist.all_gather_into_tensor(out, src, group=self.group, async_op=True)
+        shape = (self.world,) + tuple(t.shape)
+
+        def wait():
+            work.wait()
+            _ = src  # keep the source alive until the collective has finished
+            return out.view(shape)
+        return wait
 
     def all_reduce_sum(self, t: torch.Tensor) -> torch.Tensor:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
@@ -194,10 +210,23 @@ def score_topk_sharded(catalog: Catalog, k: int, queries: Optional[torch.Tensor]
     return s, r
 
 
-def _gathered_floor(coll, vals: torch.Tensor, eps: torch.Tensor, k: int) -> torch.Tensor:
-    """union_floor over every shard's (k best approx, eps), in ONE all-gather ([B, k+1] f32)."""
-    g = coll.all_gather(torch.cat([vals, eps[:, None]], 1))
-    return union_floor(g[:, :, :-1], g[:, :, -1], k)
+def _gather_start(coll, t: torch.Tensor):
+    """coll.all_gather_start when the collectives offer it, else a completed all-gather."""
+    if hasattr(coll, "all_gather_start"):
+        return coll.all_gather_start(t)
+    g = coll.all_gather(t)
+    return lambda: g
+
+
+def _gathered_floor(coll, vals: torch.Tensor, eps: torch.Tensor, k: int):
+    """union_floor over every shard's (k best approx, eps), in ONE all-gather ([B, k+1] f32);
+    returns a future (the gather runs while the caller enqueues other work)."""
+    wait = _gather_start(coll, torch.cat([vals, eps[:, None]], 1))
+
+    def floor():
+        g = wait()
+        return union_floor(g[:, :, :-1], g[:, :, -1], k)
+    return floor
 
 
 def shared_sample_tiles(n_global: int, world: int, B_pad: int) -> int:
@@ -220,10 +249,10 @@ def _shared_theta(coll, catalog: Catalog, qb, kprime: int, tiles: int, timer=Non
     all-gather ([R, B, 4 tiles] f32), theta = the j-th largest of all R * 4 tiles maxima
     (ebt_pool_kth), j from the Poisson bound of spec_params with the k'-th best of the WHOLE
     catalog as the target. Each shard then keeps ~(its share of) k' j / lambda rows per query
-    instead of ~k' j / lambda of its own, and one filter launch covers it. Returns
+    instead of ~k' j / lambda of its own, and one filter launch covers it. Returns a future of
     (theta [B_pad], expected hits per query on this shard) or None (every rank alike)."""
-    g = coll.all_gather(local_sample(catalog, qb, tiles, timer))   # [R, B, 4 tiles]
-    return theta_from_samples(g, qb, kprime, tiles, catalog.n_global, catalog.n)
+    wait = _gather_start(coll, local_sample(catalog, qb, tiles, timer))   # [R, B, 4 tiles]
+    return lambda: theta_from_samples(wait(), qb, kprime, tiles, catalog.n_global, catalog.n)
 
 
 def local_sample(catalog: Catalog, qb, tiles: int, timer=None) -> torch.Tensor:
@@ -271,6 +300,24 @@ def score_topk_sharded_local_submit(catalog: Catalog, k: int,
     merge). Every rank must submit and finish its batches in the same order: the collectives
     are issued in program order, so ranks stay in lockstep. shared_threshold: screen every
     shard at one catalog-wide threshold (_shared_theta) when the batch allows it."""
+    g = score_topk_sharded_local_stages(catalog, k, queries=queries, liked=liked,
+                                        exclude=exclude, group=group, collectives=collectives,
+                                        shared_threshold=shared_threshold, **kw)
+    next(g)
+    next(g)
+    return next(g)
+
+
+def score_topk_sharded_local_stages(catalog: Catalog, k: int,
+                                    queries: Optional[torch.Tensor] = None,
+                                    liked: Optional[Sequence[Sequence[int]]] = None,
+                                    exclude=None, group: Optional[dist.ProcessGroup] = None,
+                                    collectives=None, shared_threshold: bool = True, **kw):
+    """score_topk_sharded_local_submit in the three stages of search.score_topk_stages; every
+    stage ends by STARTING a collective (shared threshold, floor) that the next stage waits
+    for. Interleaving two batches -- stage 1 of batch i+1 before stage 3 of batch i, which runs
+    before stage 2 of batch i+1 (run_sharded_steps) -- runs each collective under the other
+    batch's kernels. The last next() returns the pending batch."""
     coll = collectives if collectives is not None else TorchCollectives(group)
     liked_arg = counts_t = hook = None
     if liked is not None:
@@ -283,12 +330,52 @@ def score_topk_sharded_local_submit(catalog: Catalog, k: int,
         timer = kw.get("timer")
         kw.setdefault("theta_hook", lambda qb, kp: _shared_theta(coll, catalog, qb, kp, tiles,
                                                                  timer))
-    pending = score_topk_submit(catalog, k, queries=queries, liked=liked_arg, exclude=exclude,
-                                liked_counts=counts_t, liked_sum_hook=hook, **kw)
-    return pending, coll, k
+    g = score_topk_stages(catalog, k, queries=queries, liked=liked_arg, exclude=exclude,
+                          liked_counts=counts_t, liked_sum_hook=hook, **kw)
+    next(g)
+    yield
+    next(g)
+    yield
+    yield next(g), coll, k
 
 
 def score_topk_sharded_local_finish(sub) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Complete a submitted batch: its retries (local), the all-gather of the per-shard exact
+    top-k and the merge."""
+    return score_topk_sharded_local_finish_start(sub)()
+
+
+def score_topk_sharded_local_finish_start(sub):
+    """score_topk_sharded_local_finish up to STARTING the all-gather of the results; the
+    returned callable waits for it and merges (the stream then waits for the gather only from
+    that point)."""
     pending, coll, k = sub
     s, r = score_topk_finish(pending)
-    return merge_topk(coll.all_gather(s), coll.all_gather(r), k)
+    ws, wr = _gather_start(coll, s), _gather_start(coll, r)
+    return lambda: merge_topk(ws(), wr(), k)
+
+
+def run_sharded_steps(make_stages, n: int):
+    """Drive n batches through score_topk_sharded_local_stages, two in flight: per step
+    [stage 1 of i] [stage 3 of i-1] [stage 2 of i] [finish of i-1 up to its gather]
+    [merge of i-2]. make_stages() returns a fresh generator; returns the last batch's
+    (scores, rows)."""
+    if n < 1:
+        return None
+    prev = make_stages()
+    next(prev)
+    next(prev)
+    merge_prev, out = None, None
+    for _ in range(1, n):
+        cur = make_stages()
+        next(cur)                      # stage 1 of i: its threshold gather starts
+        sub = next(prev)               # stage 3 of i-1: rescore (its floor gathered meanwhile)
+        next(cur)                      # stage 2 of i: screen; its floor gather starts
+        merge = score_topk_sharded_local_finish_start(sub)
+        if merge_prev is not None:
+            out = merge_prev()
+        merge_prev, prev = merge, cur
+    merge = score_topk_sharded_local_finish_start(next(prev))
+    if merge_prev is not None:
+        merge_prev()
+    return merge()

@@ -348,12 +348,37 @@ def score_topk_submit(catalog: Catalog, k: int, queries: Optional[torch.Tensor] 
     exactly once per call on every shard (retries below are local, no collective), so shards
     cannot fall out of step.
 
+    Either hook may return a callable instead (a future: its collective was started
+    asynchronously); it is called when the value is needed -- the next stage of
+    score_topk_stages.
+
     theta_hook (with t_floor_hook): hook(qb, kprime) -> (theta f32 [B_pad], hits) or None, a
     catalog-wide screening threshold (distributed.py: the all-gathered sample maxima of every
     shard). Called exactly once per call, before the screen; when it returns a threshold and
     the fused wave-merge screen applies (k' <= 512), the shard is screened at theta
     (ebt_cosine_screen_at) and a query whose theta exceeds t_floor - eps is rerun unfused.
     """
+    g = score_topk_stages(catalog, k, queries=queries, liked=liked, exclude=exclude,
+                          kprime=kprime, chunk_rows=chunk_rows, timer=timer,
+                          liked_counts=liked_counts, liked_sum_hook=liked_sum_hook, fuse=fuse,
+                          t_floor_hook=t_floor_hook, theta_hook=theta_hook)
+    next(g)
+    next(g)
+    return next(g)
+
+
+def score_topk_stages(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
+                      liked=None, exclude=None, kprime: Optional[int] = None,
+                      chunk_rows: Optional[int] = None, timer: Optional[_lib.Timer] = None,
+                      liked_counts: Optional[torch.Tensor] = None, liked_sum_hook=None,
+                      fuse: bool = True, t_floor_hook=None, theta_hook=None):
+    """score_topk_submit as a generator of three stages, so a caller can interleave the stages
+    of consecutive batches (distributed.py: each stage of a row-sharded batch ends in a
+    collective, and the next stage of the OTHER batch runs while it is in flight):
+      next() #1: query prep and theta_hook (the shared threshold's all-gather);
+      next() #2: the screen and t_floor_hook (the floor's all-gather);
+      next() #3: the rescore; returns the PendingTopk (score_topk_finish completes it).
+    Without t_floor_hook the whole first pass runs in stage 2."""
     if k < 1:
         raise EbertError("k must be >= 1")
     dev = catalog.device
@@ -361,6 +386,8 @@ def score_topk_submit(catalog: Catalog, k: int, queries: Optional[torch.Tensor] 
         liked = csr_from_lists(liked, dev)
     if exclude is not None and not isinstance(exclude, tuple):
         exclude = csr_from_lists(exclude, dev)
+    if theta_hook is not None and t_floor_hook is None:
+        raise EbertError("theta_hook needs t_floor_hook (the threshold is verified against it)")
     qb = prepare_queries(catalog, queries=queries, liked=liked, liked_counts=liked_counts,
                          liked_sum_hook=liked_sum_hook)
     n_cap = _round_up(catalog.n, 4)
@@ -370,21 +397,26 @@ def score_topk_submit(catalog: Catalog, k: int, queries: Optional[torch.Tensor] 
     kp = kprime or default_kprime(catalog, k_eff)
     kp = max(_round_up(k_eff, 4), min(_round_up(kp, 4), n_cap, KPRIME_MAX))
     flags = 0 if fuse else _lib.EBT_FLAG_NO_FUSE
-    if theta_hook is not None and t_floor_hook is None:
-        raise EbertError("theta_hook needs t_floor_hook (the threshold is verified against it)")
     if t_floor_hook is None:
+        yield
         s, r, cert = run_pipeline(catalog, qb, k_eff, kp, exclude, chunk_rows, timer, flags=flags)
+        yield
     else:
-        s, r, cert = _screen_global_cut(catalog, qb, k_eff, k, kp, exclude, chunk_rows, timer,
-                                        flags, t_floor_hook, theta_hook)
+        cut = _global_cut_stages(catalog, qb, k_eff, k, kp, exclude, chunk_rows, timer, flags,
+                                 t_floor_hook, theta_hook)
+        next(cut)
+        yield
+        next(cut)
+        yield
+        s, r, cert = next(cut)
     # the certificates travel to pinned host memory right behind this batch's kernels, so
     # finishing it waits for this batch only, not for batches submitted after it
     cert_host = torch.empty(cert.shape, dtype=cert.dtype, pin_memory=True)
     cert_host.copy_(cert, non_blocking=True)
     ready = torch.cuda.Event()
     ready.record(torch.cuda.current_stream(dev))
-    return PendingTopk(catalog, qb, k, k_eff, kp, exclude, chunk_rows, timer, flags, n_cap,
-                       s, r, cert, cert_host, ready)
+    yield PendingTopk(catalog, qb, k, k_eff, kp, exclude, chunk_rows, timer, flags, n_cap,
+                      s, r, cert, cert_host, ready)
 
 
 def score_topk_finish(p: "PendingTopk") -> Tuple[torch.Tensor, torch.Tensor]:
@@ -486,10 +518,24 @@ def _screen_global_cut(catalog: Catalog, qb: QueryBatch, k: int, k_req: int, kpr
                        exclude, chunk_rows, timer, flags, t_floor_hook, theta_hook=None):
     """score_topk's first pass under a catalog-wide cut: [theta_hook,] screen, t_floor_hook,
     rescore. A shard with fewer rows than the requested k_req pads its bounds with -inf."""
+    g = _global_cut_stages(catalog, qb, k, k_req, kprime, exclude, chunk_rows, timer, flags,
+                           t_floor_hook, theta_hook)
+    next(g)
+    next(g)
+    return next(g)
+
+
+def _global_cut_stages(catalog: Catalog, qb: QueryBatch, k: int, k_req: int, kprime: int,
+                       exclude, chunk_rows, timer, flags, t_floor_hook, theta_hook=None):
+    """_screen_global_cut as a generator: yields after the theta hook and after the floor hook,
+    then yields (scores, rows, cert)."""
     dev = catalog.device
     B = qb.B
     # the hook is a collective: called on every shard whether or not this one uses its result
     th = theta_hook(qb, kprime) if theta_hook is not None else None
+    yield
+    if callable(th):  # a future: the hook's collective was started, its result is needed now
+        th = th()
     use_theta = th is not None and flags == 0 and kprime <= MERGE_WAVE_KMAX
     if use_theta:
         lv, lr, ovf, eps = screen_at(catalog, qb, k, kprime, th[0], th[1], exclude, chunk_rows,
@@ -499,7 +545,11 @@ def _screen_global_cut(catalog: Catalog, qb: QueryBatch, k: int, k_req: int, kpr
     vals = lv[:, :k]
     if k < k_req:
         vals = torch.cat([vals, torch.full((B, k_req - k), float("-inf"), device=dev)], 1)
-    t_floor = t_floor_hook(vals.contiguous(), eps[:B].contiguous()).contiguous()
+    t_floor = t_floor_hook(vals.contiguous(), eps[:B].contiguous())
+    yield
+    if callable(t_floor):
+        t_floor = t_floor()
+    t_floor = t_floor.contiguous()
     if t_floor.dtype != torch.float64 or t_floor.shape != (B,):
         raise EbertError("t_floor_hook must return float64 [B]")
     local = lr - catalog.row_offset if catalog.row_offset else lr
@@ -517,7 +567,7 @@ def _screen_global_cut(catalog: Catalog, qb: QueryBatch, k: int, k_req: int, kpr
     if use_theta:
         drop |= ~(th[0][:B].double() <= t_floor - eps[:B].double())
     cert = torch.where(drop & (cert != -2), torch.full_like(cert, -1), cert)
-    return out_s, out_r, cert
+    yield out_s, out_r, cert
 
 
 def merge_topk(scores: torch.Tensor, rows: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:

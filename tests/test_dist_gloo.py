@@ -74,6 +74,15 @@ def _body(rank, world, q):
         ok = ok and bool((coll.all_reduce_sum(t) == sum(range(1, world + 1))).all())
         m = torch.tensor([rank, 1 - rank], dtype=torch.int32)
         ok = ok and coll.all_reduce_max(m).tolist() == [world - 1, 1]
+        # asynchronous all-gathers (the staged per-shard path): started in program order on
+        # every rank, completed later, in any order
+        w1 = coll.all_gather_start(torch.full((2, 3), float(rank)))
+        w2 = coll.all_gather_start(torch.full((4,), 10.0 + rank))
+        g2, g1 = w2(), w1()
+        ok = ok and g1.shape == (world, 2, 3) and all(bool((g1[r] == r).all())
+                                                       for r in range(world))
+        ok = ok and g2.shape == (world, 4) and all(bool((g2[r] == 10 + r).all())
+                                                    for r in range(world))
         # the per-shard path's global cut: union_floor of the gathered (approx, eps) lists is a
         # lower bound of the global k-th exact score, and no shard cuts a global top-k row
         from robot_ebert_amd.search import union_floor

@@ -289,3 +289,82 @@ def test_shared_threshold_too_high_reruns(cuda_device, monkeypatch):
         assert_topk_equal(s[sample], r[sample], s_ref, r_ref)
     s_all, r_all = R.cosine_topk(q, c, k)
     assert np.array_equal(res[0][1].cpu().numpy(), r_all)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_staged_two_in_flight_matches_single(cuda_device, world):
+    """run_sharded_steps (bench.py's N > 1 loop): batches interleaved stage by stage, two in
+    flight, every collective started in stage order on every rank; each batch's merged answer
+    equals the single-GPU one. Different queries per batch catch any mix-up between batches."""
+    import robot_ebert_amd as ebt
+    from robot_ebert_amd.distributed import run_sharded_steps, score_topk_sharded_local_stages
+    from test_gpu_parity import _t
+    n, d, B, k, steps = 240_000, 128, 300, 50, 4
+    c = gaussian(91, n, d, "f32")
+    qs = [gaussian(92 + i, B, d, "f32") for i in range(steps)]
+    full = _t(c, "f32", cuda_device)
+    qts = [_t(q, "f32", cuda_device) for q in qs]
+
+    def body(r, cat, coll):
+        it = iter(range(steps))
+        seen = []
+
+        def make():
+            i = next(it)
+            seen.append(i)
+            return score_topk_sharded_local_stages(cat, k, queries=qts[i], collectives=coll)
+        outs = []
+        # capture every batch's result: drive run_sharded_steps over 1..steps batches
+        for m in range(1, steps + 1):
+            it = iter(range(m))
+            outs.append(run_sharded_steps(make, m))
+        return outs
+    res = _run_sharded(full, world, body)
+    cat = ebt.Catalog(full)
+    for m in range(1, steps + 1):
+        s_ref, r_ref = ebt.score_topk(cat, k, queries=qts[m - 1])
+        for r in range(world):
+            s, rr = res[r][m - 1]
+            assert torch.equal(rr, r_ref)
+            torch.testing.assert_close(s, s_ref, rtol=0, atol=0)
+
+
+def test_rccl_world1_staged_path(cuda_device):
+    """The real torch.distributed calls of bench.py's N > 1 loop over RCCL ("nccl"), on a
+    one-rank group (the only group one GPU allows): async all-gathers with deferred waits
+    (TorchCollectives.all_gather_start), the floor hook, an explicit shared-threshold hook and
+    the staged two-in-flight driver; the answers equal the single-GPU path."""
+    import socket
+    import torch.distributed as dist
+    import robot_ebert_amd as ebt
+    from robot_ebert_amd.distributed import (TorchCollectives, _shared_theta, run_sharded_steps,
+                                             score_topk_sharded_local_stages, shared_sample_tiles)
+    from test_gpu_parity import _t
+    n, d, B, k = 150_000, 128, 300, 50
+    c = gaussian(101, n, d, "f32")
+    qs = [_t(gaussian(102 + i, B, d, "f32"), "f32", cuda_device) for i in range(3)]
+    cat = ebt.Catalog(_t(c, "f32", cuda_device))
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                            world_size=1, device_id=cuda_device)
+    try:
+        coll = TorchCollectives()
+        tiles = shared_sample_tiles(n * 2, 2, 512)   # a sample size the 2-rank layout would use
+        assert tiles > 0
+        it = iter(range(3))
+
+        def make():
+            i = next(it)
+            return score_topk_sharded_local_stages(
+                cat, k, queries=qs[i], collectives=coll,
+                theta_hook=lambda qb, kp: _shared_theta(coll, cat, qb, kp, tiles))
+        s, r = run_sharded_steps(make, 3)
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    s_ref, r_ref = ebt.score_topk(cat, k, queries=qs[2])
+    assert torch.equal(r, r_ref)
+    torch.testing.assert_close(s, s_ref, rtol=0, atol=0)
