@@ -307,6 +307,20 @@ int ebt_finalize_topk(const float* cand_vals, const int64_t* cand_rows, const do
                       const float* eps, const int32_t* ovf, double* out_scores, int64_t* out_rows,
                       int32_t* certified, void* stream);
 
+/* ---- implicit-feedback ALS (offline factor training) ---------
+ * Replaces pyspark.ml ALS(rank=32, maxIter=15, regParam=0.1, implicitPrefs=True) of
+ * notebooks/create-embeddings.ipynb:1055 (Spark ALS.scala computeFactors, implicit branch).
+ * ebt_als_gram: out[i*rank + j] = sum_r Y[r*rank + i] * Y[r*rank + j] (float64), Y n x rank f32.
+ * ebt_als_solve: for every destination u (users from item factors Y, or items from user
+ *   factors), with its ratings src[off[u] .. off[u+1]) / rating[...] (CSR):
+ *     A = YtY + sum alpha|r| y y^T + reg * n_pos I,  b = sum_{r > 0} (1 + alpha|r|) y,
+ *     X[u*rank ..] = (float) A^-1 b  (Cholesky in float64; n_pos = #ratings > 0).
+ *   rank <= 64. */
+int ebt_als_gram(const float* Y, int64_t n, int32_t rank, double* out, void* stream);
+int ebt_als_solve(const double* YtY, const float* Y, int32_t rank, int64_t n_dst,
+                  const int64_t* off, const int32_t* src, const float* rating, float alpha,
+                  float reg, float* X, void* stream);
+
 /* ---- per-stage GPU timing (hipEvents recorded on the launch stream) -----------------------
  * Stages: 0 screening GEMM (score-writing), 1 exclusion mask, 2 chunk select, 3 candidate
  * select (across chunks / head + fused tail), 4 rescore, 5 fused screening GEMM (filtering).

@@ -81,6 +81,8 @@ _SIGNATURES = {
     "ebt_cosine_topk": ([_VP, _VP, _VP, _VP, _I64, _I64, _VP, _INT, _I64, _VP, _VP, _VP, _INT,
                          _I32, _I64, _I32, _I32, _I64, _VP, _VP, _I32, _I32, _I64, _INT, _VP, _SZ,
                          _VP, _VP, _VP, _VP, _VP], _INT),
+    "ebt_als_gram": ([_VP, _I64, _I32, _VP, _VP], _INT),
+    "ebt_als_solve": ([_VP, _VP, _I32, _I64, _VP, _VP, _VP, _F32, _F32, _VP, _VP], _INT),
     "ebt_timer_create": ([], _VP),
     "ebt_timer_destroy": ([_VP], None),
     "ebt_timer_reset": ([_VP], _INT),
