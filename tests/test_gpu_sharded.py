@@ -368,3 +368,27 @@ def test_rccl_world1_staged_path(cuda_device):
     s_ref, r_ref = ebt.score_topk(cat, k, queries=qs[2])
     assert torch.equal(r, r_ref)
     torch.testing.assert_close(s, s_ref, rtol=0, atol=0)
+
+
+def test_shared_threshold_liked_users(cuda_device):
+    """The collaborative path (liked rows spread over the shards, all-reduced partial sums)
+    through the staged driver with the shared threshold and exclusions of the rated rows."""
+    from robot_ebert_amd.distributed import (run_sharded_steps, score_topk_sharded_local_stages,
+                                             shared_sample_tiles)
+    from robot_ebert_amd.search import pad_batch
+    from test_gpu_parity import _t, assert_topk_equal
+    n, d, k, world, B = 200_000, 64, 20, 2, 150
+    assert shared_sample_tiles(n, world, pad_batch(B)) > 0
+    c = gaussian(111, n, d, "f64")
+    rng = np.random.default_rng(112)
+    liked = [sorted(rng.choice(n, int(rng.integers(1, 12)), replace=False).tolist())
+             for _ in range(B)]
+    rated = [sorted(set(l) | set(rng.choice(n, 30, replace=False).tolist())) for l in liked]
+    full = _t(c, "f64", cuda_device)
+    res = _run_sharded(full, world, lambda r, cat, coll: run_sharded_steps(
+        lambda: score_topk_sharded_local_stages(cat, k, liked=liked, exclude=rated,
+                                                collectives=coll), 2))
+    sample = [0, 75, 149]
+    want_s, want_r = R.liked_topk(c, [liked[i] for i in sample], k, [rated[i] for i in sample])
+    for s, r in res:
+        assert_topk_equal(s[sample], r[sample], want_s, want_r)
