@@ -298,6 +298,16 @@ int ebt_cosine_screen_at(const double* q64, const void* qimg, const float* qscal
                          void* workspace, size_t ws_bytes, float* list_vals, int64_t* list_rows,
                          int32_t* ovf_out, float* eps_out, const float* theta, double hits,
                          void* timer, void* stream);
+/* After the floor all-gather of the per-shard path: g = [R][B][ld] float32 (each shard's k best
+ * approx in columns [0, ld-1), its eps in column ld-1) ->
+ * t_floor[b] = the k-th largest of g[r][b][j] - g[r][b][ld-1] over all r and j < ld-1, in float64
+ * (NaN counts as -inf): a lower bound of query b's k-th best exact score over the catalog. */
+int ebt_union_floor(const float* gathered, int32_t R, int64_t B, int32_t ld, int32_t k,
+                    double* t_floor, void* stream);
+/* cert[b] = -1 (rerun unfused) where ovf[b] != 0, or where theta (if not NULL) may have dropped
+ * a global top-k row: !(theta[b] <= t_floor[b] - eps[b]); a -2 (corrupt list) stays. */
+int ebt_certify_cut(int32_t* cert, const int32_t* ovf, const float* theta,
+                    const double* t_floor, const float* eps, int64_t B, void* stream);
 int ebt_rescore_owned(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
                       int64_t ld, const double* gnorm64, int64_t row_offset, int64_t n_rows,
                       const float* cand_vals, const int64_t* cand_rows, int32_t kprime, int32_t k,

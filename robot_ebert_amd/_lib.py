@@ -58,6 +58,8 @@ _SIGNATURES = {
     "ebt_cosine_sample": ([_VP, _VP, _I64, _VP, _VP, _INT, _I32, _I64, _I32, _I64, _I64, _VP,
                            _I64, _VP, _VP], _INT),
     "ebt_pool_kth": ([_VP, _I64, _I64, _I64, _I32, _I32, _VP, _VP], _INT),
+    "ebt_union_floor": ([_VP, _I32, _I64, _I32, _I32, _VP, _VP], _INT),
+    "ebt_certify_cut": ([_VP, _VP, _VP, _VP, _VP, _I64, _VP], _INT),
     "ebt_rescore_owned": ([_VP, _I64, _I32, _VP, _INT, _I64, _VP, _I64, _I64, _VP, _VP, _I32,
                            _I32, _VP, _VP, _VP], _INT),
     "ebt_finalize_topk": ([_VP, _VP, _VP, _I64, _I32, _I32, _I64, _VP, _VP, _VP, _VP, _VP, _VP],

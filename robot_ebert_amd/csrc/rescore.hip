@@ -600,4 +600,89 @@ int finalize_topk(const float* cand_vals, const int64_t* cand_rows, const double
   return launch_check("finalize_topk_kernel");
 }
 
+// ---------------------------------------------------------------------------------------------
+// Row-sharded per-shard path (distributed.py), after the floor all-gather: the catalog-wide floor
+// and the certificate adjustment in two launches instead of ~17 small torch ops.
+// union_floor: g = [R][B][ld] f32 (the shards' k best approx in columns [0, ld-1), their eps in
+// column ld-1); t_floor[b] = the k-th largest of g[r][b][j] - g[r][b][ld-1] over r, j (float64,
+// exact differences of two floats; NaN counts as -inf). One wave per query: bisection over the
+// order-preserving 64-bit keys of the doubles, counts by a strided pass over the R*(ld-1) values.
+__device__ __forceinline__ uint64_t d2key(double x) {
+  if (!(x == x)) return 0ull;  // NaN -> below -inf
+  uint64_t u = (uint64_t)__double_as_longlong(x);
+  if (x == 0.0) u = 0ull;      // -0 == +0
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double key2d(uint64_t k) {
+  const uint64_t u = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+  return __longlong_as_double((long long)u);
+}
+
+__global__ __launch_bounds__(256) void union_floor_kernel(const float* __restrict__ g, int R,
+                                                          int64_t B, int ld, int k,
+                                                          double* __restrict__ t_floor) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int per = ld - 1, n = R * per;
+  auto val = [&](int i) {
+    const int r = i / per, j = i - r * per;
+    const float* row = g + ((int64_t)r * B + b) * ld;
+    return (double)row[j] - (double)row[per];
+  };
+  auto count_ge = [&](uint64_t t) {
+    int c = 0;
+    for (int i = lane; i < n; i += 64) c += d2key(val(i)) >= t ? 1 : 0;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    return c;
+  };
+  // the largest key t with count(key >= t) >= k (key 0 = NaN / below everything)
+  uint64_t lo = 0ull, hi = ~0ull;
+  while (lo < hi) {
+    const uint64_t mid = lo + ((hi - lo) >> 1) + 1;
+    if (count_ge(mid) >= k) lo = mid;
+    else hi = mid - 1;
+  }
+  if (lane == 0) t_floor[b] = lo == 0ull ? -__builtin_inf() : key2d(lo);
+}
+
+// cert[b] = -1 (rerun unfused) when the fused screen overflowed (ovf[b] != 0) or the shared
+// threshold may have dropped a global top-k row (theta[b] > t_floor[b] - eps[b]); -2 stays.
+__global__ void certify_cut_kernel(int32_t* __restrict__ cert, const int32_t* __restrict__ ovf,
+                                   const float* __restrict__ theta,
+                                   const double* __restrict__ t_floor,
+                                   const float* __restrict__ eps, int64_t B) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B || cert[b] == -2) return;
+  bool drop = ovf[b] != 0;
+  if (theta) drop |= !((double)theta[b] <= t_floor[b] - (double)eps[b]);
+  if (drop) cert[b] = -1;
+}
+
 }  // namespace ebt
+
+extern "C" int ebt_union_floor(const float* gathered, int32_t R, int64_t B, int32_t ld, int32_t k,
+                               double* t_floor, void* stream) {
+  using namespace ebt;
+  if (!gathered || !t_floor || R < 1 || B < 0 || ld < 2 || k < 1 || (int64_t)R * (ld - 1) > (1 << 30)) {
+    set_error("ebt_union_floor: bad arguments (R=%d B=%lld ld=%d k=%d)", R, (long long)B, ld, k);
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  hipLaunchKernelGGL(union_floor_kernel, dim3((unsigned)ceil_div(B, 4)), dim3(256), 0,
+                     (hipStream_t)stream, gathered, R, B, ld, k, t_floor);
+  return launch_check("union_floor_kernel");
+}
+
+extern "C" int ebt_certify_cut(int32_t* cert, const int32_t* ovf, const float* theta,
+                               const double* t_floor, const float* eps, int64_t B, void* stream) {
+  using namespace ebt;
+  if (!cert || !ovf || B < 0 || (theta && (!t_floor || !eps))) {
+    set_error("ebt_certify_cut: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  hipLaunchKernelGGL(certify_cut_kernel, dim3((unsigned)ceil_div(B, 256)), dim3(256), 0,
+                     (hipStream_t)stream, cert, ovf, theta, t_floor, eps, B);
+  return launch_check("certify_cut_kernel");
+}

@@ -36,7 +36,7 @@ from .catalog import Catalog
 from .search import (KPRIME_MAX, _round_up, csr_from_lists, csr_subset, default_kprime,
                      merge_topk, pad_batch, pool_kth, prepare_queries, run_screen,
                      sample_maxima, score_topk, score_topk_finish, score_topk_stages,
-                     score_topk_submit, spec_rank, union_floor)
+                     score_topk_submit, spec_rank, union_floor, union_floor_gathered)
 
 SAMPLE_TILES_MAX = 64   # per shard, as the single-GPU speculative screen (api.hip spec_params)
 # Larger shards screen at their own sample threshold: there the shard's first segment raises
@@ -225,6 +225,8 @@ def _gathered_floor(coll, vals: torch.Tensor, eps: torch.Tensor, k: int):
 
     def floor():
         g = wait()
+        if g.is_cuda:
+            return union_floor_gathered(g, k)
         return union_floor(g[:, :, :-1], g[:, :, -1], k)
     return floor
 
@@ -237,7 +239,9 @@ def shared_sample_tiles(n_global: int, world: int, B_pad: int) -> int:
     if world < 2 or B_pad % 256 != 0 or -(-n_global // world) > SHARED_MAX_SHARD_ROWS:
         return 0
     full = -(-n_global // world) // 256
-    P = min(SAMPLE_TILES_MAX, full // 24)
+    # about the single-GPU sample in total (64 tiles over all shards, >= 4 per shard): a larger
+    # pooled sample tightens theta little but costs every shard its GEMM and a wider pool_kth
+    P = min(SAMPLE_TILES_MAX, full // 24, max(4, -(-SAMPLE_TILES_MAX // world)))
     per = max(1, 256 // (B_pad // 256))
     if P // per * per >= 8:
         P = P // per * per

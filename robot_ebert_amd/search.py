@@ -505,12 +505,26 @@ class PendingTopk:
     ready: torch.cuda.Event
 
 
+def union_floor_gathered(g: torch.Tensor, k: int) -> torch.Tensor:
+    """ebt_union_floor over an all-gathered [R, B, k'+1] f32 tensor (the shards' k' best approx,
+    then their eps): float64 [B]."""
+    g = g.contiguous()
+    R, B, ld = g.shape
+    out = torch.empty(B, dtype=torch.float64, device=g.device)
+    call("ebt_union_floor", ptr(g), R, B, ld, k, ptr(out), stream_of(g.device))
+    return out
+
+
 def union_floor(vals: torch.Tensor, eps: torch.Tensor, k: int) -> torch.Tensor:
     """The k-th largest of vals[r, b, j] - eps[r, b] over all shards r and slots j: a lower bound
     of query b's k-th best exact score (vals f32 [R, B, k] approx, eps f32 [R, B])."""
     R, B, kk = vals.shape
+    if vals.is_cuda:   # one kernel (ebt_union_floor) on the device
+        g = torch.cat([vals.float(), eps.float()[:, :, None]], 2).contiguous()
+        return union_floor_gathered(g, k)
     lo = vals.double() - eps.double()[:, :, None]
-    lo = torch.nan_to_num(lo, nan=float("-inf")).permute(1, 0, 2).reshape(B, R * kk)
+    lo = torch.nan_to_num(lo, nan=float("-inf"), neginf=float("-inf"))
+    lo = lo.permute(1, 0, 2).reshape(B, R * kk)
     return torch.topk(lo, k, dim=1).values[:, k - 1].contiguous()
 
 
@@ -563,10 +577,8 @@ def _global_cut_stages(catalog: Catalog, qb: QueryBatch, k: int, k_req: int, kpr
     # an overflowed fused list is rerun unfused (cert -1), unless a row is corrupt (-2); so is a
     # query whose shared threshold may have dropped a row of the global top k: every top-k row
     # has approx >= t_floor - eps, so theta <= t_floor - eps keeps them all
-    drop = ovf != 0
-    if use_theta:
-        drop |= ~(th[0][:B].double() <= t_floor - eps[:B].double())
-    cert = torch.where(drop & (cert != -2), torch.full_like(cert, -1), cert)
+    call("ebt_certify_cut", ptr(cert), ptr(ovf), ptr(th[0]) if use_theta else None,
+         ptr(t_floor), ptr(eps), B, stream_of(dev))
     yield out_s, out_r, cert
 
 

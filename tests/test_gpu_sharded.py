@@ -392,3 +392,21 @@ def test_shared_threshold_liked_users(cuda_device):
     want_s, want_r = R.liked_topk(c, [liked[i] for i in sample], k, [rated[i] for i in sample])
     for s, r in res:
         assert_topk_equal(s[sample], r[sample], want_s, want_r)
+
+
+@pytest.mark.parametrize("R,k,kk", [(8, 100, 100), (3, 7, 16), (2, 1000, 1000)])
+def test_union_floor_kernel_matches_torch(cuda_device, R, k, kk):
+    """ebt_union_floor (one wave per query, bisection over 64-bit keys) equals the torch
+    restatement (the k-th largest of approx - eps over all shards), with -inf padding, NaNs and
+    ties."""
+    from robot_ebert_amd.search import union_floor, union_floor_gathered
+    B = 333
+    g = torch.Generator().manual_seed(R * 1000 + k)
+    vals = torch.randn((R, B, kk), generator=g) * 0.03
+    vals[:, :, kk // 2:] = float("-inf")                 # short lists
+    vals[0, :5, 0] = float("nan")
+    vals[:, 7, :] = 0.25                                 # ties
+    eps = torch.rand((R, B), generator=g) * 1e-3
+    want = union_floor(vals, eps, k)                     # CPU tensors: the torch form
+    got = union_floor_gathered(torch.cat([vals, eps[:, :, None]], 2).to(cuda_device), k)
+    assert torch.equal(got.cpu(), want)
