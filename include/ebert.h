@@ -82,6 +82,11 @@ int ebt_query_dense(const void* q, int dtype, int64_t B, int32_t d, int64_t ldq,
 int ebt_query_liked_sum(const void* cat, int dtype, int32_t d, int64_t ld,
                         const double* gnorm64_cat, int64_t B, const int64_t* liked_off,
                         const int64_t* liked_rows, double* q64, void* stream);
+/* ebt_query_dense + ebt_query_image in one launch for dense queries (d <= 4096; same q64,
+ * qimg, qscale and eps; with native_q the query dtype must equal img_dtype). */
+int ebt_query_prep(const void* q, int dtype, int64_t B, int64_t B_pad, int32_t d, int64_t ldq,
+                   int img_dtype, int native_q, float u_cat, double* q64, void* qimg,
+                   int32_t ld_img, float* qscale, float* eps, void* stream);
 /* q64[b] *= scale[b] (scale is device float64[B]); used for the 1/L of lib.py:52. */
 int ebt_scale_rows_f64(double* q64, int64_t B, int32_t d, const double* scale, void* stream);
 

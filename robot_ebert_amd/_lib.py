@@ -41,6 +41,8 @@ _SIGNATURES = {
     "ebt_query_dense": ([_VP, _INT, _I64, _I32, _I64, _VP, _VP], _INT),
     "ebt_query_liked_sum": ([_VP, _INT, _I32, _I64, _VP, _I64, _VP, _VP, _VP, _VP], _INT),
     "ebt_scale_rows_f64": ([_VP, _I64, _I32, _VP, _VP], _INT),
+    "ebt_query_prep": ([_VP, _INT, _I64, _I64, _I32, _I64, _INT, _INT, _F32, _VP, _VP, _I32, _VP,
+                        _VP, _VP], _INT),
     "ebt_query_image": ([_VP, _I64, _I64, _I32, _INT, _VP, _I64, _INT, _F32, _VP, _I32, _VP, _VP,
                          _VP], _INT),
     "ebt_screen_scores": ([_VP, _I64, _VP, _I64, _I32, _I32, _INT, _VP, _VP, _VP, _I64, _VP],

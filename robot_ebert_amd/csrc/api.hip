@@ -42,6 +42,8 @@ int query_liked_sum(const void*, int, int32_t, int64_t, const double*, int64_t, 
 int scale_rows_f64(double*, int64_t, int32_t, const double*, hipStream_t);
 int query_image(const double*, int64_t, int64_t, int32_t, int, const void*, int64_t, int, float,
                 void*, int32_t, float*, float*, hipStream_t);
+int query_prep(const void*, int, int64_t, int64_t, int32_t, int64_t, int, int, float, double*,
+               void*, int32_t, float*, float*, hipStream_t);
 int mask_excluded(float*, int64_t, int64_t, int64_t, int64_t, const int64_t*, const int64_t*,
                   hipStream_t);
 int rescore(const double*, int64_t, int32_t, const void*, int, int64_t, const double*, int64_t,
@@ -401,6 +403,13 @@ int ebt_query_liked_sum(const void* cat, int dtype, int32_t d, int64_t ld,
                         const int64_t* liked_rows, double* q64, void* stream) {
   return query_liked_sum(cat, dtype, d, ld, gnorm64_cat, B, liked_off, liked_rows, q64,
                          (hipStream_t)stream);
+}
+
+int ebt_query_prep(const void* q, int dtype, int64_t B, int64_t B_pad, int32_t d, int64_t ldq,
+                   int img_dtype, int native_q, float u_cat, double* q64, void* qimg,
+                   int32_t ld_img, float* qscale, float* eps, void* stream) {
+  return query_prep(q, dtype, B, B_pad, d, ldq, img_dtype, native_q, u_cat, q64, qimg, ld_img,
+                    qscale, eps, (hipStream_t)stream);
 }
 
 int ebt_scale_rows_f64(double* q64, int64_t B, int32_t d, const double* scale, void* stream) {

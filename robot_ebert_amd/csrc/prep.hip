@@ -313,6 +313,87 @@ int query_image(const double* q64, int64_t B, int64_t B_pad, int32_t d, int img_
   return launch_check("query_image_kernel");
 }
 
+// ------------------------------------------------------ dense queries in one pass ----------
+// query_dense + query_image for dense queries with d <= 16 * 256: each thread keeps its elements
+// (j = tid, tid + 256, ...: the same order, so the same float64 sums as the two kernels) in
+// registers; the row is read once and q64, the image, qscale and eps are written in one launch.
+constexpr int QP_PER = 16;
+template <int DT, int IMG>
+__global__ __launch_bounds__(256) void query_prep_kernel(
+    const void* __restrict__ q, int64_t B, int d, int64_t ldq, int native_q, float u_cat,
+    double* __restrict__ q64, uint16_t* __restrict__ qimg, int ld_img,
+    float* __restrict__ qscale, float* __restrict__ eps) {
+  __shared__ double red[4];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  uint16_t* orow = qimg + b * ld_img;
+  if (b >= B) {  // padding rows
+    for (int j = tid; j < ld_img; j += blockDim.x) orow[j] = 0;
+    if (tid == 0) {
+      qscale[b] = 1.f;
+      eps[b] = 0.f;
+    }
+    return;
+  }
+  double v[QP_PER];
+  double s = 0.0;
+#pragma unroll
+  for (int e = 0; e < QP_PER; ++e) {
+    const int j = tid + e * 256;
+    v[e] = j < d ? load_as_f64<DT>(q, b * ldq + j) : 0.0;
+    s += v[e] * v[e];
+  }
+  const double nq = sqrt(block_sum_f64(s, red));
+  const double g = guard_norm(nq);
+  double s2 = 0.0;
+#pragma unroll
+  for (int e = 0; e < QP_PER; ++e) {
+    const int j = tid + e * 256;
+    if (j < d) {
+      const double x = v[e] / g;
+      q64[b * d + j] = x;
+      s2 += x * x;
+      orow[j] = native_q ? ((const uint16_t*)q)[b * ldq + j] : f64_to_img<IMG>(x);
+    }
+  }
+  for (int j = d + tid; j < ld_img; j += blockDim.x) orow[j] = 0;
+  const double qnrm = sqrt(block_sum_f64(s2, red));
+  if (tid == 0) {
+    // native: the image holds q itself, scaled by 1 / ||q|| in the epilogue (query_image)
+    qscale[b] = native_q ? (float)(1.0 / g) : 1.f;
+    const double uq = native_q ? 0.0 : (IMG == EBT_F16 ? 0x1p-11 : 0x1p-8);
+    const double uc = (double)u_cat;
+    eps[b] = (float)(1.05 * (qnrm * (uq + uc + uq * uc) + (d + 8) * 0x1p-24 * (qnrm + 1.0)) +
+                     1e-9);
+  }
+}
+
+int query_prep(const void* q, int dtype, int64_t B, int64_t B_pad, int32_t d, int64_t ldq,
+               int img_dtype, int native_q, float u_cat, double* q64, void* qimg, int32_t ld_img,
+               float* qscale, float* eps, hipStream_t st) {
+  if (!q || !q64 || !qimg || !qscale || !eps || B < 0 || B_pad < B || d <= 0 ||
+      d > QP_PER * 256 || ldq < d || ld_img < d || ld_img % 64 != 0 || dtype < 0 || dtype > 3 ||
+      (img_dtype != EBT_F16 && img_dtype != EBT_BF16) ||
+      (native_q && dtype != img_dtype)) {
+    set_error("ebt_query_prep: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (B_pad == 0) return EBT_OK;
+  dim3 grid((unsigned)B_pad), block(256);
+#define EBT_QP(DT, IMG)                                                                      \
+  hipLaunchKernelGGL((query_prep_kernel<DT, IMG>), grid, block, 0, st, q, B, d, ldq, native_q, \
+                     u_cat, q64, (uint16_t*)qimg, ld_img, qscale, eps)
+  const bool f16 = img_dtype == EBT_F16;
+  switch (dtype) {
+    case EBT_F32: if (f16) { EBT_QP(EBT_F32, EBT_F16); } else { EBT_QP(EBT_F32, EBT_BF16); } break;
+    case EBT_BF16: if (f16) { EBT_QP(EBT_BF16, EBT_F16); } else { EBT_QP(EBT_BF16, EBT_BF16); } break;
+    case EBT_F16: if (f16) { EBT_QP(EBT_F16, EBT_F16); } else { EBT_QP(EBT_F16, EBT_BF16); } break;
+    default: if (f16) { EBT_QP(EBT_F64, EBT_F16); } else { EBT_QP(EBT_F64, EBT_BF16); } break;
+  }
+#undef EBT_QP
+  return launch_check("query_prep_kernel");
+}
+
 // ------------------------------------------------------------------------- exclusions ------
 __global__ __launch_bounds__(256) void mask_excluded_kernel(float* __restrict__ s, int64_t ld,
                                                              int64_t c0, int64_t c1,

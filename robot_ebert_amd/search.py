@@ -29,6 +29,7 @@ from ._lib import DTYPE_CODE, EbertError, call, ptr, require_cuda, stream_of
 from .catalog import Catalog
 
 KPRIME_MAX = 4096
+QUERY_PREP_MAX_D = 4096  # ebt_query_prep keeps 16 elements per thread
 MERGE_WAVE_KMAX = 512   # largest k' of the fused wave-merge screen (select_topk.hip WMERGE_K)
 DEFAULT_SCORE_BUDGET = int(os.environ.get("EBT_SCORE_BUDGET", str(4 << 30)))  # bytes of f32 scores
 
@@ -123,9 +124,19 @@ def prepare_queries(catalog: Catalog, queries: Optional[torch.Tensor] = None,
             queries = queries.contiguous()
         B = int(queries.shape[0])
         q64 = torch.empty((B, d), dtype=torch.float64, device=dev)
+        native_q = catalog.native and queries.dtype == catalog.img_torch_dtype
+        if d <= QUERY_PREP_MAX_D:   # one launch: q64, image, scale and eps (ebt_query_prep)
+            B_pad = pad_batch(B)
+            qimg = torch.empty((B_pad, catalog.ld_img), dtype=catalog.img_torch_dtype, device=dev)
+            qscale = torch.empty(B_pad, dtype=torch.float32, device=dev)
+            eps = torch.empty(B_pad, dtype=torch.float32, device=dev)
+            call("ebt_query_prep", ptr(queries), DTYPE_CODE[queries.dtype], B, B_pad, d,
+                 int(queries.stride(0)), catalog.img_dtype, 1 if native_q else 0,
+                 float(catalog.u_cat), ptr(q64), ptr(qimg), catalog.ld_img, ptr(qscale),
+                 ptr(eps), st)
+            return QueryBatch(q64, qimg, qscale, eps, B)
         call("ebt_query_dense", ptr(queries), DTYPE_CODE[queries.dtype], B, d,
              int(queries.stride(0)), ptr(q64), st)
-        native_q = catalog.native and queries.dtype == catalog.img_torch_dtype
     else:
         off, rows = liked
         B = int(off.numel()) - 1

@@ -762,3 +762,31 @@ def test_torch_ops_cosine_topk(cuda_device, case):
     ms, mr = torch.ops.ebert.merge_topk(torch.stack([p[0] for p in parts]),
                                         torch.stack([p[1] for p in parts]), k)
     assert_topk_equal(ms, mr, s_ref, r_ref)
+
+
+@pytest.mark.parametrize("qdt,cdt,d", [("f32", "f32", 1536), ("bf16", "bf16", 768),
+                                       ("f16", "f16", 200), ("f64", "f64", 32),
+                                       ("f16", "f32", 4096)])
+def test_query_prep_fused_equals_two_kernels(cuda_device, qdt, cdt, d):
+    """ebt_query_prep (one launch) writes exactly what ebt_query_dense + ebt_query_image write,
+    native images included."""
+    ebt, L = _ebt()
+    from robot_ebert_amd.search import pad_batch
+    B = 300
+    cat = ebt.Catalog(_t(gaussian(41, 1000, d, cdt), cdt, cuda_device))
+    q = _t(gaussian(42, B, d, qdt), qdt, cuda_device)
+    qb = ebt.prepare_queries(cat, queries=q)          # the fused launch (d <= 4096)
+    st = L.stream_of(cuda_device)
+    q64 = torch.empty((B, d), dtype=torch.float64, device=cuda_device)
+    L.call("ebt_query_dense", L.ptr(q), L.DTYPE_CODE[q.dtype], B, d, d, L.ptr(q64), st)
+    B_pad = pad_batch(B)
+    native = cat.native and q.dtype == cat.img_torch_dtype
+    qimg = torch.empty((B_pad, cat.ld_img), dtype=cat.img_torch_dtype, device=cuda_device)
+    qs = torch.empty(B_pad, dtype=torch.float32, device=cuda_device)
+    eps = torch.empty(B_pad, dtype=torch.float32, device=cuda_device)
+    L.call("ebt_query_image", L.ptr(q64), B, B_pad, d, cat.img_dtype, L.ptr(q) if native else None,
+           d if native else 0, 1 if native else 0, float(cat.u_cat), L.ptr(qimg), cat.ld_img,
+           L.ptr(qs), L.ptr(eps), st)
+    assert torch.equal(qb.q64, q64)
+    assert torch.equal(qb.qimg.view(torch.int16), qimg.view(torch.int16))
+    assert torch.equal(qb.qscale, qs) and torch.equal(qb.eps, eps)
