@@ -80,9 +80,11 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     int ovf_cap) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* qs = (double*)smem;                 // d
-  double* sc = qs + ((d + 1) & ~1);           // kpp
+  double* sc = qs + ((d + 1) & ~1);           // kpp: approx, then exact
   int64_t* rw = (int64_t*)(sc + kpp);         // kpp
-  __shared__ int nvalid, corrupt, nkeep;
+  int* pl = (int*)(rw + kpp);                 // kpp: list position of each kept row
+  __shared__ int nvalid, corrupt, nkeep, ntop;
+  __shared__ unsigned long long smin_key;
   constexpr int NW = RTHREADS / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
@@ -90,6 +92,8 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     nvalid = 0;
     corrupt = 0;
     nkeep = 0;
+    ntop = 0;
+    smin_key = ~0ull;
   }
   for (int j = tid; j < d; j += RTHREADS) qs[j] = q64[b * d + j];
   const int64_t* cr = cand_rows + b * kprime;
@@ -124,16 +128,35 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
       if (kb) base = atomicAdd(&nkeep, __popcll(kb));
     }
     base = __shfl(base, 0, 64);
-    if (keep) rw[base + __popcll(kb & ((1ull << lane) - 1))] = row;
+    if (keep) {
+      const int at = base + __popcll(kb & ((1ull << lane) - 1));
+      rw[at] = row;
+      sc[at] = (double)v;
+      pl[at] = c;
+    }
   }
   __syncthreads();
   const int nk = nkeep;
-  // 2. exact scores, two rows per wave at a time with all of a lane's loads for both rows
-  //    issued before the arithmetic (chunk order per lane unchanged: bit-identical sums)
-  for (int j = wave; j < nk; j += 2 * NW) {
+  // 2. exact scores in two passes. The list's first k positions hold its k best approx (a
+  //    partitioned or sorted list): pass A scores those; their smallest exact score s_min
+  //    bounds the k-th best exact score from below (k rows reach it), so a later candidate
+  //    with approx < s_min - eps (exact < s_min) cannot enter the top k: pass B skips it. About
+  //    half of the 2 eps band is never gathered.
+  //    Two rows per wave at a time with all of a lane's loads for both rows issued before the
+  //    arithmetic (chunk order per lane unchanged: bit-identical sums).
+  auto exact_pass = [&](bool top, double cut2) {
+    for (int j = wave; j < nk; j += 2 * NW) {
     const int jb = j + NW;
-    const bool hb = jb < nk;
-    const int64_t ra = rw[j], rb = hb ? rw[jb] : ra;
+    const bool sel_a = (pl[j] < k) == top && (top || !(sc[j] < cut2));
+    const bool sel_b = jb < nk && (pl[jb] < k) == top && (top || !(sc[jb] < cut2));
+    if (!top) {  // skipped: below the two-stage cut, sorted last
+      if (lane == 0 && pl[j] >= k && !sel_a) sc[j] = -__builtin_inf();
+      if (lane == 0 && jb < nk && pl[jb] >= k && !sel_b) sc[jb] = -__builtin_inf();
+    }
+    if (!sel_a && !sel_b) continue;
+    const int ja = sel_a ? j : jb;          // one selected row goes first
+    const bool hb = sel_a && sel_b;         // a second one
+    const int64_t ra = rw[ja], rb = hb ? rw[jb] : ra;
     const double ga = gnorm[ra], gb = gnorm[rb];
     double sa = 0.0, sb = 0.0;
     if constexpr (VEC) {
@@ -172,13 +195,35 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     sb = wave_sum_f64(sb);
     if (lane == 0) {
       const double va = sa / ga;
-      sc[j] = (va == va) ? va : -__builtin_inf();
+      sc[ja] = (va == va) ? va : -__builtin_inf();
       if (hb) {
         const double vb2 = sb / gb;
         sc[jb] = (vb2 == vb2) ? vb2 : -__builtin_inf();
       }
     }
+    }
+  };
+  exact_pass(true, 0.0);
+  __syncthreads();
+  // s_min over the k top entries (all k present and valid), as an order-preserving key
+  for (int j = tid; j < nk; j += RTHREADS) {
+    if (pl[j] < k) {
+      atomicAdd(&ntop, 1);
+      const double x = sc[j];
+      unsigned long long key = (unsigned long long)__double_as_longlong(x);
+      key = (key >> 63) ? ~key : (key | 0x8000000000000000ull);
+      if (x == x) atomicMin(&smin_key, key);
+    }
   }
+  __syncthreads();
+  double cut2 = cut;
+  if (ntop == k && smin_key != ~0ull) {
+    const unsigned long long key = smin_key;
+    const double smin = __longlong_as_double(
+        (long long)((key >> 63) ? (key & 0x7fffffffffffffffull) : ~key));
+    if (smin - (double)eps[b] > cut2) cut2 = smin - (double)eps[b];
+  }
+  exact_pass(false, cut2);
   // 3. sort the kept rows (padded to a power of two >= k); slots past them read NaN / -1
   int P = 1;
   while (P < nk || P < k) P <<= 1;
@@ -204,7 +249,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
       // rows below the k'-th candidate have approx <= amin; none of them can enter the top k
       // when amin < cut (the local k-th - 2 eps, or t_floor - eps when that is higher)
       const double amin = (double)cv[kprime - 1];
-      ok = amin < cut;
+      ok = amin < cut2;
     }
     if (ovf_cnt && ovf_cnt[b] > ovf_cap) ok = -1;  // fused screen dropped candidates
     if (corrupt) ok = -2;                           // internal error: row out of range
@@ -214,7 +259,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
 
 size_t rescore_lds_bytes(int d, int kprime) {
   const int kpp = next_pow2_h(kprime);
-  return 8 * (size_t)((d + 1) & ~1) + 16 * (size_t)kpp;
+  return 8 * (size_t)((d + 1) & ~1) + 20 * (size_t)kpp;
 }
 
 int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype, int64_t ld,
