@@ -151,11 +151,14 @@ int ebt_select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B
  * best by (score desc, row asc) go to out_scores/out_rows[b*k + j] (rows + row_offset; empty
  * slots NaN / -1). certified[b] = 1 iff the candidate set provably contains the exact top-k:
  * kprime >= n_rows (every row is a candidate),
- * fewer than kprime valid candidates, or approx[kprime-1] < cut[b] (below).
+ * fewer than kprime valid candidates, or approx[kprime-1] < cut[b] (below, after its rise).
  * n_rows is the catalog's row count; a candidate row >= n_rows is never read and gives
  * certified[b] = -2 (corrupt candidate list).
  * Candidates with approx < cut[b] = max(approx[k-1] - 2*eps[b], t_floor[b] - eps[b]) cannot
- * be in the top k and are not gathered (equal cand_vals and eps = 0 rescore every candidate). t_floor
+ * be in the top k and are not gathered (equal cand_vals and eps = 0 rescore every candidate).
+ * With eps[b] > 0 the cut then rises to s_min - eps[b], s_min = the smallest exact score of the
+ * list's first k entries (k rows score >= s_min, so a row with exact < s_min is not in the top
+ * k): those k are scored first and later candidates below the raised cut are skipped. t_floor
  * (float64 [B], NULL = none) is a lower bound of the k-th best EXACT score over the whole
  * (sharded) catalog, e.g. the all-reduced max over shards of approx[k-1] - eps: a shard then
  * rescores only rows that can enter the GLOBAL top k, and the slots of its top k that such a

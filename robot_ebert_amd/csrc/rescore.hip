@@ -217,7 +217,8 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
   }
   __syncthreads();
   double cut2 = cut;
-  if (ntop == k && smin_key != ~0ull) {
+  // (eps = 0 means "rescore every candidate above the first cut", not an exact approx)
+  if (ntop == k && smin_key != ~0ull && eps[b] > 0.f) {
     const unsigned long long key = smin_key;
     const double smin = __longlong_as_double(
         (long long)((key >> 63) ? (key & 0x7fffffffffffffffull) : ~key));

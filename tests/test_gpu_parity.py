@@ -790,3 +790,50 @@ def test_query_prep_fused_equals_two_kernels(cuda_device, qdt, cdt, d):
     assert torch.equal(qb.q64, q64)
     assert torch.equal(qb.qimg.view(torch.int16), qimg.view(torch.int16))
     assert torch.equal(qb.qscale, qs) and torch.equal(qb.eps, eps)
+
+
+@pytest.mark.parametrize("eps_v", [0.0, 0.002, 0.05])
+def test_rescore_two_stage_cut(cuda_device, eps_v):
+    """ebt_rescore's raised cut (s_min - eps, s_min = the smallest exact score of the list's
+    first k): approx values perturbed within +-eps of the exact scores, the list = the k' best
+    approx of the whole catalog. Its top k equals the exact top k of the candidates; with
+    certified = 1 it is the catalog's exact top k; eps = 0 with equal cand_vals rescores every
+    candidate (the header's contract)."""
+    ebt, L = _ebt()
+    n, d, B, k, kp = 3000, 48, 6, 20, 300
+    rng = np.random.default_rng(7)
+    cat = rng.standard_normal((n, d))
+    q = rng.standard_normal((B, d))
+    q64 = q / np.linalg.norm(q, axis=1, keepdims=True)
+    g = np.linalg.norm(cat, axis=1)
+    exact = (q64 @ cat.T) / g
+    if eps_v > 0:
+        approx = (exact + rng.uniform(-0.9 * eps_v, 0.9 * eps_v, exact.shape)).astype(np.float32)
+    else:
+        approx = exact.astype(np.float32)
+    cand = np.argsort(-approx.astype(np.float64), axis=1, kind="stable")[:, :kp]
+    cv = np.take_along_axis(approx, cand, 1)
+    if eps_v == 0.0:
+        cv[:] = 0.0  # the "rescore every candidate" form
+    dev = cuda_device
+    T = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x)).to(dev).to(dt)
+    qt, ct, gt = T(q64, torch.float64), T(cat, torch.float64), T(g, torch.float64)
+    cvt, crt = T(cv, torch.float32), T(cand, torch.int64)
+    epst = torch.full((B,), eps_v, dtype=torch.float32, device=dev)
+    out_s = torch.empty((B, k), dtype=torch.float64, device=dev)
+    out_r = torch.empty((B, k), dtype=torch.int64, device=dev)
+    cert = torch.empty(B, dtype=torch.int32, device=dev)
+    L.call("ebt_rescore", L.ptr(qt), B, d, L.ptr(ct), L.DTYPE_CODE[torch.float64], d, L.ptr(gt),
+           0, L.ptr(cvt), L.ptr(crt), kp, k, n, L.ptr(epst), None, L.ptr(out_s), L.ptr(out_r),
+           L.ptr(cert), L.stream_of(dev))
+    torch.cuda.synchronize()
+    s, r, c = out_s.cpu().numpy(), out_r.cpu().numpy(), cert.cpu().numpy()
+    for b in range(B):
+        ce = exact[b, cand[b]]
+        o = np.lexsort((cand[b], -ce))[:k]
+        np.testing.assert_array_equal(r[b], cand[b][o])
+        np.testing.assert_allclose(s[b], ce[o], rtol=0, atol=SCORE_ATOL)
+        if c[b] == 1:
+            np.testing.assert_array_equal(r[b], np.lexsort((np.arange(n), -exact[b]))[:k])
+    if eps_v == 0.002:
+        assert (c == 1).all()
