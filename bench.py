@@ -140,6 +140,29 @@ def pmc_traffic(config: str, world: int):
         return None
 
 
+def host_boundary(cat, k, q, timer, steps=3):
+    """Untimed for `value`: the same step with the queries handed over in pinned host memory
+    and the results copied back (PCIe-inclusive; steps not overlapped)."""
+    import robot_ebert_amd as ebt
+    dev = q.device
+    qh = q.cpu().pin_memory()
+    timer.only()
+    outs = None
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        qd = qh.to(dev, non_blocking=True)
+        s, r = ebt.score_topk_finish(ebt.score_topk_submit(cat, k, queries=qd, timer=timer))
+        outs = (s.to("cpu", non_blocking=True), r.to("cpu", non_blocking=True))
+        torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t0) / steps
+    return {"ms_per_step": round(1e3 * el, 3), "queries_per_s": round(q.shape[0] / el, 1),
+            "h2d_bytes": qh.numel() * qh.element_size(),
+            "d2h_bytes": sum(t.numel() * t.element_size() for t in outs), "steps": steps,
+            "note": "queries from pinned host memory, results back to host memory, "
+                    "one step at a time (no overlap); never `value`"}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -243,6 +266,7 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     st = {name: timer.query(name) for name in ("gemm", "gemm_filter", "mask", "select",
                                                "merge_select", "rescore")}
+    host = host_boundary(cat, k, q, timer) if world == 1 else None
     n_local = end - begin
     B, d = cfg["b"], cfg["d"]
     head = pl["head_rows"]
@@ -299,6 +323,7 @@ def main() -> None:
             },
             "plan": pl,
             "stage_ms_per_step": {name: round(v[0], 4) for name, v in st.items()},
+            "host_boundary": host,
         }
         if world == 1 and not args.no_cpu_baseline:
             base, parity = cpu_baseline_and_parity(cfg, emb, q, s, r, args.cpu_budget)
