@@ -62,7 +62,8 @@ int pool_kth(const float*, int64_t, int64_t, int64_t, int, int, float*, hipStrea
 int screen_gemm_pool(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
                      const float*, const float*, int64_t, float*, int64_t, hipStream_t);
 int merge_segment(float*, int64_t*, int64_t, int, const uint64_t*, int64_t, int, const uint8_t*,
-                  int64_t, int64_t, int64_t, const int64_t*, const int64_t*, int*, hipStream_t);
+                  int64_t, int64_t, int64_t, const int64_t*, const int64_t*, int*, hipStream_t,
+                  double expect_hits = 0.0);
 bool merge_wave_fits(int);
 int merge_wave_capacity();
 int merge_block_capacity(int);
@@ -703,7 +704,7 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
       else  // sorted lists (the block merge sorts the union)
         rc = merge_segment(fv, fi, B, kprime, cand, L.ld_cand, slots, counts, L.ld_counts,
                            ceil_div(seg, L.group_rows), a.row_offset, a.excl_off, a.excl_rows,
-                           ovf, st);
+                           ovf, st, rate * (double)seg);
     }
     if (rc) return rc;
     r0 += seg;

@@ -416,6 +416,7 @@ int select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B, in
 // the LDS holds sets ovf[b]: the query's certificate becomes -1 and it is rerun unfused.
 // ---------------------------------------------------------------------------------------------
 constexpr int MERGE_MAX = 16384;  // LDS entries (128 KiB)
+constexpr int MERGE_DEFER = 1 << 4;  // ovf bit: the query waits for the full-size merge
 
 static int merge_entries(int kprime) {
   int P = 2;
@@ -428,12 +429,17 @@ __global__ __launch_bounds__(STHREADS) void merge_segment_kernel(
     const uint64_t* __restrict__ cand, int64_t ld_cand, int slots,
     const uint8_t* __restrict__ counts, int64_t ld_counts, int n_groups, int P_max,
     int64_t row_offset,
-    const int64_t* __restrict__ eo, const int64_t* __restrict__ er, int* __restrict__ ovf) {
+    const int64_t* __restrict__ eo, const int64_t* __restrict__ er, int* __restrict__ ovf,
+    int tier) {
   extern __shared__ __attribute__((aligned(16))) uint64_t mkeep[];
   __shared__ int wsum[STHREADS / 64];
   __shared__ int flag;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
+  // tier 1 (P_max = a small LDS buffer, several workgroups per CU) defers a query whose union
+  // does not fit (ovf bit MERGE_DEFER, nothing written); tier 2 (the full buffer) merges only those
+  const int ovf_in = tier ? ovf[b] : 0;
+  if (tier == 2 && !(ovf_in & MERGE_DEFER)) return;
   const uint8_t* cr = counts + b * ld_counts;
   const uint64_t* cb = cand + b * ld_cand;
   if (tid == 0) flag = 0;
@@ -465,6 +471,10 @@ __global__ __launch_bounds__(STHREADS) void merge_segment_kernel(
   }
   int pos = base + incl - mine;
   const int room = P_max - kprime;
+  if (tier == 1 && total > room) {  // block-uniform
+    if (tid == 0) ovf[b] = ovf_in | MERGE_DEFER;
+    return;
+  }
   if (total > room) over = true;
   const int64_t elo = eo ? eo[b] : 0, ehi = eo ? eo[b + 1] : 0;
   for (int g = g0; g < g1; ++g) {
@@ -503,14 +513,14 @@ __global__ __launch_bounds__(STHREADS) void merge_segment_kernel(
     fv[b * kprime + i] = key ? key2f(key) : -__builtin_inff();
     fi[b * kprime + i] = key ? (int64_t)(~(uint32_t)comp) : -1;
   }
-  if (tid == 0 && flag) ovf[b] = 1;
+  if (tid == 0 && (flag || tier == 2)) ovf[b] = (ovf_in & ~MERGE_DEFER) | (flag ? 1 : 0);
 }
 
 int merge_segment(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t* cand,
                   int64_t ld_cand, int slots, const uint8_t* counts, int64_t ld_counts,
                   int64_t n_groups,
                   int64_t row_offset, const int64_t* eo, const int64_t* er, int* ovf,
-                  hipStream_t st) {
+                  hipStream_t st, double expect_hits) {
   if (B < 0 || B > 0x7fffffffLL || kprime < 1 || kprime > KPRIME_MAX || n_groups < 1 ||
       n_groups > 0x7fffffffLL || ld_counts < n_groups ||
       ld_cand < n_groups * slots) {
@@ -519,13 +529,30 @@ int merge_segment(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t*
   }
   if (B == 0) return EBT_OK;
   const int P_max = merge_entries(kprime);
-  const size_t lds = (size_t)P_max * 8;
   (void)hipFuncSetAttribute((const void*)merge_segment_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(merge_segment_kernel, dim3((unsigned)B), dim3(STHREADS), lds, st, fv, fi,
-                     kprime, cand, ld_cand, slots, counts, ld_counts, (int)n_groups, P_max,
-                     row_offset,
-                     eo, er, ovf);
+                            hipFuncAttributeMaxDynamicSharedMemorySize, P_max * 8);
+  // with an expected hit count (and an ovf array for the deferral bit): a first pass with room
+  // for 3x the expected hits, at 4+ workgroups per CU instead of 1, then the full-size pass for
+  // the (rare) queries that did not fit
+  int P_small = 2;
+  if (expect_hits > 0.0 && ovf) {
+    const char* mv = getenv("EBT_MERGE_MARGIN");  // tests: 0 defers (nearly) every query
+    const double margin = mv ? atof(mv) : 3.0;
+    const double want = (double)kprime + margin * expect_hits + 256.0;
+    while (P_small < want && P_small < P_max) P_small <<= 1;
+  } else {
+    P_small = P_max;
+  }
+  if (P_small < P_max) {
+    hipLaunchKernelGGL(merge_segment_kernel, dim3((unsigned)B), dim3(STHREADS),
+                       (size_t)P_small * 8, st, fv, fi, kprime, cand, ld_cand, slots, counts,
+                       ld_counts, (int)n_groups, P_small, row_offset, eo, er, ovf, 1);
+    const int rc = launch_check("merge_segment_kernel");
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(merge_segment_kernel, dim3((unsigned)B), dim3(STHREADS), (size_t)P_max * 8,
+                     st, fv, fi, kprime, cand, ld_cand, slots, counts, ld_counts, (int)n_groups,
+                     P_max, row_offset, eo, er, ovf, P_small < P_max ? 2 : 0);
   return launch_check("merge_segment_kernel");
 }
 

@@ -481,6 +481,25 @@ def test_fused_large_kprime_block_path(cuda_device, B):
     assert_topk_equal(s1[sample], r1[sample], s_ref, r_ref)
 
 
+def test_block_merge_deferred_tier(cuda_device, monkeypatch):
+    """The block merge's two tiers: EBT_MERGE_MARGIN=0 sizes the first (small-LDS) pass for
+    k' + 256 entries, so queries with more hits are deferred to the full-size pass; the answer
+    is the same as the unfused path's."""
+    ebt, L = _ebt()
+    n, d, k, B = 400_000, 128, 600, 300
+    c = gaussian(4, n, d, "f16")
+    q = gaussian(5, B, d, "f16")
+    cat = ebt.Catalog(_t(c, "f16", cuda_device))
+    qt = _t(q, "f16", cuda_device)
+    assert ebt.search.plan(cat, B, k)["spec"] is not None
+    s2, r2 = ebt.score_topk(cat, k, queries=qt, fuse=False)
+    for margin in ("0", "3"):
+        monkeypatch.setenv("EBT_MERGE_MARGIN", margin)
+        s1, r1 = ebt.score_topk(cat, k, queries=qt)
+        assert torch.equal(r1, r2), margin
+        torch.testing.assert_close(s1, s2, rtol=0, atol=0)
+
+
 def test_speculative_screen_matches_oracle(cuda_device):
     """The speculative fused screen (pooled sample threshold, one filter pass, verify) on a
     shape where it is the default: bit-exact rows vs the oracle, equal to the unfused path."""
