@@ -166,6 +166,26 @@ struct WsLayout {
 
 constexpr int SPEC_KPRIME_MAX = 2048;
 
+// P(Poisson(lam) > m)
+static double poisson_tail(double lam, int m) {
+  double pmf = exp(-lam), cdf = pmf;
+  for (int i = 1; i <= m; ++i) {
+    pmf *= lam / i;
+    cdf += pmf;
+  }
+  const double t = 1.0 - cdf;
+  // 1 - cdf loses everything below ~1e-16: bound the tail by its first terms instead
+  if (t < 1e-12) {
+    double term = pmf * lam / (m + 1), sum = 0.0;
+    for (int i = m + 1; i < m + 64 && term > 0.0; ++i) {
+      sum += term;
+      term *= lam / (i + 1);
+    }
+    return sum;
+  }
+  return t;
+}
+
 // Speculative screen parameters (see run_screen). The sample: P evenly spaced full 256-row tiles
 // (P = min(64, tiles / 24), so at most ~4 % of the rows are screened twice); lambda = the expected
 // number of sample rows at or above the rank-k' score, taking the sample as a uniform draw of
@@ -200,7 +220,12 @@ static bool spec_params(int64_t B_pad, int64_t n_rows, int32_t kprime, int64_t* 
   if (jj < 1) jj = 1;
   if (jj > (int)(m / 64) / 2) return false;  // the pooled estimate: 4P maxima per query
   *tiles = P;
+  // an odd stride: the sample tiles visit every 256-row phase of 1024-row (and larger
+  // power-of-two) blocks instead of one -- with an even stride a generated catalog whose rows
+  // repeat structure per block was sampled at one phase only (a C4 query got 3.8x its expected
+  // hits from an unrepresentative sample)
   *stride = full / P;
+  if (*stride > 1 && *stride % 2 == 0) *stride -= 1;
   *j = jj;
   // the j-th of the 4P pooled maxima sits ~j^2 / (2 * 4P) sample ranks lower (two of the top j
   // sample rows in one 64-row subgroup count once)
@@ -655,23 +680,47 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
   if (!rc) rc = hip_check(hipMemsetAsync(fi, 0xff, (size_t)B * kprime * 8, st), "hipMemsetAsync");
   if (!rc) rc = hip_check(hipMemsetAsync(ovf, 0, (size_t)B_pad * 4, st), "hipMemsetAsync");
   if (rc) return rc;
-  // hits per 256-row group ~ H 256 / n: slots for 4x that (+4; a group overflow only costs
-  // its query an unfused rerun)
+  // hits per group ~ H group_rows / n (per query; its threshold's own spread ~ 1/sqrt(j) on
+  // top): slots for 4x that + 4, and at least enough that a group overflow (which costs its
+  // query an unfused rerun of the whole catalog) is expected less than once per thousand batches
   const double per_group = spec_hits * (double)L.group_rows / (double)n_rows;
+  const double n_cells = (double)B * (double)ceil_div(n_rows, L.group_rows);
   int slots = 8;
-  while (slots < 4.0 * per_group + 4.0 && slots < EBT_FILTER_SLOTS_MAX) slots *= 2;
+  while (slots < EBT_FILTER_SLOTS_MAX &&
+         (slots < 4.0 * per_group + 4.0 || n_cells * poisson_tail(1.5 * per_group, slots) > 1e-3))
+    slots *= 2;
   const bool wave = merge_wave_fits(kprime);
   int64_t seg_cap = L.ld_cand / slots;
   if (wave) seg_cap = seg_cap < merge_wave_max_groups() ? seg_cap : merge_wave_max_groups();
   seg_cap *= L.group_rows;
   const double cap = (double)(wave ? merge_wave_capacity() : merge_block_capacity(kprime));
+  // A query's hits are ~ Gamma(j) n / m around the expected H = j n / m (its threshold is the
+  // j-th of its own sample): the merge's room beside the list must hold f times the expected
+  // hits, f = the Gamma(j) quantile at 1e-2 / B over its mean (P(Gamma(j) > x) = P(Poisson(x)
+  // < j)), so that an overflow -- an unfused rerun of the query -- is expected less than once
+  // per hundred batches (f = 2.6 at j = 16, B = 4096; 3.0 at j = 12, B = 8192; floor 2.5).
+  double f_spread = 2.5;
+  if (!given && L.spec_j > 0) {
+    const double target = 1e-2 / (double)(B > 0 ? B : 1);
+    double x = (double)L.spec_j;
+    while (x < 8.0 * L.spec_j) {
+      double pmf = exp(-x), cdf = pmf;
+      for (int i = 1; i < L.spec_j; ++i) {
+        pmf *= x / i;
+        cdf += pmf;
+      }
+      if (cdf <= target) break;
+      x += 0.25;
+    }
+    f_spread = x / (double)L.spec_j;
+    f_spread = f_spread < 2.5 ? 2.5 : f_spread;
+  }
   int64_t r0 = 0;
   while (r0 < n_rows) {
-    // expected hits <= 0.4 of the merge's room beside the list (the hit count has a relative
-    // spread of ~1/sqrt(j): an overflow, i.e. an unfused rerun, stays rare). Hits per row: at
+    // expected hits <= 1 / f_spread of the merge's room beside the list. Hits per row: at
     // theta_spec H / n; after r0 rows the raised threshold (the list's k-th - 2 eps) keeps at
     // most ~k' / r0 of the rows. A remainder of less than half a segment joins the last one.
-    const double room = 0.4 * (cap - kprime);
+    const double room = (cap - kprime) / f_spread;
     double rate = spec_hits / (double)n_rows;
     if (r0 > 0 && (double)kprime / (double)r0 < rate) rate = (double)kprime / (double)r0;
     int64_t seg = (int64_t)(room / (rate > 1e-12 ? rate : 1e-12));

@@ -287,6 +287,8 @@ def sample_maxima(catalog: Catalog, qb: QueryBatch, tiles: int,
     """ebt_cosine_sample: `tiles` evenly spaced full 256-row tiles of this catalog (shard)
     through the screening GEMM, keeping the max of every 64-row subgroup: [B_pad, 4 tiles] f32."""
     stride = (catalog.n // 256) // tiles
+    if stride > 1 and stride % 2 == 0:  # odd, as ebt_cosine_topk's own sample (api.hip)
+        stride -= 1
     out = torch.empty((qb.B_pad, 4 * tiles), dtype=torch.float32, device=catalog.device)
     call("ebt_cosine_sample", ptr(qb.qimg), ptr(qb.qscale), qb.B_pad, ptr(catalog.image),
          ptr(catalog.cscale), catalog.img_dtype, catalog.ld_img, catalog.n, catalog.d_pad, tiles,
