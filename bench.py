@@ -201,9 +201,104 @@ def host_boundary(cat, k, q, timer, steps=3):
                     "one step at a time (no overlap); never `value`"}
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` without an external launcher: start N child processes of this same
+    script, one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (the
+    environment torch.distributed.run would give them). Nothing here has touched the GPU: the
+    children are started, never exec'd into. Rank 0's stdout carries the JSON line; the exit
+    status is the first non-zero child status (the remaining ranks are then stopped, since they
+    would wait in a collective forever)."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env, start_new_session=True))
+    log(f"launched {n} ranks (pids {[p.pid for p in procs]}), rendezvous 127.0.0.1:{port}")
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                log(f"rank pid {p.pid} exited with {code}: stopping the other ranks")
+                for q in live:
+                    try:
+                        os.killpg(q.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        time.sleep(0.2)
+    return rc
+
+
+def dry_run(args, world: int, rank: int) -> None:
+    """--dry-run: the multi-rank protocol of a real run on the CPU (gloo), without the GPU
+    path: rendezvous, the world-size check, K barrier-bracketed steps of one small all-gather
+    each, max-over-ranks timing, and rank 0's single JSON line (n_gpus, rccl_world_size and
+    the ranks that reported). CPU test coverage of the launcher (tests/test_bench_launch.py)."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        if dist.get_world_size() != args.gpus:
+            log(f"error: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+            sys.exit(3)
+    got = [rank]
+    t = torch.tensor([float(rank)])
+
+    def step():
+        if world > 1:
+            out = torch.empty(world)
+            dist.all_gather_into_tensor(out, t)
+            return out
+        return t.clone()
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    g = t
+    for _ in range(args.steps):
+        g = step()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+        got = [int(x) for x in g.tolist()]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "queries/s", "n_gpus": world,
+                          "rccl_world_size": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(1e3 * elapsed / max(args.steps, 1), 3),
+                          "dry_run": True, "ranks_reported": sorted(got),
+                          "backend": "gloo" if world > 1 else None}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU/gloo rehearsal of the multi-rank protocol (no GPU work)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C3", choices=sorted(CONFIGS))
@@ -220,16 +315,28 @@ def main() -> None:
     if args.b:
         cfg["b"] = args.b
 
+    if args.gpus < 1:
+        log("error: --gpus must be >= 1")
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no external launcher: this process only starts the ranks (before any GPU call)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={world} (launch N ranks for --gpus N)")
+        sys.exit(2)
+    if args.dry_run:
+        return dry_run(args, world, rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if dist.get_world_size() != args.gpus:
+            log(f"error: RCCL process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+            sys.exit(3)
     dev = torch.device("cuda", local_rank)
 
     import robot_ebert_amd as ebt
@@ -332,6 +439,7 @@ def main() -> None:
             "value": round(value, 3),
             "unit": "queries/s",
             "n_gpus": world,
+            "rccl_world_size": dist.get_world_size() if dist is not None else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3),
@@ -360,6 +468,9 @@ def main() -> None:
                                                 "of the fused screen; averaged over the "
                                                 "segments)"},
                 "all_gemm_tflops": round(all_tf, 2) if all_tf else None,
+                "per_n": "rank 0's own launches of the dominant kernel over its shard "
+                         "(n_local rows); traffic from the committed PMC summary for this "
+                         "config and N (profiles/pmc_<config>_n<N>.json), null when none",
             },
             "plan": pl,
             "stage_ms_per_step": {name: round(v[0], 4) for name, v in st.items()},

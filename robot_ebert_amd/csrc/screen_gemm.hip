@@ -170,13 +170,9 @@ __device__ __forceinline__ void filter_finish(const EpiArgs& e, const uint32_t* 
   // LDS-only barrier: the counters are LDS atomics, the hits are read by a later kernel, so
   // the waves need not wait for their hit stores here (__syncthreads() adds vmcnt(0); measured
   // no difference either way on MI355X -- the hit path's cost is its instructions)
-#if EBT_ABL_SYNCFIN
-  __syncthreads();
-#else
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-#endif
   for (int t = threadIdx.x; t < nq; t += blockDim.x) {
     const uint32_t c = lcnt[t];
     const int64_t q = q0 + t;
@@ -322,32 +318,11 @@ __device__ __forceinline__ void wait_vm_halves(int halves_after) {
 // machine scheduler.
 __device__ __forceinline__ void qp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
-#if EBT_ABL_PRIO == 1
-  __builtin_amdgcn_s_setprio(0);
-#endif
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-#if EBT_ABL_PRIO == 1
-  __builtin_amdgcn_s_setprio(1);
-#endif
   __builtin_amdgcn_sched_barrier(0);
 }
-#ifndef EBT_ABL_PRIO
-#define EBT_ABL_PRIO 0
-#endif
-#ifndef EBT_ABL_NOFINISH
-#define EBT_ABL_NOFINISH 0
-#endif
-#ifndef EBT_ABL_NOEPI
-#define EBT_ABL_NOEPI 0
-#endif
-#ifndef EBT_ABL_NOWAIT
-#define EBT_ABL_NOWAIT 0
-#endif
-#ifndef EBT_ABL_SLEEP
-#define EBT_ABL_SLEEP 1
-#endif
 
 
 // =============================================================================================
@@ -544,7 +519,7 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     const char* nbuf = smem + ((t_ + 1) & 1) * QP_BUF;                                           \
     /* Q1 (A0, B0): read B1(t) */                                                                \
     qp_barrier();                                                                                \
-    if (EBT_ABL_SLEEP && !(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
+    if (!(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
     QP2_ISSUE(4 * t_ + 7, GUARD);                                                                \
     qp2_mma<BF16>(acc0, fa0, s0);                                                                \
     read_b(s1, buf + p_half_off(P_B1));                                                          \
@@ -567,10 +542,10 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
       }                                                                                          \
     }                                                                                            \
-    if (GUARD) wait_for(4 * t_ + 3, 4 * t_ + 7); else if (!EBT_ABL_NOWAIT) wait_vm<8>(); /* A1(t) for Q2 */           \
+    if (GUARD) wait_for(4 * t_ + 3, 4 * t_ + 7); else wait_vm<8>(); /* A1(t) for Q2 */           \
     /* Q2 (A0, B1): read A1(t) */                                                                \
     qp_barrier();                                                                                \
-    if (EBT_ABL_SLEEP && !(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
+    if (!(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
     QP2_ISSUE(4 * t_ + 8, GUARD);                                                                \
     qp2_mma<BF16>(acc1, fa0, s1);                                                                \
     read_a(fa1, buf + p_half_off(P_A1));                                                         \
@@ -595,7 +570,7 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     }                                                                                            \
     /* Q3 (A1, B1): no reads */                                                                  \
     qp_barrier();                                                                                \
-    if (EBT_ABL_SLEEP && !(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
+    if (!(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
     QP2_ISSUE(4 * t_ + 9, GUARD);                                                                \
     qp2_mma<BF16>(acc2, fa1, s1);                                                                \
     if (!(GUARD)) {                                                                              \
@@ -605,10 +580,10 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
       __builtin_amdgcn_sched_group_barrier(0x008, 10, 0);                                        \
     }                                                                                            \
-    if (GUARD) wait_for(4 * t_ + 5, 4 * t_ + 9); else if (!EBT_ABL_NOWAIT) wait_vm<8>(); /* A0(t+1), B0(t+1) for Q4 */\
+    if (GUARD) wait_for(4 * t_ + 5, 4 * t_ + 9); else wait_vm<8>(); /* A0(t+1), B0(t+1) for Q4 */\
     /* Q4 (A1, B0): read A0(t+1), B0(t+1) */                                                     \
     qp_barrier();                                                                                \
-    if (EBT_ABL_SLEEP && !(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
+    if (!(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
     QP2_ISSUE(4 * t_ + 10, GUARD);                                                               \
     qp2_mma<BF16>(acc3, fa1, s0);                                                                \
     if (!(GUARD) || t_ + 1 < ktiles) {                                                           \
@@ -636,12 +611,9 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
       }                                                                                          \
     }                                                                                            \
-    if (GUARD) wait_for(4 * t_ + 6, 4 * t_ + 10); else if (!EBT_ABL_NOWAIT) wait_vm<8>(); /* B1(t+1) for Q1(t+1) */   \
+    if (GUARD) wait_for(4 * t_ + 6, 4 * t_ + 10); else wait_vm<8>(); /* B1(t+1) for Q1(t+1) */   \
   }
 
-#if EBT_ABL_PRIO == 2
-  if (wa) __builtin_amdgcn_s_setprio(1);
-#endif
   int t = 0;
   // steady state: the last half-tile issued by the pair (t, t+1) is 4 (t+1) + 10 < 4 ktiles
   for (; t + 4 < ktiles; t += 2) {
@@ -829,20 +801,6 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
       }
     }
   };
-#if EBT_ABL_NOEPI
-  {  // ablation: no epilogue (keeps every accumulator chain alive)
-    float sum = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) sum += acc0[i][j][v] + acc1[i][j][v] + acc2[i][j][v] + acc3[i][j][v];
-    if (sum == 1234.5678f) e.ovf[0] = 7;
-    (void)store_quadrant;
-    (void)lcnt;
-  }
-#else
   // pool mode: max over the 64 rows (ah, wa) of each query: 4 accumulators x 4 values in the
   // lane, then the 4 lanes of the same fr (lane ^ 16, ^ 32); rows past n_rows are skipped
   auto pool_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh) {
@@ -880,12 +838,7 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     store_quadrant(acc2, 1, 1);
     store_quadrant(acc3, 1, 0);
   }
-#if EBT_ABL_NOFINISH
-  (void)lcnt;
-#else
   if constexpr (FILTER) filter_finish(e, lcnt, q0, QP_TILE, ct);
-#endif
-#endif
 }
 
 
