@@ -136,6 +136,75 @@ def cosine_topk(queries: np.ndarray, catalog: np.ndarray, k: int,
     return out_s, out_r
 
 
+def _chunk_topk(qn: np.ndarray, row0: int, chunk: np.ndarray, k: int,
+                exclude: Optional[Sequence[np.ndarray]]) -> List[Tuple[np.ndarray, np.ndarray]]:
+    """Per-query top-k (ties at the cut kept) of one catalog row block, float64."""
+    c = np.asarray(chunk, dtype=np.float64)
+    s = (qn @ c.T) / zero_guard_norms(row_norms(c))[None, :]   # == normalize(q) . normalize(c)
+    out = []
+    for i in range(s.shape[0]):
+        ex = None
+        if exclude is not None:
+            e = exclude[i]
+            e = e[(e >= row0) & (e < row0 + c.shape[0])] - row0
+            ex = e
+        sc, rw = topk_from_scores(s[i], k, ex)
+        # topk_from_scores cuts at exactly k; keep every value tied with the k-th as well, so a
+        # later merge still orders equal scores by row
+        if sc.shape[0] == k:
+            row = s[i].copy()
+            if ex is not None and len(ex):
+                row[ex] = -np.inf
+            tied = np.nonzero(row == sc[-1])[0]
+            extra = np.setdiff1d(tied, rw, assume_unique=False)
+            if extra.size:
+                sc = np.concatenate([sc, row[extra]])
+                rw = np.concatenate([rw, extra])
+        out.append((sc, rw + row0))
+    return out
+
+
+def cosine_topk_stream(queries: np.ndarray, chunks: Iterable[Tuple[int, np.ndarray]], k: int,
+                       exclude: Optional[Sequence[Iterable[int]]] = None, workers: int = 8
+                       ) -> Tuple[np.ndarray, np.ndarray]:
+    """``cosine_topk`` over a catalog delivered as row blocks ``(row0, rows[r, d])``.
+
+    Same arithmetic as ``cosine_topk`` (lib.py:51 via sklearn normalise + dot, float64; lib.py:55
+    exclusion + (score desc, row asc) top-k), but it never holds the catalog in float64: each
+    block is upcast, scored and reduced to its per-query top-k (all values tied with the k-th
+    kept), and the blocks' lists are merged at the end. This is what lets the tests check the
+    BASELINE workloads (up to 10M x 768 and 6.25M x 1536 per GPU) against the host oracle.
+    Blocks are processed by ``workers`` threads (numpy releases the GIL in upcasts and GEMMs).
+    """
+    from concurrent.futures import ThreadPoolExecutor
+
+    qn = normalize_rows(np.asarray(queries, dtype=np.float64))
+    B = qn.shape[0]
+    ex = None
+    if exclude is not None:
+        ex = [np.asarray(sorted(set(int(v) for v in e)), dtype=np.int64) for e in exclude]
+    parts: List[List[Tuple[np.ndarray, np.ndarray]]] = []
+    workers = max(1, workers)
+    with ThreadPoolExecutor(max_workers=workers) as pool:
+        pending = []
+        for r0, blk in chunks:   # at most 2 x workers blocks in host memory at once
+            pending.append(pool.submit(_chunk_topk, qn, int(r0), blk, k, ex))
+            if len(pending) >= 2 * workers:
+                parts.append(pending.pop(0).result())
+        parts.extend(f.result() for f in pending)
+    out_s = np.full((B, k), np.nan)
+    out_r = np.full((B, k), -1, dtype=np.int64)
+    for b in range(B):
+        if not parts:
+            break
+        s = np.concatenate([p[b][0] for p in parts])
+        r = np.concatenate([p[b][1] for p in parts])
+        o = order_desc(s, r)[:k]
+        out_s[b, :o.shape[0]] = s[o]
+        out_r[b, :o.shape[0]] = r[o]
+    return out_s, out_r
+
+
 def liked_topk(catalog: np.ndarray, liked: Sequence[Sequence[int]], k: int,
                exclude: Optional[Sequence[Iterable[int]]] = None) -> Tuple[np.ndarray, np.ndarray]:
     """Mean-over-liked cosine (lib.py:51-52) + exclusion + top-k (lib.py:55), per user."""

@@ -42,6 +42,7 @@ class RecBatcher:
         self._score = score_fn
         self._q: "queue.Queue" = queue.Queue()
         self._closed = False
+        self._lock = threading.Lock()  # orders submit()'s check-and-put against close()
         self.batches: List[int] = []  # sizes of the batches run (observability / tests)
         self._thread = threading.Thread(target=self._run, name="ebert-batcher", daemon=True)
         self._thread.start()
@@ -51,9 +52,6 @@ class RecBatcher:
         """Queue one user's request; the Future resolves to (scores [k'], rows [k']) numpy arrays
         (k' <= k: fewer when the catalog has fewer candidates) or raises the request's error."""
         fut: Future = Future()
-        if self._closed:
-            fut.set_exception(RuntimeError("batcher is closed"))
-            return fut
         if k < 1:
             fut.set_exception(ValueError("k must be >= 1"))
             return fut
@@ -62,13 +60,21 @@ class RecBatcher:
                 f"Found array with 0 sample(s) (shape=(0, {self.catalog.d})) while a minimum of 1 "
                 "is required by check_pairwise_arrays."))
             return fut
-        self._q.put((list(liked_rows), sorted(set(int(r) for r in exclude_rows)), int(k), fut))
+        item = (list(liked_rows), sorted(set(int(r) for r in exclude_rows)), int(k), fut)
+        with self._lock:   # a request is either queued before close()'s sentinel or refused
+            if self._closed:
+                fut.set_exception(RuntimeError("batcher is closed"))
+                return fut
+            self._q.put(item)
         return fut
 
     def close(self, timeout: Optional[float] = 10.0) -> None:
         """Stop accepting requests, finish the queued ones, join the dispatcher."""
-        self._closed = True
-        self._q.put(_SENTINEL)
+        with self._lock:
+            if self._closed:
+                return
+            self._closed = True
+            self._q.put(_SENTINEL)
         self._thread.join(timeout)
 
     # ---- dispatcher thread ---------------------------------------------------------------------

@@ -36,7 +36,7 @@ from .catalog import Catalog
 from .search import (KPRIME_MAX, _round_up, csr_from_lists, csr_subset, default_kprime,
                      merge_topk, pad_batch, pool_kth, prepare_queries, run_screen,
                      sample_maxima, score_topk, score_topk_finish, score_topk_stages,
-                     score_topk_submit, spec_rank, union_floor, union_floor_gathered)
+                     score_topk_submit, spec_rank, union_floor_gathered)
 
 SAMPLE_TILES_MAX = 64   # per shard, as the single-GPU speculative screen (api.hip spec_params)
 # Larger shards screen at their own sample threshold: there the shard's first segment raises
@@ -224,10 +224,7 @@ def _gathered_floor(coll, vals: torch.Tensor, eps: torch.Tensor, k: int):
     wait = _gather_start(coll, torch.cat([vals, eps[:, None]], 1))
 
     def floor():
-        g = wait()
-        if g.is_cuda:
-            return union_floor_gathered(g, k)
-        return union_floor(g[:, :, :-1], g[:, :, -1], k)
+        return union_floor_gathered(wait(), k)
     return floor
 
 

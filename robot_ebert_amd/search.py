@@ -82,6 +82,25 @@ def csr_from_lists(lists: Sequence[Sequence[int]], device) -> Tuple[torch.Tensor
     return o, r
 
 
+def csr_sorted(off: torch.Tensor, rows: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """A caller's device CSR with every segment sorted ascending (the fused merge drops excluded
+    rows by binary search over the segment, so an unsorted segment would silently keep rated
+    rows). One torch.sort of (segment << 32 | row) keys; rows must lie in [0, 2^32)."""
+    if off.dtype != torch.int64 or rows.dtype != torch.int64:
+        raise EbertError("exclusion CSR must be int64 (offsets, rows)")
+    nnz = int(rows.numel())
+    B = int(off.numel()) - 1
+    if nnz <= 1 or B < 1:
+        return off, rows
+    lens = off[1:] - off[:-1]
+    seg = torch.repeat_interleave(torch.arange(B, device=off.device), lens)
+    if seg.numel() != nnz:          # padded rows past off[-1] keep their place
+        seg = torch.cat([seg, torch.full((nnz - seg.numel(),), B, device=off.device,
+                                         dtype=torch.int64)])
+    key, _ = torch.sort((seg << 32) | (rows & 0xFFFFFFFF))
+    return off, key & 0xFFFFFFFF
+
+
 def csr_subset(off: torch.Tensor, rows: torch.Tensor, idx: torch.Tensor):
     """Rows `idx` of a device CSR (torch ops only; used for the certification retry)."""
     starts = off.index_select(0, idx)
@@ -397,8 +416,9 @@ def score_topk_stages(catalog: Catalog, k: int, queries: Optional[torch.Tensor] 
     dev = catalog.device
     if liked is not None and not isinstance(liked, tuple):
         liked = csr_from_lists(liked, dev)
-    if exclude is not None and not isinstance(exclude, tuple):
-        exclude = csr_from_lists(exclude, dev)
+    if exclude is not None:
+        exclude = (csr_from_lists(exclude, dev) if not isinstance(exclude, tuple)
+                   else csr_sorted(*exclude))
     if theta_hook is not None and t_floor_hook is None:
         raise EbertError("theta_hook needs t_floor_hook (the threshold is verified against it)")
     qb = prepare_queries(catalog, queries=queries, liked=liked, liked_counts=liked_counts,
@@ -530,15 +550,11 @@ def union_floor_gathered(g: torch.Tensor, k: int) -> torch.Tensor:
 
 def union_floor(vals: torch.Tensor, eps: torch.Tensor, k: int) -> torch.Tensor:
     """The k-th largest of vals[r, b, j] - eps[r, b] over all shards r and slots j: a lower bound
-    of query b's k-th best exact score (vals f32 [R, B, k] approx, eps f32 [R, B])."""
-    R, B, kk = vals.shape
-    if vals.is_cuda:   # one kernel (ebt_union_floor) on the device
-        g = torch.cat([vals.float(), eps.float()[:, :, None]], 2).contiguous()
-        return union_floor_gathered(g, k)
-    lo = vals.double() - eps.double()[:, :, None]
-    lo = torch.nan_to_num(lo, nan=float("-inf"), neginf=float("-inf"))
-    lo = lo.permute(1, 0, 2).reshape(B, R * kk)
-    return torch.topk(lo, k, dim=1).values[:, k - 1].contiguous()
+    of query b's k-th best exact score (vals f32 [R, B, k] approx, eps f32 [R, B]); one
+    ebt_union_floor launch on the device (no CPU path: CPU tensors raise EbertError)."""
+    require_cuda(vals, "union_floor vals")
+    g = torch.cat([vals.float(), eps.float()[:, :, None]], 2).contiguous()
+    return union_floor_gathered(g, k)
 
 
 def _screen_global_cut(catalog: Catalog, qb: QueryBatch, k: int, k_req: int, kprime: int,

@@ -85,7 +85,7 @@ def _body(rank, world, q):
                                                     for r in range(world))
         # the per-shard path's global cut: union_floor of the gathered (approx, eps) lists is a
         # lower bound of the global k-th exact score, and no shard cuts a global top-k row
-        from robot_ebert_amd.search import union_floor
+        from floor_ref import union_floor_torch as union_floor
         vals = torch.from_numpy(np.nan_to_num(s, nan=-np.inf).astype(np.float32))
         eps = torch.full((vals.shape[0],), 1e-6, dtype=torch.float32)
         floor = union_floor(coll.all_gather(vals), coll.all_gather(eps), k).numpy()

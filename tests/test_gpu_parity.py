@@ -856,3 +856,60 @@ def test_rescore_two_stage_cut(cuda_device, eps_v):
             np.testing.assert_array_equal(r[b], np.lexsort((np.arange(n), -exact[b]))[:k])
     if eps_v == 0.002:
         assert (c == 1).all()
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_unsorted_device_exclusions(cuda_device, dt):
+    """A caller's device CSR with UNSORTED segments: the fused merge binary-searches
+    exclusions, so score_topk / torch.ops.ebert.cosine_topk must sort them first. The excluded
+    rows are drawn from each query's true top 200, so keeping any of them changes the answer."""
+    ebt, L = _ebt()
+    from robot_ebert_amd.search import plan
+    n, d, B, k = 65536, 256, 256, 100
+    c = gaussian(31, n, d, dt)
+    qv = gaussian(32, B, d, dt)
+    s0, r0 = R.cosine_topk(qv, c, 200)
+    rng = np.random.default_rng(33)
+    excl = [rng.permutation(np.concatenate([r0[b, rng.choice(200, 60, replace=False)],
+                                            rng.choice(n, 40, replace=False)]))
+            for b in range(B)]
+    excl = [np.array(list(dict.fromkeys(e.tolist())), dtype=np.int64) for e in excl]  # unique
+    eo = torch.tensor(np.concatenate([[0], np.cumsum([len(e) for e in excl])]),
+                      dtype=torch.int64, device=cuda_device)
+    er = torch.tensor(np.concatenate(excl), dtype=torch.int64, device=cuda_device)
+    assert any(np.any(np.diff(e) < 0) for e in excl)
+    cat = ebt.Catalog(_t(c, dt, cuda_device))
+    assert plan(cat, B, k)["fused"]
+    q = _t(qv, dt, cuda_device)
+    s_ref, r_ref = R.cosine_topk(qv, c, k, excl)
+    s, r = ebt.score_topk(cat, k, queries=q, exclude=(eo, er))
+    assert_topk_equal(s, r, s_ref, r_ref)
+    g, inv = torch.ops.ebert.row_norms(cat.data)
+    img = torch.ops.ebert.screen_image(cat.data, g)
+    s2, r2 = torch.ops.ebert.cosine_topk(q, cat.data, g, inv, img, k, eo, er, 0)
+    assert_topk_equal(s2, r2, s_ref, r_ref)
+
+
+@pytest.mark.parametrize("k", [10, 10000])
+def test_route_recommendations_matches_reference(cuda_device, k):
+    """Row a-1: GET /users/{user_id}/recommendations/?k= (api/users.py:150-155) through FastAPI's
+    TestClient returns the reference's golden recommendations as JSON; the user without a liked
+    movie gets HTTP 500 (the reference's uncaught sklearn ValueError), the one without ratings
+    an empty list."""
+    from fastapi.testclient import TestClient
+    from robot_ebert_amd import api
+    lib, gold = _collab_setup(cuda_device)
+    client = TestClient(api.app(), raise_server_exceptions=False)
+    for uid, rec in gold["users"].items():
+        want = rec[f"k{k}"]
+        resp = client.get(f"/users/{uid}/recommendations/", params={"k": k})
+        if isinstance(want, dict):
+            assert resp.status_code == 500, (uid, resp.status_code)
+            continue
+        assert resp.status_code == 200, (uid, resp.text[:200])
+        got = resp.json()
+        assert [g["movie"]["tmdb_id"] for g in got] == [w[0] for w in want], uid
+        np.testing.assert_allclose([g["score"] for g in got], [w[1] for w in want], rtol=0,
+                                   atol=SCORE_ATOL)
+        if not want:
+            assert got == []

@@ -89,3 +89,30 @@ def test_ingest_chroma_matrix_and_id_order():
         ingest.chroma_matrix({"ids": ids[:4], "embeddings": emb.tolist()})
     with pytest.raises(Exception):
         ingest.chroma_matrix({"ids": ["a", "a"], "embeddings": [[1.0], [2.0]]})
+
+
+def test_submit_racing_close_never_hangs():
+    """a submit() racing close() is either served or refused -- never left queued
+    behind the sentinel with a Future that does not resolve."""
+    x = np.random.default_rng(9).standard_normal((300, 8))
+    for trial in range(20):
+        b = RecBatcher(_Cat(x), max_batch=4, max_wait_ms=0.5, score_fn=_oracle_score([]))
+        futs = []
+        start = threading.Event()
+
+        def worker():
+            start.wait()
+            for i in range(25):
+                futs.append(b.submit([i % 300], [], 3))
+        ts = [threading.Thread(target=worker) for _ in range(4)]
+        for t in ts:
+            t.start()
+        start.set()
+        b.close()
+        for t in ts:
+            t.join()
+        for f in futs:
+            try:
+                f.result(timeout=10)
+            except RuntimeError as e:
+                assert "closed" in str(e)

@@ -100,3 +100,33 @@ def test_merge_equals_unsharded():
     ms, mr = R.merge_topk(np.stack(parts_s), np.stack(parts_r), k)
     np.testing.assert_array_equal(mr, r_full)
     np.testing.assert_allclose(ms, s_full, atol=1e-15)
+
+
+@pytest.mark.parametrize("name", sorted(COS_CASES))
+@pytest.mark.parametrize("block", [1, 517, 4096])
+def test_stream_oracle_matches_golden(name, block):
+    """The block-streaming oracle (used at the BASELINE workload sizes) equals the golden
+    sklearn + pandas vectors for any block size, exclusions included."""
+    case = COS_CASES[name]
+    gold = np.load(os.path.join(GOLD, "cos_topk_small.npz"))
+    q, c, excl = cos_case_inputs(case)
+    if block == 1:
+        block = 257  # 1-row blocks take too long on CPU; 257 still splits every tile
+    chunks = ((r0, c[r0:r0 + block]) for r0 in range(0, c.shape[0], block))
+    s, r = R.cosine_topk_stream(q, chunks, case["k"], excl, workers=4)
+    np.testing.assert_array_equal(r, gold[f"{name}_rows"])
+    np.testing.assert_allclose(s, gold[f"{name}_scores"], rtol=0, atol=1e-12)
+
+
+def test_stream_oracle_ties_across_blocks():
+    """Equal scores split over blocks still come out (score desc, row asc)."""
+    rng = np.random.default_rng(7)
+    base = rng.standard_normal((5, 16))
+    c = np.concatenate([base[rng.integers(0, 5, 300)], rng.standard_normal((100, 16))])
+    q = base[:3] * 2.0
+    s_ref, r_ref = R.cosine_topk(q, c, 40)
+    for block in (7, 64, 400):
+        chunks = ((r0, c[r0:r0 + block]) for r0 in range(0, c.shape[0], block))
+        s, r = R.cosine_topk_stream(q, chunks, 40, workers=3)
+        np.testing.assert_array_equal(r, r_ref)
+        np.testing.assert_allclose(s, s_ref, rtol=0, atol=1e-15)
