@@ -42,6 +42,14 @@ def _rows(kind: str, n: int, d: int, seed: int, dev) -> torch.Tensor:
     raise ValueError(kind)
 
 
+def _fit(x: torch.Tensor, dt: str) -> torch.Tensor:
+    """Cast to the test dtype; f16 holds |x| <= 65504, so Cauchy tails are clamped to stay finite
+    (an inf row has no cosine)."""
+    if dt == "f16":
+        x = x.clamp(-6e4, 6e4)
+    return x.to(TDT[dt])
+
+
 def _max_ratio(cat, qb, dev) -> float:
     from robot_ebert_amd import _lib as L
     B, B_pad = qb.B, qb.B_pad
@@ -87,9 +95,9 @@ def test_screen_error_within_eps(cuda_device, kind, cdt, qdt, d, n, B):
     import robot_ebert_amd as ebt
     from robot_ebert_amd.search import prepare_queries
     dev = cuda_device
-    cat = ebt.Catalog(_rows(kind, n, d, 101, dev).to(TDT[cdt]))
+    cat = ebt.Catalog(_fit(_rows(kind, n, d, 101, dev), cdt))
     # queries: half drawn like the catalog, half copies of catalog rows (s close to 1)
-    qa = _rows(kind, B // 2, d, 202, dev)
+    qa = _fit(_rows(kind, B // 2, d, 202, dev), qdt).float()
     qc = cat.data[torch.arange(B - B // 2, device=dev) * 7 % n].float()
     q = torch.cat([qa, qc]).to(TDT[qdt])
     qb = prepare_queries(cat, queries=q)
@@ -149,20 +157,27 @@ def mfma_probe_values(dev):
 
 
 def test_mfma_accumulation_rounding(cuda_device):
-    """Measured on MI355X (tools/mfma_rounding.py, profiles/r2/mfma_rounding.json): the result in
-    ulps of 1.0 for each probe. Whatever the mode, the bound's accumulation term
-    (d+8) 2^-24 (|q|+1) covers truncating adds for |q| <= 1; this test
-    pins the mode so a change of hardware / compiler behaviour is seen."""
+    """Measured on MI355X (tools/mfma_rounding.py, profiles/r2/mfma_rounding.json), in ulps of
+    1.0 above 1.0: r0 = 6, r1 = 0, r2 = 1, r3 = 0, r4 = 0. Model that fits every probe: inside
+    one v_mfma_f32_16x16x32_f16 the 32 products are summed in groups of 8 (one 8-wide k chunk),
+    each product truncated to the f32 grid of its group's largest product (r0: the group
+    holding 1.0 drops its 7 small products, the other 3 groups add 2 ulps each; r1, r3: the
+    sub-ulp products vanish), and the sum is added to the accumulator C rounding to nearest even
+    (r2: +0.75 -> 1; r4: +0.5 tie -> even). Error per MFMA <= 8 ulp(max product of a group) per
+    group + one rounding of C, so over d = 32 m products
+    |acc - exact| <= (2^-20 + m 2^-24) sum|p_i| <= (16 + d/32) 2^-24 |q||c|,
+    which the bound's accumulation term (d + 8) 2^-24 (|q| + 1) covers for every d >= 32
+    (DESIGN.md section 3). This test pins the measured behaviour so a change of hardware or
+    compiler is seen."""
     got = mfma_probe_values(cuda_device)
     print("mfma probes (ulps above 1.0):", got)
     exact = {"r0": 7.75, "r1": 0.75, "r2": 0.75, "r3": 0.5, "r4": 0.5}
     for name, v in got.items():
-        # every result is a representable neighbour of the exact sum (error < 1 ulp) ...
-        assert abs(v - exact[name]) < 1.0, (name, v)
+        # every result is on the f32 grid and inside the model's error (< 8 ulps per group)
         assert v == int(v), (name, v)
-    # ... and the measured mode (see the docstring) is reproduced exactly
+        assert abs(v - exact[name]) < 8.0, (name, v)
     assert got == MFMA_MEASURED, got
 
 
-# Filled in from the first MI355X run of tools/mfma_rounding.py (profiles/r2/mfma_rounding.json).
-MFMA_MEASURED = None
+# From the first MI355X run of tools/mfma_rounding.py (profiles/r2/mfma_rounding.json).
+MFMA_MEASURED = {"r0": 6.0, "r1": 0.0, "r2": 1.0, "r3": 0.0, "r4": 0.0}
