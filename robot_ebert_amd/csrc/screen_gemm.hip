@@ -519,7 +519,6 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     const char* nbuf = smem + ((t_ + 1) & 1) * QP_BUF;                                           \
     /* Q1 (A0, B0): read B1(t) */                                                                \
     qp_barrier();                                                                                \
-    if (!(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
     QP2_ISSUE(4 * t_ + 7, GUARD);                                                                \
     qp2_mma<BF16>(acc0, fa0, s0);                                                                \
     read_b(s1, buf + p_half_off(P_B1));                                                          \
@@ -545,7 +544,6 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     if (GUARD) wait_for(4 * t_ + 3, 4 * t_ + 7); else wait_vm<8>(); /* A1(t) for Q2 */           \
     /* Q2 (A0, B1): read A1(t) */                                                                \
     qp_barrier();                                                                                \
-    if (!(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
     QP2_ISSUE(4 * t_ + 8, GUARD);                                                                \
     qp2_mma<BF16>(acc1, fa0, s1);                                                                \
     read_a(fa1, buf + p_half_off(P_A1));                                                         \
@@ -570,7 +568,6 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     }                                                                                            \
     /* Q3 (A1, B1): no reads */                                                                  \
     qp_barrier();                                                                                \
-    if (!(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
     QP2_ISSUE(4 * t_ + 9, GUARD);                                                                \
     qp2_mma<BF16>(acc2, fa1, s1);                                                                \
     if (!(GUARD)) {                                                                              \
@@ -583,7 +580,6 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
     if (GUARD) wait_for(4 * t_ + 5, 4 * t_ + 9); else wait_vm<8>(); /* A0(t+1), B0(t+1) for Q4 */\
     /* Q4 (A1, B0): read A0(t+1), B0(t+1) */                                                     \
     qp_barrier();                                                                                \
-    if (!(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \
     QP2_ISSUE(4 * t_ + 10, GUARD);                                                               \
     qp2_mma<BF16>(acc3, fa1, s0);                                                                \
     if (!(GUARD) || t_ + 1 < ktiles) {                                                           \

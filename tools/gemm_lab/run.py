@@ -1,0 +1,100 @@
+"""Interleaved timing of screening-GEMM variants (_abl/libebert_<name>.so) in ONE process.
+
+    python tools/gemm_lab/run.py [--n 327680] [--b 4096] [--d 1536] [--rounds 5] names...
+
+Each library is loaded with its own ctypes handle; every round times every variant (10
+back-to-back launches after 3 warm-up launches, hipEvents on torch's current stream, which is
+the stream the calls launch on). Filter epilogue at a 3-sigma threshold (~0.13 % of scores kept,
+~430 hits per query per 327680 rows: the C3 regime) and with no hits (threshold +inf). Prints
+one JSON line per variant: median / min ms and TFLOP/s (2 B N d per launch)."""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+VP, I32, I64, INT = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int
+
+
+def load(name):
+    lib = ctypes.CDLL(os.path.join(ROOT, "_abl", f"libebert_{name}.so"))
+    f = lib.ebt_screen_filter
+    f.argtypes = [VP, I64, VP, I64, I32, I32, INT, VP, VP, VP, VP, I64, I32, VP, I64, VP, I64, VP]
+    f.restype = INT
+    lib.ebt_last_error.restype = ctypes.c_char_p
+    return lib
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=327680)
+    ap.add_argument("--b", type=int, default=4096)
+    ap.add_argument("--d", type=int, default=1536)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("names", nargs="+")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    B, N, d = a.b, a.n, a.d
+    q = torch.randn((B, d), generator=g, device=dev).half()
+    c = torch.randn((N, d), generator=g, device=dev).half()
+    qs = torch.ones(B, device=dev)
+    thr3 = torch.full((B,), 3.0 * d ** 0.5, device=dev)
+    thri = torch.full((B,), float("inf"), device=dev)
+    G, slots = 256, 32
+    groups = (N + G - 1) // G
+    cand = torch.empty((B, groups * slots), dtype=torch.int64, device=dev)
+    counts = torch.empty((B, groups), dtype=torch.uint8, device=dev)
+    ovf = torch.zeros(B, dtype=torch.int32, device=dev)
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    libs = {n: load(n) for n in a.names}
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def launch(lib, thr):
+        rc = lib.ebt_screen_filter(P(q), B, P(c), N, d, d, 2, P(qs), None, P(thr), P(cand),
+                                   groups * slots, slots, P(counts), groups, P(ovf), 0, st)
+        if rc:
+            raise RuntimeError(lib.ebt_last_error().decode())
+
+    def timed(lib, thr):
+        for _ in range(3):
+            launch(lib, thr)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.iters):
+            launch(lib, thr)
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / a.iters
+
+    res = {n: {"hits": [], "nohit": []} for n in a.names}
+    hits_per_q = None
+    ref = None
+    same = {}
+    for r in range(a.rounds):
+        for n in a.names:
+            res[n]["hits"].append(timed(libs[n], thr3))
+            if hits_per_q is None:
+                hits_per_q = float(counts.float().sum(1).mean())
+            if r == 0:   # the per-(query, group) hit counts must not depend on the variant
+                if ref is None:
+                    ref = counts.clone()
+                same[n] = bool(torch.equal(ref, counts))
+            res[n]["nohit"].append(timed(libs[n], thri))
+    fl = 2.0 * B * N * d
+    for n in a.names:
+        out = {"variant": n, "shape": [B, N, d], "hits_per_query": hits_per_q,
+               "counts_equal_first": same.get(n)}
+        for kind, v in res[n].items():
+            med = statistics.median(v)
+            out[kind] = {"median_ms": round(med, 4), "min_ms": round(min(v), 4),
+                         "tflops_median": round(fl / med / 1e9, 1)}
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

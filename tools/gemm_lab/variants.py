@@ -1,0 +1,84 @@
+"""Screening-GEMM experiments: source patches of csrc/screen_gemm.hip, built into separate
+libraries (_abl/libebert_<name>.so, never shipped) and timed against each other by run.py in
+ONE process, interleaved (cdna_hip_programming.md section 5.4 rule 24). A variant that wins is
+folded into csrc/screen_gemm.hip by hand; the shipping source carries no ablation switches.
+
+    python tools/gemm_lab/variants.py build [names...]   # on the CPU container
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+CSRC = os.path.join(ROOT, "robot_ebert_amd", "csrc")
+OUT = os.path.join(ROOT, "_abl")
+
+STAGGER = "    if (!(GUARD) && wa) __builtin_amdgcn_s_sleep(1); /* stagger 2nd wave */    \\\n"
+
+
+def _sub(src, old, new, count=None):
+    n = src.count(old)
+    if n == 0 or (count is not None and n != count):
+        raise SystemExit(f"patch anchor found {n} times: {old[:60]!r}")
+    return src.replace(old, new)
+
+
+def nosleep(src):
+    # adopted in csrc/screen_gemm.hip (r2: +2.7 % with hits, +3.7 % without, interleaved)
+    return src.replace(STAGGER, "")
+
+
+def prio_static(src):
+    src = nosleep(src)
+    return _sub(src, "  int t = 0;\n  // steady state", "  if (wa) __builtin_amdgcn_s_setprio(1);\n"
+                "  int t = 0;\n  // steady state", 1)
+
+
+def prio_static_sleep(src):
+    src = _sub(src, "    QP2_ISSUE(4 * t_ + 7", "    if (!(GUARD) && wa) __builtin_amdgcn_s_sleep(1);"
+               " \\\n    QP2_ISSUE(4 * t_ + 7", 1)
+    return _sub(src, "  int t = 0;\n  // steady state", "  if (wa) __builtin_amdgcn_s_setprio(1);\n"
+                "  int t = 0;\n  // steady state", 1)
+
+
+def grp(n):
+    def f(src):
+        return _sub(nosleep(src), "constexpr int QP_GROUP_C = 4;", f"constexpr int QP_GROUP_C = {n};", 1)
+    return f
+
+
+VARIANTS = {"grp2": grp(2), "grp8": grp(8), "grp16": grp(16),"base": lambda s: s, "nosleep": nosleep, "prio_static": prio_static,
+            "prio_static_sleep": prio_static_sleep}
+
+
+def build(name):
+    src = open(os.path.join(CSRC, "screen_gemm.hip")).read()
+    src = VARIANTS[name](src)
+    base = os.path.join("/tmp", "gemm_lab", name)
+    work = os.path.join(base, "x", "csrc")   # common.h includes ../../include/ebert.h
+    os.makedirs(work, exist_ok=True)
+    if not os.path.exists(os.path.join(base, "include")):
+        os.symlink(os.path.join(ROOT, "include"), os.path.join(base, "include"))
+    shutil.copy(os.path.join(CSRC, "common.h"), work)
+    with open(os.path.join(work, "screen_gemm.hip"), "w") as f:
+        f.write(src)
+    obj = os.path.join(work, "screen_gemm.o")
+    flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wall",
+             "-Wno-unused-function", "-I" + os.path.join(ROOT, "include")]
+    subprocess.run(["/opt/rocm/bin/hipcc"] + flags + ["-c", os.path.join(work, "screen_gemm.hip"),
+                                                      "-o", obj], check=True)
+    others = [os.path.join(CSRC, "build", f) for f in
+              ("api.o", "select_topk.o", "prep.o", "rescore.o", "als.o")]
+    os.makedirs(OUT, exist_ok=True)
+    lib = os.path.join(OUT, f"libebert_{name}.so")
+    subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "--offload-arch=gfx950", "-o", lib, obj]
+                   + others + ["-Wl,-rpath,/opt/rocm/lib"], check=True)
+    print("built", lib)
+
+
+if __name__ == "__main__":
+    if len(sys.argv) < 2 or sys.argv[1] != "build":
+        raise SystemExit(__doc__)
+    for n in (sys.argv[2:] or list(VARIANTS)):
+        build(n)
