@@ -79,7 +79,10 @@ def host_info() -> dict:
                     break
     except OSError:
         pass
-    return {"nproc": cores, "cpu_count_machine": os.cpu_count(), "cpu_model": model}
+    return {"nproc": cores, "cpu_count_machine": os.cpu_count(), "cpu_model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "note": "nproc = CPUs in this process's affinity mask; the GPU box grants a share "
+                    "of 16 (OMP_NUM_THREADS), which is what the BLAS threads use"}
 
 
 def blas_threads() -> int:

@@ -205,12 +205,12 @@ int ebt_screen_exact(const double* q64, int64_t B, int32_t d, const void* cat, i
 #define EBT_FLAG_EXACT 2
 #define EBT_FLAG_THETA 4 /* internal: set by ebt_cosine_screen_at (workspace sizing only) */
 #define EBT_EXACT_EPS 1.1920928955078125e-07f /* 2^-23 >= f32 rounding of |s| <= 1 + f64 error */
-/* How ebt_cosine_topk will run these sizes (host pointers out): head rows screened unfused,
+/* How ebt_cosine_topk_prepared will run these sizes (host pointers out): head rows screened unfused,
  * the largest fused tail segment in rows (cap; 0 = not fused), score chunk rows, fused flag. */
 int ebt_cosine_topk_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
                          int64_t chunk_rows, int flags, int64_t* head_rows, int64_t* cap,
                          int64_t* chunk, int32_t* fused);
-/* The speculative fused screen ebt_cosine_topk uses for these sizes (all 0: not used).
+/* The speculative fused screen ebt_cosine_topk_prepared uses for these sizes (all 0: not used).
  * sample_tiles full 256-row tiles, tile_stride tiles apart (tiles 0, s, 2s, ...), go through the
  * screening GEMM keeping only each query's max per 64-row subgroup; the rank-th largest of those
  * maxima is the query's speculative threshold theta for one filter pass over the whole catalog;
@@ -219,11 +219,12 @@ int ebt_cosine_topk_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprim
 int ebt_cosine_topk_spec_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
                               int flags, int64_t* sample_tiles, int64_t* tile_stride,
                               int32_t* rank, double* hits);
-/* Workspace bytes needed by ebt_cosine_topk for these sizes. */
+/* Workspace bytes needed by ebt_cosine_topk_prepared for these sizes. */
 size_t ebt_cosine_topk_workspace(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
                                  int64_t chunk_rows, int flags);
 
-/* Query x catalog cosine top-k over one (shard of a) catalog:
+/* The prepared-query pipeline under ebt_cosine_topk (one pass, no retries): query x catalog
+ * cosine top-k over one (shard of a) catalog:
  *   unfused: for every catalog chunk of chunk_rows rows: screening GEMM -> mask excluded ->
  *   streaming select of kprime candidates; then a select across chunks; then the exact float64
  *   rescore.
@@ -245,7 +246,7 @@ size_t ebt_cosine_topk_workspace(int64_t B, int64_t B_pad, int64_t n_rows, int32
  * NULL, ld_img, d_pad), exclusions as CSR of GLOBAL rows (NULL = none), k <= kprime.
  * Outputs: out_scores (float64 [B][k]), out_rows (int64 [B][k], global), certified (int32 [B]).
  * timer (NULL or an ebt_timer) collects per-stage GPU time. */
-int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, const float* eps,
+int ebt_cosine_topk_prepared(const double* q64, const void* qimg, const float* qscale, const float* eps,
                     int64_t B, int64_t B_pad, const void* cat, int dtype, int64_t ld,
                     const double* gnorm64, const void* cimg, const float* cscale, int img_dtype,
                     int32_t ld_img, int64_t n_rows, int32_t d, int32_t d_pad, int64_t row_offset,
@@ -254,8 +255,100 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
                     double* out_scores, int64_t* out_rows, int32_t* certified, void* timer,
                     void* stream);
 
+/* ---- the self-contained path: one call per batch ------------------
+ * What a non-Python caller binds (cgo / JNI / N-API / ctypes): raw queries
+ * in, certified float64 top-k out; query prep, the screen, the certificate check and every
+ * retry (fused-list overflow -> unfused rerun, uncertified -> k' x 4 -> float64 screen) run
+ * inside the library. Replaces /root/reference/src/backend/app/lib.py:51-55 (cosine_similarity
+ * of the liked rows against the catalog, mean over them, exclusion of rated rows, descending
+ * sort, [:k]) for a batch of users, and constants.py:55-56 (the resident catalog).
+ *
+ * ebt_catalog: the resident (shard of a) catalog, filled by ebt_catalog_init from the caller's
+ * device matrix and a caller-provided device STATE buffer of ebt_catalog_state_bytes() bytes
+ * (float64 guarded row norms, float32 inverse norms, and the f16 screening image unless the
+ * matrix itself is the MFMA operand: f16 / bf16 with d, ld % 64 == 0). Immutable afterwards;
+ * the struct and the state buffer must outlive every call that uses them. */
+typedef struct ebt_catalog {
+  const void* data;       /* [n][ld] of dtype (device, caller-owned)                        */
+  int32_t dtype, d;
+  int64_t n, ld, row_offset; /* row_offset: global id of local row 0 (row-sharded catalogs)  */
+  double* gnorm64;        /* [n]                   (state)                                  */
+  float* inv32;           /* [round_up(n, 128)]    (state)                                  */
+  const void* image;      /* [n][ld_img] f16/bf16  (state, or `data` itself)                */
+  const float* cscale;    /* epilogue row scales: inv32 for native images, NULL otherwise   */
+  int32_t img_dtype, ld_img, d_pad, native;
+  float u_cat;            /* unit round-off of the image (0: exact native values)           */
+} ebt_catalog;
+
+size_t ebt_catalog_state_bytes(const void* data, int dtype, int64_t n, int32_t d, int64_t ld);
+int ebt_catalog_init(ebt_catalog* cat, const void* data, int dtype, int64_t n, int32_t d,
+                     int64_t ld, int64_t row_offset, void* state, size_t state_bytes,
+                     void* stream);
+
+/* Optional knobs (NULL = defaults; a zero field = its default): kprime = the screen's candidate
+ * count k' (default: k + slack for the image's error band), chunk_rows = catalog rows per
+ * materialised score chunk of the unfused path (default: 4 GiB of f32 scores),
+ * flags = EBT_FLAG_NO_FUSE to disable the fused screen. Results do not depend on them. */
+typedef struct ebt_options {
+  int32_t kprime;
+  int32_t flags;
+  int64_t chunk_rows;
+} ebt_options;
+
+/* Device workspace bytes ebt_cosine_topk needs for a batch of B queries and top-k
+ * (0 = invalid arguments). */
+size_t ebt_workspace_bytes(const ebt_catalog* cat, int64_t B, int32_t k, const ebt_options* opt);
+
+/* Top-k by cosine for B queries, ordered (score desc, row asc), rows GLOBAL ids.
+ * Queries: EITHER dense q [B][ldq] of q_dtype (EBT_F32 / F64 / BF16 / F16; a zero row scores
+ * 0 against everything, sklearn's zero-norm guard), OR liked rows (q = NULL): CSR liked_off
+ * [B+1] / liked_rows (GLOBAL rows of this catalog) and the query of user b is the mean of its
+ * liked rows' normalised vectors (lib.py:51-52). A user with no liked row fails with
+ * EBT_EINVAL and sklearn's message ("Found array with 0 sample(s) ..."), as the reference
+ * raises ValueError; a liked row outside the catalog fails with EBT_EINVAL.
+ * Exclusions (the rated movies, lib.py:48,55): CSR excl_off [B+1] / excl_rows of GLOBAL rows,
+ * each segment sorted ascending (checked: EBT_EINVAL otherwise), or both NULL.
+ * Output: out_scores float64 [B][k] (within 1e-12 of the float64 reference), out_rows int64
+ * [B][k]; slots past the catalog's candidates (k > n minus exclusions) are NaN / -1.
+ * ebt_cosine_topk synchronises the stream once (the certificates) and returns when the results
+ * are final. The two halves let a caller overlap batches: _submit enqueues the first pass
+ * (no synchronisation for dense queries; the liked path reads its CSR offsets on the host) and
+ * fills the caller's ebt_pending; _finish waits for THAT batch only (an event), reads its
+ * certificates from cert_host (host memory, B + 1 int32; pinned memory keeps the copy
+ * asynchronous) and runs the retries. Workspace, outputs and cert_host stay in use until
+ * _finish returns. timer: NULL or an ebt_timer. */
+typedef struct ebt_pending {
+  const ebt_catalog* cat;
+  ebt_options opt;
+  int64_t B, B_pad, chunk;
+  int32_t k, k_eff, kprime, flags;
+  const int64_t* excl_off;
+  const int64_t* excl_rows;
+  char* ws;
+  size_t ws_bytes;
+  double* out_scores;
+  int64_t* out_rows;
+  int32_t* cert_host;
+  void* event;
+  void* timer;
+  void* stream;
+} ebt_pending;
+int ebt_cosine_topk(const ebt_catalog* cat, const void* q, int q_dtype, int64_t B, int64_t ldq,
+                    const int64_t* liked_off, const int64_t* liked_rows, int32_t k,
+                    const int64_t* excl_off, const int64_t* excl_rows, const ebt_options* opt,
+                    void* workspace, size_t ws_bytes, double* out_scores, int64_t* out_rows,
+                    void* timer, void* stream);
+int ebt_cosine_topk_submit(const ebt_catalog* cat, const void* q, int q_dtype, int64_t B,
+                           int64_t ldq, const int64_t* liked_off, const int64_t* liked_rows,
+                           int32_t k, const int64_t* excl_off, const int64_t* excl_rows,
+                           const ebt_options* opt, void* workspace, size_t ws_bytes,
+                           double* out_scores,
+                           int64_t* out_rows, int32_t* cert_host, ebt_pending* pending,
+                           void* timer, void* stream);
+int ebt_cosine_topk_finish(ebt_pending* pending);
+
 /* ---- two-phase top-k over a row-sharded catalog (robot_ebert_amd/distributed.py) ---------
- * Phase 1, every rank: ebt_cosine_screen = ebt_cosine_topk without the rescore: the shard's k'
+ * Phase 1, every rank: ebt_cosine_screen = ebt_cosine_topk_prepared without the rescore: the shard's k'
  * best approx candidates, list_vals (f32) / list_rows (GLOBAL, -1 empty) [B][kprime]
  * partitioned at k as ebt_merge_hits describes (sorted when the unfused path ran),
  * ovf_out[b] = 1 when the fused screen overflowed for b, eps_out = the eps the certificate

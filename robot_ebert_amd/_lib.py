@@ -33,7 +33,40 @@ class EbertError(RuntimeError):
 _VP, _I32, _I64, _SZ, _F32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t, ctypes.c_float
 _INT = ctypes.c_int
 
+class EbtCatalog(ctypes.Structure):
+    """include/ebert.h `ebt_catalog` (filled by ebt_catalog_init)."""
+    _fields_ = [("data", _VP), ("dtype", _I32), ("d", _I32), ("n", _I64), ("ld", _I64),
+                ("row_offset", _I64), ("gnorm64", _VP), ("inv32", _VP), ("image", _VP),
+                ("cscale", _VP), ("img_dtype", _I32), ("ld_img", _I32), ("d_pad", _I32),
+                ("native", _I32), ("u_cat", _F32)]
+
+
+class EbtOptions(ctypes.Structure):
+    """include/ebert.h `ebt_options` (zero fields = defaults)."""
+    _fields_ = [("kprime", _I32), ("flags", _I32), ("chunk_rows", _I64)]
+
+
+class EbtPending(ctypes.Structure):
+    """include/ebert.h `ebt_pending`: a submitted batch (ebt_cosine_topk_submit / _finish)."""
+    _fields_ = [("cat", _VP), ("opt", EbtOptions), ("B", _I64), ("B_pad", _I64),
+                ("chunk", _I64), ("k", _I32), ("k_eff", _I32), ("kprime", _I32),
+                ("flags", _I32), ("excl_off", _VP), ("excl_rows", _VP), ("ws", _VP),
+                ("ws_bytes", _SZ), ("out_scores", _VP), ("out_rows", _VP), ("cert_host", _VP),
+                ("event", _VP), ("timer", _VP), ("stream", _VP)]
+
+
+_PCAT, _POPT, _PPEND = (ctypes.POINTER(EbtCatalog), ctypes.POINTER(EbtOptions),
+                        ctypes.POINTER(EbtPending))
+
 _SIGNATURES = {
+    "ebt_catalog_state_bytes": ([_VP, _INT, _I64, _I32, _I64], _SZ),
+    "ebt_catalog_init": ([_PCAT, _VP, _INT, _I64, _I32, _I64, _I64, _VP, _SZ, _VP], _INT),
+    "ebt_workspace_bytes": ([_PCAT, _I64, _I32, _POPT], _SZ),
+    "ebt_cosine_topk": ([_PCAT, _VP, _INT, _I64, _I64, _VP, _VP, _I32, _VP, _VP, _POPT, _VP, _SZ,
+                         _VP, _VP, _VP, _VP], _INT),
+    "ebt_cosine_topk_submit": ([_PCAT, _VP, _INT, _I64, _I64, _VP, _VP, _I32, _VP, _VP, _POPT,
+                                _VP, _SZ, _VP, _VP, _VP, _PPEND, _VP, _VP], _INT),
+    "ebt_cosine_topk_finish": ([_PPEND], _INT),
     "ebt_version": ([], _INT),
     "ebt_last_error": ([], ctypes.c_char_p),
     "ebt_row_norms": ([_VP, _INT, _I64, _I32, _I64, _VP, _VP, _VP], _INT),
@@ -82,7 +115,7 @@ _SIGNATURES = {
     "ebt_cosine_topk_spec_plan": ([_I64, _I64, _I64, _I32, _INT, ctypes.POINTER(_I64),
                                    ctypes.POINTER(_I64), ctypes.POINTER(ctypes.c_int32),
                                    ctypes.POINTER(ctypes.c_double)], _INT),
-    "ebt_cosine_topk": ([_VP, _VP, _VP, _VP, _I64, _I64, _VP, _INT, _I64, _VP, _VP, _VP, _INT,
+    "ebt_cosine_topk_prepared": ([_VP, _VP, _VP, _VP, _I64, _I64, _VP, _INT, _I64, _VP, _VP, _VP, _INT,
                          _I32, _I64, _I32, _I32, _I64, _VP, _VP, _I32, _I32, _I64, _INT, _VP, _SZ,
                          _VP, _VP, _VP, _VP, _VP], _INT),
     "ebt_als_gram": ([_VP, _I64, _I32, _VP, _VP], _INT),

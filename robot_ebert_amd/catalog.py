@@ -19,19 +19,25 @@ screening").
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Dict, Iterable, List, Optional, Sequence
 
 import numpy as np
 import torch
 
 from . import _lib
-from ._lib import DTYPE_CODE, EBT_BF16, EBT_F16, EbertError, call, ptr, require_cuda, stream_of
+from ._lib import DTYPE_CODE, EBT_BF16, EBT_F16, EbertError, call, ptr, require_cuda, stream_of  # noqa: F401
 
 IMG_ALIGN = 64
 
 
 def _round_up(v: int, m: int) -> int:
     return (v + m - 1) // m * m
+
+
+def _al(v: int) -> int:
+    """ebt_catalog_init's state-buffer alignment (256 bytes)."""
+    return _round_up(v, 256)
 
 
 class Catalog:
@@ -62,35 +68,32 @@ class Catalog:
         self.row_offset = int(row_offset)
         self.n_global = int(n_global) if n_global is not None else self.n
         self.d_pad = _round_up(self.d, IMG_ALIGN)
-        st = stream_of(self.device)
-        self.gnorm = torch.empty(self.n, dtype=torch.float64, device=self.device)
-        self.inv32 = torch.empty(_round_up(self.n, 128), dtype=torch.float32, device=self.device)
-        self.inv32[self.n:] = 1.0
-        call("ebt_row_norms", ptr(emb), self.dtype_code, self.n, self.d, self.ld, ptr(self.gnorm),
-             ptr(self.inv32), st)
-        native_16 = emb.dtype in (torch.float16, torch.bfloat16)
-        if native_16:
-            self.img_dtype = EBT_F16 if emb.dtype == torch.float16 else EBT_BF16
-            self.u_cat = 0.0
-            self.cscale = self.inv32
-            self.native = True
-            if self.d % IMG_ALIGN == 0 and self.ld % IMG_ALIGN == 0 and emb.data_ptr() % 16 == 0:
-                self.image = emb  # the matrix itself is the MFMA operand
-                self.ld_img = self.ld
-            else:
-                self.ld_img = self.d_pad
-                self.image = torch.empty((self.n, self.ld_img), dtype=emb.dtype, device=self.device)
-                call("ebt_screen_image", ptr(emb), self.dtype_code, self.n, self.d, self.ld,
-                     ptr(self.gnorm), 0, self.img_dtype, ptr(self.image), self.ld_img, st)
+        # the C ABI's catalog (ebt_catalog_init): guarded float64 norms, float32 inverse norms
+        # and the screening image in one device state buffer owned here
+        lib = _lib.load()
+        need = lib.ebt_catalog_state_bytes(ptr(emb), self.dtype_code, self.n, self.d, self.ld)
+        if need == 0:
+            raise EbertError(f"bad catalog shape {tuple(emb.shape)} (ld {self.ld})")
+        self.state = torch.empty(need, dtype=torch.uint8, device=self.device)
+        self.cstruct = _lib.EbtCatalog()
+        call("ebt_catalog_init", ctypes.byref(self.cstruct), ptr(emb), self.dtype_code, self.n,
+             self.d, self.ld, self.row_offset, ptr(self.state), need, stream_of(self.device))
+        c = self.cstruct
+        off_inv = _al(self.n * 8)
+        n128 = _round_up(self.n, 128)
+        off_img = off_inv + _al(n128 * 4)
+        self.gnorm = self.state[:self.n * 8].view(torch.float64)
+        self.inv32 = self.state[off_inv:off_inv + n128 * 4].view(torch.float32)
+        self.img_dtype = int(c.img_dtype)
+        self.ld_img = int(c.ld_img)
+        self.native = bool(c.native)
+        self.u_cat = float(c.u_cat)
+        self.cscale = self.inv32 if self.native else None
+        if c.image == emb.data_ptr():
+            self.image = emb  # the matrix itself is the MFMA operand
         else:
-            self.img_dtype = EBT_F16
-            self.u_cat = 2.0 ** -11
-            self.cscale = None
-            self.native = False
-            self.ld_img = self.d_pad
-            self.image = torch.empty((self.n, self.ld_img), dtype=torch.float16, device=self.device)
-            call("ebt_screen_image", ptr(emb), self.dtype_code, self.n, self.d, self.ld,
-                 ptr(self.gnorm), 1, self.img_dtype, ptr(self.image), self.ld_img, st)
+            self.image = self.state[off_img:off_img + self.n * self.ld_img * 2].view(
+                self.img_torch_dtype).view(self.n, self.ld_img)
         self.ids: Optional[List[str]] = list(ids) if ids is not None else None
         if self.ids is not None and len(self.ids) != self.n:
             raise EbertError(f"{len(self.ids)} ids for {self.n} rows")
@@ -151,6 +154,12 @@ class Catalog:
         self.u_cat = 0.0 if native_16 else 2.0 ** -11
         self.cscale = self.inv32 if native_16 else None
         self.ids, self._pos = None, None
+        self.state = None
+        self.cstruct = _lib.EbtCatalog(
+            data=ptr(self.data), dtype=self.dtype_code, d=self.d, n=self.n, ld=self.ld,
+            row_offset=self.row_offset, gnorm64=ptr(gnorm), inv32=ptr(inv32), image=ptr(image),
+            cscale=ptr(self.cscale), img_dtype=self.img_dtype, ld_img=self.ld_img,
+            d_pad=self.d_pad, native=1 if native_16 else 0, u_cat=self.u_cat)
         return self
 
     # ---- id helpers (the DataFrame index of constants.py:56) -----------------------------

@@ -1,5 +1,5 @@
 // extern "C" entry points of libebert.so (declared in include/ebert.h), the pipeline
-// orchestrator ebt_cosine_topk, the per-stage hipEvent timer and error reporting.
+// orchestrator ebt_cosine_topk_prepared, the per-stage hipEvent timer and error reporting.
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -38,7 +38,7 @@ int screen_image(const void*, int, int64_t, int32_t, int64_t, const double*, int
                  int32_t, hipStream_t);
 int query_dense(const void*, int, int64_t, int32_t, int64_t, double*, hipStream_t);
 int query_liked_sum(const void*, int, int32_t, int64_t, const double*, int64_t, const int64_t*,
-                    const int64_t*, double*, hipStream_t);
+                    const int64_t*, double*, hipStream_t, int64_t row_offset = 0);
 int scale_rows_f64(double*, int64_t, int32_t, const double*, hipStream_t);
 int query_image(const double*, int64_t, int64_t, int32_t, int, const void*, int64_t, int, float,
                 void*, int32_t, float*, float*, hipStream_t);
@@ -875,7 +875,7 @@ static int run_screen(const PipeArgs& a, const WsLayout& L, char* ws, float* fv,
 
 extern "C" {
 
-int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, const float* eps,
+int ebt_cosine_topk_prepared(const double* q64, const void* qimg, const float* qscale, const float* eps,
                     int64_t B, int64_t B_pad, const void* cat, int dtype, int64_t ld,
                     const double* gnorm64, const void* cimg, const float* cscale, int img_dtype,
                     int32_t ld_img, int64_t n_rows, int32_t d, int32_t d_pad, int64_t row_offset,
@@ -887,15 +887,15 @@ int ebt_cosine_topk(const double* q64, const void* qimg, const float* qscale, co
   const PipeArgs a{q64, qimg, qscale, eps, B, B_pad, cat, dtype, ld, gnorm64, cimg, cscale,
                    img_dtype, ld_img, n_rows, d, d_pad, row_offset, excl_off, excl_rows, k, kprime,
                    chunk_rows, flags};
-  int rc = check_pipe(a, "ebt_cosine_topk");
+  int rc = check_pipe(a, "ebt_cosine_topk_prepared");
   if (rc) return rc;
   if (!workspace || !out_scores || !out_rows || !certified) {
-    set_error("ebt_cosine_topk: null pointer");
+    set_error("ebt_cosine_topk_prepared: null pointer");
     return EBT_EINVAL;
   }
   const WsLayout L = ws_layout(B, B_pad, n_rows, kprime, chunk_rows, flags);
   if (ws_bytes < L.bytes) {
-    set_error("ebt_cosine_topk: workspace %zu < %zu bytes", ws_bytes, L.bytes);
+    set_error("ebt_cosine_topk_prepared: workspace %zu < %zu bytes", ws_bytes, L.bytes);
     return EBT_ENOMEM;
   }
   char* ws = (char*)workspace;

@@ -1,0 +1,661 @@
+// The self-contained C-ABI path (include/ebert.h: ebt_catalog_init, ebt_workspace_bytes,
+// ebt_cosine_topk{,_submit,_finish}): what a caller without Python binds in place of
+// /root/reference/src/backend/app/lib.py:51-55 (and the resident catalog of constants.py:55-56).
+//
+// One batch = query prep (ebt_query_prep / ebt_query_liked_sum + ebt_query_image) -> the
+// prepared-query pipeline (ebt_cosine_topk_prepared: screen + exact float64 rescore +
+// certificate) -> on the host, after ONE wait for this batch's certificates, the retries:
+//   certified -1 (a fused candidate list overflowed, or the speculative threshold was wrong)
+//                -> the query again with EBT_FLAG_NO_FUSE at the same k';
+//   certified  0 (more than k' rows inside the screen's error band) -> k' x 4 up to 4096, then
+//                the float64 screen (EBT_FLAG_EXACT); still 0 there is an error (more than
+//                4096 rows tied at f32 resolution), never a silent approximation;
+//   certified -2 (a corrupt candidate row) -> error.
+// Retried queries are gathered into groups of at most RETRY_GROUP (their prepared rows, their
+// exclusion segments), run through the same pipeline and scattered back. Everything lives in
+// the caller's workspace; the library allocates no device memory.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+
+namespace ebt {
+
+int query_liked_sum(const void*, int, int32_t, int64_t, const double*, int64_t, const int64_t*,
+                    const int64_t*, double*, hipStream_t, int64_t row_offset);
+
+namespace {
+
+constexpr int64_t KPRIME_MAX = 4096;
+constexpr int64_t QUERY_PREP_MAX_D = 4096;
+constexpr int64_t SCORE_BUDGET = 4LL << 30;   // f32 score bytes of the unfused path per pass
+constexpr int64_t RETRY_GROUP = 256;          // queries per retry pass
+constexpr int64_t RETRY_BUDGET = 256LL << 20; // f32 score bytes of a retry pass
+constexpr int64_t RETRY_EXCL_MAX = 1LL << 20; // gathered exclusion rows per retry pass
+
+int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+size_t al(size_t v) { return (v + 255) & ~(size_t)255; }
+
+int64_t pad_batch(int64_t B) {
+  B = B < 1 ? 1 : B;
+  return B <= 128 ? round_up(B, 128) : round_up(B, 256);
+}
+
+// search.py default_kprime: the rows inside the 2 eps band around the k-th score grow with k;
+// native images have the smaller band
+int32_t default_kprime(const ebt_catalog& c, int64_t k_eff) {
+  int64_t kp = c.native ? k_eff + (k_eff / 4 > 16 ? k_eff / 4 : 16)
+                        : (2 * k_eff > k_eff + 32 ? 2 * k_eff : k_eff + 32);
+  kp = round_up(kp, 8);
+  kp = kp < KPRIME_MAX ? kp : KPRIME_MAX;
+  int64_t lo = round_up(k_eff, 4), hi = round_up(c.n, 4);
+  kp = round_up(kp, 4);
+  kp = kp < hi ? kp : hi;
+  kp = kp < KPRIME_MAX ? kp : KPRIME_MAX;
+  return (int32_t)(kp > lo ? kp : lo);
+}
+
+int64_t chunk_rows(const ebt_catalog& c, int64_t B_pad, int64_t budget) {
+  int64_t rows = budget / (4 * B_pad);
+  rows = rows / 128 * 128;
+  rows = rows < 128 ? 128 : rows;
+  const int64_t cap = round_up(c.n, 128);
+  return rows < cap ? rows : cap;
+}
+
+int elem_size(int dt) { return dt == EBT_F64 ? 8 : dt == EBT_F32 ? 4 : 2; }
+
+// Per-batch prepared queries (the ebt_query_* outputs) for `rows` queries.
+struct PrepLayout {
+  size_t q64, qimg, qscale, eps, bytes;
+};
+PrepLayout prep_layout(const ebt_catalog& c, int64_t rows) {
+  const int64_t rp = pad_batch(rows);
+  PrepLayout p{};
+  size_t o = 0;
+  p.q64 = o;
+  o = al(o + (size_t)rows * c.d * 8);
+  p.qimg = o;
+  o = al(o + (size_t)rp * c.ld_img * 2);
+  p.qscale = o;
+  o = al(o + (size_t)rp * 4);
+  p.eps = o;
+  o = al(o + (size_t)rp * 4);
+  p.bytes = o;
+  return p;
+}
+
+// The whole workspace of one batch:
+//   [prep B] [pass: max(first pass, every retry pass)] [results k_eff < k] [cert B + flag]
+//   [retry: prep R, results R x k_eff, cert R, gather indices, exclusion CSR of the group]
+struct DriverLayout {
+  int64_t B, B_pad, R, chunk, chunk_r;
+  int32_t k_eff, kprime, flags;
+  PrepLayout prep, prep_r;
+  size_t off_prep, off_pass, pass_bytes, off_res_s, off_res_r, off_cert, off_rprep, off_rs,
+      off_rr, off_rcert, off_idx, off_roff, off_rrows, bytes;
+};
+
+bool driver_layout(const ebt_catalog& c, int64_t B, int32_t k, const ebt_options& opt,
+                   DriverLayout* L) {
+  if (B < 1 || k < 1 || c.n < 1 || opt.kprime < 0 || opt.chunk_rows < 0 ||
+      (opt.chunk_rows && opt.chunk_rows % 128) || (opt.flags & ~EBT_FLAG_NO_FUSE))
+    return false;
+  DriverLayout& D = *L;
+  D = DriverLayout{};
+  D.B = B;
+  D.B_pad = pad_batch(B);
+  D.k_eff = (int32_t)(k < c.n ? k : c.n);
+  if (D.k_eff > KPRIME_MAX) return false;
+  D.kprime = default_kprime(c, D.k_eff);
+  if (opt.kprime) {  // search.py's clamp: [round_up(k, 4), min(round_up(n, 4), 4096)]
+    int64_t kp = round_up(opt.kprime, 4), hi = round_up(c.n, 4), lo = round_up(D.k_eff, 4);
+    kp = kp < hi ? kp : hi;
+    kp = kp < KPRIME_MAX ? kp : KPRIME_MAX;
+    D.kprime = (int32_t)(kp > lo ? kp : lo);
+  }
+  D.flags = opt.flags;
+  D.chunk = opt.chunk_rows ? opt.chunk_rows : chunk_rows(c, D.B_pad, SCORE_BUDGET);
+  D.R = B < RETRY_GROUP ? B : RETRY_GROUP;
+  const int64_t R_pad = pad_batch(D.R);
+  D.chunk_r = opt.chunk_rows ? opt.chunk_rows : chunk_rows(c, R_pad, RETRY_BUDGET);
+  size_t pass = ebt_cosine_topk_workspace(B, D.B_pad, c.n, D.kprime, D.chunk, D.flags);
+  if (pass == 0) return false;
+  // every retry configuration: k' from the first pass up to 4096 (x 4 steps), fused or not,
+  // and the float64 screen from the default k' up
+  const int64_t kcap = round_up(c.n, 4) < KPRIME_MAX ? round_up(c.n, 4) : KPRIME_MAX;
+  const int fl[3] = {D.flags, EBT_FLAG_NO_FUSE, EBT_FLAG_EXACT};
+  for (int f = 0; f < 3; ++f) {
+    for (int64_t kp = D.kprime;; kp = kp * 4 < kcap ? kp * 4 : kcap) {
+      const size_t w = ebt_cosine_topk_workspace(D.R, R_pad, c.n, (int32_t)kp, D.chunk_r, fl[f]);
+      if (w == 0) return false;
+      pass = w > pass ? w : pass;
+      if (kp >= kcap) break;
+    }
+  }
+  D.prep = prep_layout(c, B);
+  D.prep_r = prep_layout(c, D.R);
+  size_t o = 0;
+  D.off_prep = o;
+  o = al(o + D.prep.bytes);
+  D.off_pass = o;
+  D.pass_bytes = pass;
+  o = al(o + pass);
+  D.off_res_s = o;
+  if (D.k_eff < k) o = al(o + (size_t)B * D.k_eff * 8);
+  D.off_res_r = o;
+  if (D.k_eff < k) o = al(o + (size_t)B * D.k_eff * 8);
+  D.off_cert = o;
+  o = al(o + (size_t)(B + 1) * 4);
+  D.off_rprep = o;
+  o = al(o + D.prep_r.bytes);
+  D.off_rs = o;
+  o = al(o + (size_t)D.R * D.k_eff * 8);
+  D.off_rr = o;
+  o = al(o + (size_t)D.R * D.k_eff * 8);
+  D.off_rcert = o;
+  o = al(o + (size_t)D.R * 4);
+  D.off_idx = o;
+  o = al(o + (size_t)D.R * 8);
+  D.off_roff = o;
+  o = al(o + (size_t)(D.R + 1) * 8);
+  D.off_rrows = o;
+  o = al(o + (size_t)RETRY_EXCL_MAX * 8);
+  D.bytes = o;
+  return true;
+}
+
+// ------------------------------------------------------------------------------ kernels ----
+// dst row i <- src row idx[i] (gather) or dst row idx[i] <- src row i (scatter), 4-byte words
+__global__ void move_rows_kernel(const uint32_t* __restrict__ src, int64_t src_ld,
+                                 uint32_t* __restrict__ dst, int64_t dst_ld,
+                                 const int64_t* __restrict__ idx, int64_t n, int64_t words,
+                                 int scatter) {
+  const int64_t total = n * words;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / words, w = t - i * words;
+    if (scatter) dst[idx[i] * dst_ld + w] = src[i * src_ld + w];
+    else dst[i * dst_ld + w] = src[idx[i] * src_ld + w];
+  }
+}
+
+int move_rows(const void* src, int64_t src_ld_bytes, void* dst, int64_t dst_ld_bytes,
+              const int64_t* idx, int64_t n, int64_t row_bytes, bool scatter, hipStream_t st) {
+  if (n == 0) return EBT_OK;
+  const int64_t words = row_bytes / 4, total = n * words;
+  int64_t blocks = (total + 255) / 256;
+  blocks = blocks > 4096 ? 4096 : blocks;
+  hipLaunchKernelGGL(move_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                     (const uint32_t*)src, src_ld_bytes / 4, (uint32_t*)dst, dst_ld_bytes / 4,
+                     idx, n, words, scatter ? 1 : 0);
+  return launch_check("move_rows_kernel");
+}
+
+// the exclusion segments of the retried queries, gathered (new offsets computed on the host)
+__global__ void csr_gather_kernel(const int64_t* __restrict__ off, const int64_t* __restrict__ rows,
+                                  const int64_t* __restrict__ idx,
+                                  const int64_t* __restrict__ new_off, int64_t* __restrict__ out) {
+  const int64_t i = blockIdx.x;
+  const int64_t s = off[idx[i]], n = new_off[i + 1] - new_off[i];
+  for (int64_t t = threadIdx.x; t < n; t += blockDim.x) out[new_off[i] + t] = rows[s + t];
+}
+
+// out[b][j] = j < k_eff ? res[b][j] : NaN / -1
+__global__ void pad_results_kernel(const double* __restrict__ rs, const int64_t* __restrict__ rr,
+                                   int64_t B, int k_eff, int k, double* __restrict__ os,
+                                   int64_t* __restrict__ orow) {
+  const int64_t total = B * k;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = t / k, j = t - b * k;
+    os[t] = j < k_eff ? rs[b * k_eff + j] : __builtin_nan("");
+    orow[t] = j < k_eff ? rr[b * k_eff + j] : -1;
+  }
+}
+
+// flag[0] = 1 when some exclusion segment is not sorted ascending (the fused merge drops
+// excluded rows by binary search); one block per query
+__global__ void csr_sorted_kernel(const int64_t* __restrict__ off, const int64_t* __restrict__ rows,
+                                  int32_t* __restrict__ flag) {
+  const int64_t b = blockIdx.x;
+  const int64_t s = off[b], e = off[b + 1];
+  bool bad = e < s;
+  for (int64_t t = s + threadIdx.x; t + 1 < e; t += blockDim.x) bad |= rows[t] > rows[t + 1];
+  if (bad) flag[0] = 1;
+}
+
+int prep_dense(const ebt_catalog& c, const void* q, int q_dtype, int64_t B, int64_t ldq,
+               const PrepLayout& P, char* base, hipStream_t st) {
+  double* q64 = (double*)(base + P.q64);
+  void* qimg = base + P.qimg;
+  float* qscale = (float*)(base + P.qscale);
+  float* eps = (float*)(base + P.eps);
+  const int64_t B_pad = pad_batch(B);
+  const int native_q = c.native && q_dtype == c.img_dtype;
+  if (c.d <= QUERY_PREP_MAX_D)
+    return ebt_query_prep(q, q_dtype, B, B_pad, c.d, ldq, c.img_dtype, native_q, c.u_cat, q64,
+                          qimg, c.ld_img, qscale, eps, st);
+  int rc = ebt_query_dense(q, q_dtype, B, c.d, ldq, q64, st);
+  if (rc) return rc;
+  return ebt_query_image(q64, B, B_pad, c.d, c.img_dtype, native_q ? q : nullptr,
+                         native_q ? ldq : 0, native_q, c.u_cat, qimg, c.ld_img, qscale, eps, st);
+}
+
+// liked path: validated on the host (counts >= 1 with sklearn's message, rows in the catalog)
+int prep_liked(const ebt_catalog& c, const int64_t* off, const int64_t* rows, int64_t B,
+               const PrepLayout& P, char* base, char* scratch, size_t scratch_bytes,
+               hipStream_t st) {
+  std::vector<int64_t> h_off(B + 1);
+  int rc = hip_check(hipMemcpyAsync(h_off.data(), off, (B + 1) * 8, hipMemcpyDeviceToHost, st),
+                     "hipMemcpyAsync");
+  if (!rc) rc = hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+  if (rc) return rc;
+  const int64_t nnz = h_off[B] - h_off[0];
+  std::vector<double> scale(B);
+  for (int64_t b = 0; b < B; ++b) {
+    const int64_t cnt = h_off[b + 1] - h_off[b];
+    if (cnt <= 0) {
+      set_error("Found array with 0 sample(s) (shape=(0, %d)) while a minimum of 1 is required "
+                "by check_pairwise_arrays.", c.d);
+      return EBT_EINVAL;
+    }
+    scale[b] = 1.0 / (double)cnt;
+  }
+  if (nnz > 0) {
+    std::vector<int64_t> h_rows(nnz);
+    rc = hip_check(hipMemcpy(h_rows.data(), rows + h_off[0], nnz * 8, hipMemcpyDeviceToHost),
+                   "hipMemcpy");
+    if (rc) return rc;
+    for (int64_t r : h_rows)
+      if (r < c.row_offset || r >= c.row_offset + c.n) {
+        set_error("liked row %lld is not in the catalog rows [%lld, %lld)", (long long)r,
+                  (long long)c.row_offset, (long long)(c.row_offset + c.n));
+        return EBT_EINVAL;
+      }
+  }
+  if (scratch_bytes < (size_t)B * 8) {
+    set_error("ebt_cosine_topk: workspace too small for the liked-query scales");
+    return EBT_ENOMEM;
+  }
+  double* d_scale = (double*)scratch;
+  rc = hip_check(hipMemcpy(d_scale, scale.data(), B * 8, hipMemcpyHostToDevice), "hipMemcpy");
+  if (rc) return rc;
+  double* q64 = (double*)(base + P.q64);
+  rc = query_liked_sum(c.data, c.dtype, c.d, c.ld, c.gnorm64, B, off, rows, q64, st,
+                       c.row_offset);
+  if (!rc) rc = ebt_scale_rows_f64(q64, B, c.d, d_scale, st);
+  if (rc) return rc;
+  return ebt_query_image(q64, B, pad_batch(B), c.d, c.img_dtype, nullptr, 0, 0, c.u_cat,
+                         base + P.qimg, c.ld_img, (float*)(base + P.qscale),
+                         (float*)(base + P.eps), st);
+}
+
+int run_prepared(const ebt_catalog& c, const PrepLayout& P, char* base, int64_t B,
+                 const int64_t* excl_off, const int64_t* excl_rows, int32_t k_eff, int32_t kp,
+                 int64_t chunk, int flags, char* pass, size_t pass_bytes, double* out_s,
+                 int64_t* out_r, int32_t* cert, void* timer, hipStream_t st) {
+  const bool exact = flags & EBT_FLAG_EXACT;
+  return ebt_cosine_topk_prepared(
+      (const double*)(base + P.q64), exact ? nullptr : base + P.qimg,
+      exact ? nullptr : (const float*)(base + P.qscale),
+      exact ? nullptr : (const float*)(base + P.eps), B, pad_batch(B), c.data, c.dtype, c.ld,
+      c.gnorm64, c.image, c.cscale, c.img_dtype, c.ld_img, c.n, c.d, c.d_pad, c.row_offset,
+      excl_off, excl_rows, k_eff, kp, chunk, flags, pass, pass_bytes, out_s, out_r, cert, timer,
+      st);
+}
+
+bool valid_catalog(const ebt_catalog* c) {
+  return c && c->data && c->gnorm64 && c->image && c->n > 0 && c->d > 0 && c->ld >= c->d &&
+         c->d_pad % 64 == 0 && c->d_pad >= c->d && c->ld_img >= c->d_pad;
+}
+
+}  // namespace
+}  // namespace ebt
+
+using namespace ebt;
+
+extern "C" {
+
+size_t ebt_catalog_state_bytes(const void* data, int dtype, int64_t n, int32_t d, int64_t ld) {
+  if (n < 1 || d < 1 || ld < d || dtype < 0 || dtype > 3) return 0;
+  const int64_t d_pad = round_up(d, 64);
+  const bool native = dtype == EBT_F16 || dtype == EBT_BF16;
+  const bool alias = native && d % 64 == 0 && ld % 64 == 0 && ((uintptr_t)data & 15) == 0;
+  size_t o = al((size_t)n * 8) + al((size_t)round_up(n, 128) * 4);
+  if (!alias) o += al((size_t)n * d_pad * 2);
+  return o;
+}
+
+int ebt_catalog_init(ebt_catalog* cat, const void* data, int dtype, int64_t n, int32_t d,
+                     int64_t ld, int64_t row_offset, void* state, size_t state_bytes,
+                     void* stream) {
+  const size_t need = ebt_catalog_state_bytes(data, dtype, n, d, ld);
+  if (!cat || !data || !state || need == 0 || row_offset < 0) {
+    set_error("ebt_catalog_init: bad arguments (n=%lld d=%d ld=%lld dtype=%d)", (long long)n, d,
+              (long long)ld, dtype);
+    return EBT_EINVAL;
+  }
+  if (state_bytes < need) {
+    set_error("ebt_catalog_init: state %zu < %zu bytes", state_bytes, need);
+    return EBT_ENOMEM;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  ebt_catalog c{};
+  c.data = data;
+  c.dtype = dtype;
+  c.d = d;
+  c.n = n;
+  c.ld = ld;
+  c.row_offset = row_offset;
+  c.d_pad = (int32_t)round_up(d, 64);
+  char* s = (char*)state;
+  c.gnorm64 = (double*)s;
+  c.inv32 = (float*)(s + al((size_t)n * 8));
+  char* img = s + al((size_t)n * 8) + al((size_t)round_up(n, 128) * 4);
+  const float one = 1.0f;
+  uint32_t one_bits;
+  memcpy(&one_bits, &one, 4);
+  int rc = EBT_OK;
+  if (round_up(n, 128) > n)
+    rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)(c.inv32 + n), (int)one_bits,
+                                     (size_t)(round_up(n, 128) - n), st), "hipMemsetD32Async");
+  if (!rc) rc = ebt_row_norms(data, dtype, n, d, ld, c.gnorm64, c.inv32, st);
+  if (rc) return rc;
+  const bool native = dtype == EBT_F16 || dtype == EBT_BF16;
+  if (native) {
+    c.img_dtype = dtype;
+    c.u_cat = 0.0f;
+    c.cscale = c.inv32;
+    c.native = 1;
+    if (d % 64 == 0 && ld % 64 == 0 && ((uintptr_t)data & 15) == 0) {
+      c.image = data;  // the matrix itself is the MFMA operand
+      c.ld_img = (int32_t)ld;
+    } else {
+      c.ld_img = c.d_pad;
+      c.image = img;
+      rc = ebt_screen_image(data, dtype, n, d, ld, c.gnorm64, 0, c.img_dtype, img, c.ld_img, st);
+    }
+  } else {
+    c.img_dtype = EBT_F16;
+    c.u_cat = 1.0f / 2048.0f;  // 2^-11: f16 image of the normalised rows
+    c.cscale = nullptr;
+    c.native = 0;
+    c.ld_img = c.d_pad;
+    c.image = img;
+    rc = ebt_screen_image(data, dtype, n, d, ld, c.gnorm64, 1, c.img_dtype, img, c.ld_img, st);
+  }
+  if (rc) return rc;
+  *cat = c;
+  return EBT_OK;
+}
+
+size_t ebt_workspace_bytes(const ebt_catalog* cat, int64_t B, int32_t k, const ebt_options* opt) {
+  if (!valid_catalog(cat)) return 0;
+  DriverLayout L;
+  if (!driver_layout(*cat, B, k, opt ? *opt : ebt_options{}, &L)) return 0;
+  return L.bytes;
+}
+
+int ebt_cosine_topk_submit(const ebt_catalog* cat, const void* q, int q_dtype, int64_t B,
+                           int64_t ldq, const int64_t* liked_off, const int64_t* liked_rows,
+                           int32_t k, const int64_t* excl_off, const int64_t* excl_rows,
+                           const ebt_options* opt, void* workspace, size_t ws_bytes,
+                           double* out_scores, int64_t* out_rows, int32_t* cert_host,
+                           ebt_pending* p, void* timer, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!valid_catalog(cat) || !p || !workspace || !out_scores || !out_rows || !cert_host ||
+      B < 1 || k < 1 || ((q == nullptr) == (liked_off == nullptr)) ||
+      (liked_off && !liked_rows) || ((excl_off == nullptr) != (excl_rows == nullptr)) ||
+      (q && (q_dtype < 0 || q_dtype > 3 || ldq < cat->d))) {
+    set_error("ebt_cosine_topk: bad arguments (B=%lld k=%d; pass exactly one of q / liked)",
+              (long long)B, k);
+    return EBT_EINVAL;
+  }
+  const ebt_options o = opt ? *opt : ebt_options{};
+  DriverLayout L;
+  if (!driver_layout(*cat, B, k, o, &L)) {
+    set_error("ebt_cosine_topk: unsupported sizes or options (B=%lld k=%d n=%lld: k <= 4096 "
+              "or k >= n; chunk_rows % 128 == 0; flags EBT_FLAG_NO_FUSE only)",
+              (long long)B, k, (long long)cat->n);
+    return EBT_EINVAL;
+  }
+  if (ws_bytes < L.bytes) {
+    set_error("ebt_cosine_topk: workspace %zu < %zu bytes (ebt_workspace_bytes)", ws_bytes,
+              L.bytes);
+    return EBT_ENOMEM;
+  }
+  char* ws = (char*)workspace;
+  char* prep = ws + L.off_prep;
+  int rc = q ? prep_dense(*cat, q, q_dtype, B, ldq, L.prep, prep, st)
+             : prep_liked(*cat, liked_off, liked_rows, B, L.prep, prep, ws + L.off_pass,
+                          L.pass_bytes, st);
+  if (rc) return rc;
+  int32_t* cert = (int32_t*)(ws + L.off_cert);
+  const bool padded = L.k_eff < k;
+  double* rs = padded ? (double*)(ws + L.off_res_s) : out_scores;
+  int64_t* rr = padded ? (int64_t*)(ws + L.off_res_r) : out_rows;
+  rc = run_prepared(*cat, L.prep, prep, B, excl_off, excl_rows, L.k_eff, L.kprime, L.chunk,
+                    L.flags, ws + L.off_pass, L.pass_bytes, rs, rr, cert, timer, st);
+  if (rc) return rc;
+  // the exclusion check's flag sits right after the certificates: one copy brings both
+  rc = hip_check(hipMemsetAsync(cert + B, 0, 4, st), "hipMemsetAsync");
+  if (rc) return rc;
+  if (excl_off) {
+    hipLaunchKernelGGL(csr_sorted_kernel, dim3((unsigned)B), dim3(256), 0, st, excl_off,
+                       excl_rows, cert + B);
+    rc = launch_check("csr_sorted_kernel");
+    if (rc) return rc;
+  }
+  rc = hip_check(hipMemcpyAsync(cert_host, cert, (size_t)(B + 1) * 4, hipMemcpyDeviceToHost, st),
+                 "hipMemcpyAsync");
+  if (rc) return rc;
+  hipEvent_t ev;
+  rc = hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+  if (rc) return rc;
+  rc = hip_check(hipEventRecord(ev, st), "hipEventRecord");
+  if (rc) {
+    (void)hipEventDestroy(ev);
+    return rc;
+  }
+  ebt_pending P{};
+  P.cat = cat;
+  P.opt = o;
+  P.B = B;
+  P.B_pad = L.B_pad;
+  P.chunk = L.chunk;
+  P.k = k;
+  P.k_eff = L.k_eff;
+  P.kprime = L.kprime;
+  P.excl_off = excl_off;
+  P.excl_rows = excl_rows;
+  P.ws = ws;
+  P.ws_bytes = ws_bytes;
+  P.out_scores = out_scores;
+  P.out_rows = out_rows;
+  P.cert_host = cert_host;
+  P.event = ev;
+  P.timer = timer;
+  P.stream = stream;
+  *p = P;
+  return EBT_OK;
+}
+
+int ebt_cosine_topk_finish(ebt_pending* p) {
+  if (!p || !p->event || !p->cat) {
+    set_error("ebt_cosine_topk_finish: not a submitted batch");
+    return EBT_EINVAL;
+  }
+  hipStream_t st = (hipStream_t)p->stream;
+  const ebt_catalog& c = *p->cat;
+  hipEvent_t ev = (hipEvent_t)p->event;
+  int rc = hip_check(hipEventSynchronize(ev), "hipEventSynchronize");
+  (void)hipEventDestroy(ev);
+  p->event = nullptr;
+  if (rc) return rc;
+  const int64_t B = p->B;
+  DriverLayout L;
+  if (!driver_layout(c, B, p->k, p->opt, &L)) {
+    set_error("ebt_cosine_topk_finish: bad pending batch");
+    return EBT_EINVAL;
+  }
+  if (p->cert_host[B] != 0) {
+    set_error("ebt_cosine_topk: exclusion rows must be sorted ascending within each query");
+    return EBT_EINVAL;
+  }
+  char* ws = p->ws;
+  const bool padded = L.k_eff < p->k;
+  double* rs = padded ? (double*)(ws + L.off_res_s) : p->out_scores;
+  int64_t* rr = padded ? (int64_t*)(ws + L.off_res_r) : p->out_rows;
+  const int32_t kcap = (int32_t)(round_up(c.n, 4) < KPRIME_MAX ? round_up(c.n, 4) : KPRIME_MAX);
+  // per-query retry state
+  std::vector<int32_t> cert(p->cert_host, p->cert_host + B);
+  std::vector<int32_t> kp(B, L.kprime), fl(B, L.flags);
+  std::vector<int64_t> h_off;
+  char* prep = ws + L.off_prep;
+  char* rprep = ws + L.off_rprep;
+  int64_t* d_idx = (int64_t*)(ws + L.off_idx);
+  int64_t* d_roff = (int64_t*)(ws + L.off_roff);
+  int64_t* d_rrows = (int64_t*)(ws + L.off_rrows);
+  double* r_s = (double*)(ws + L.off_rs);
+  int64_t* r_r = (int64_t*)(ws + L.off_rr);
+  int32_t* r_c = (int32_t*)(ws + L.off_rcert);
+  const int64_t qrow = (int64_t)c.d * 8, irow = (int64_t)c.ld_img * 2;
+  for (int round = 0;; ++round) {
+    // next configuration of every query that needs one
+    std::vector<int64_t> todo;
+    for (int64_t b = 0; b < B; ++b) {
+      if (cert[b] == 1) continue;
+      if (cert[b] == -2 || cert[b] < -2 || cert[b] > 1) {
+        set_error("internal error: candidate row out of range (certificate %d)", cert[b]);
+        return EBT_EHIP;
+      }
+      if (cert[b] == -1) {
+        fl[b] |= EBT_FLAG_NO_FUSE;
+      } else if (kp[b] < kcap) {
+        kp[b] = kp[b] * 4 < kcap ? kp[b] * 4 : kcap;
+      } else if (!(fl[b] & EBT_FLAG_EXACT)) {
+        fl[b] = EBT_FLAG_EXACT;
+        kp[b] = L.kprime;
+      } else {
+        set_error("query %lld could not be certified at k'=%d (more than k' rows tie with the "
+                  "k-th score at f32 precision)", (long long)b, kp[b]);
+        return EBT_EUNSUPPORTED;
+      }
+      todo.push_back(b);
+    }
+    if (todo.empty()) break;
+    if (round > 64) {
+      set_error("ebt_cosine_topk: retries did not converge");
+      return EBT_EHIP;
+    }
+    if (p->excl_off && h_off.empty()) {
+      h_off.resize(B + 1);
+      rc = hip_check(hipMemcpy(h_off.data(), p->excl_off, (B + 1) * 8, hipMemcpyDeviceToHost),
+                     "hipMemcpy");
+      if (rc) return rc;
+    }
+    // groups of equal (k', flags), at most R queries and RETRY_EXCL_MAX exclusion rows each
+    std::vector<char> done(todo.size(), 0);
+    for (size_t s = 0; s < todo.size(); ++s) {
+      if (done[s]) continue;
+      const int32_t gkp = kp[todo[s]], gfl = fl[todo[s]];
+      std::vector<int64_t> grp;
+      std::vector<int64_t> goff(1, 0);
+      bool solo = false;  // one query whose own segment exceeds the gather buffer
+      for (size_t u = s; u < todo.size() && (int64_t)grp.size() < L.R; ++u) {
+        const int64_t b = todo[u];
+        if (done[u] || kp[b] != gkp || fl[b] != gfl) continue;
+        const int64_t len = p->excl_off ? h_off[b + 1] - h_off[b] : 0;
+        if (len > RETRY_EXCL_MAX) {
+          if (!grp.empty()) continue;
+          solo = true;
+        } else if (goff.back() + len > RETRY_EXCL_MAX) {
+          continue;
+        }
+        grp.push_back(b);
+        goff.push_back(goff.back() + len);
+        done[u] = 1;
+        if (solo) break;
+      }
+      const int64_t m = (int64_t)grp.size(), m_pad = pad_batch(m);
+      rc = hip_check(hipMemcpy(d_idx, grp.data(), m * 8, hipMemcpyHostToDevice), "hipMemcpy");
+      if (rc) return rc;
+      // the group's prepared queries (padding rows: zero image, scale 1, eps 0)
+      const PrepLayout& RP = L.prep_r;
+      rc = hip_check(hipMemsetAsync(rprep + RP.qimg, 0, (size_t)m_pad * irow, st), "memset");
+      if (!rc) rc = hip_check(hipMemsetAsync(rprep + RP.eps, 0, (size_t)m_pad * 4, st), "memset");
+      if (!rc) rc = move_rows(prep + L.prep.q64, qrow, rprep + RP.q64, qrow, d_idx, m, qrow,
+                              false, st);
+      if (!rc) rc = move_rows(prep + L.prep.qimg, irow, rprep + RP.qimg, irow, d_idx, m, irow,
+                              false, st);
+      if (!rc) rc = move_rows(prep + L.prep.qscale, 4, rprep + RP.qscale, 4, d_idx, m, 4, false,
+                              st);
+      if (!rc) rc = move_rows(prep + L.prep.eps, 4, rprep + RP.eps, 4, d_idx, m, 4, false, st);
+      if (rc) return rc;
+      const int64_t* eo = nullptr;
+      const int64_t* er = nullptr;
+      if (p->excl_off) {
+        if (solo) {  // the segment in place: offsets {off[b], off[b+1]} into the caller's rows
+          rc = hip_check(hipMemcpy(d_roff, p->excl_off + grp[0], 16, hipMemcpyDeviceToDevice),
+                         "hipMemcpy");
+          if (rc) return rc;
+          eo = d_roff;
+          er = p->excl_rows;
+        } else {
+          rc = hip_check(hipMemcpy(d_roff, goff.data(), (m + 1) * 8, hipMemcpyHostToDevice),
+                         "hipMemcpy");
+          if (rc) return rc;
+          hipLaunchKernelGGL(csr_gather_kernel, dim3((unsigned)m), dim3(256), 0, st, p->excl_off,
+                             p->excl_rows, d_idx, d_roff, d_rrows);
+          rc = launch_check("csr_gather_kernel");
+          if (rc) return rc;
+          eo = d_roff;
+          er = d_rrows;
+        }
+      }
+      rc = run_prepared(c, RP, rprep, m, eo, er, L.k_eff, gkp, L.chunk_r, gfl, ws + L.off_pass,
+                        L.pass_bytes, r_s, r_r, r_c, p->timer, st);
+      if (!rc) rc = move_rows(r_s, (int64_t)L.k_eff * 8, rs, (int64_t)L.k_eff * 8, d_idx, m,
+                              (int64_t)L.k_eff * 8, true, st);
+      if (!rc) rc = move_rows(r_r, (int64_t)L.k_eff * 8, rr, (int64_t)L.k_eff * 8, d_idx, m,
+                              (int64_t)L.k_eff * 8, true, st);
+      if (rc) return rc;
+      std::vector<int32_t> gc(m);
+      rc = hip_check(hipMemcpyAsync(gc.data(), r_c, m * 4, hipMemcpyDeviceToHost, st),
+                     "hipMemcpyAsync");
+      if (!rc) rc = hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+      if (rc) return rc;
+      for (int64_t i = 0; i < m; ++i) cert[grp[i]] = gc[i];
+    }
+  }
+  if (padded) {
+    const int64_t total = B * p->k;
+    int64_t blocks = (total + 255) / 256;
+    blocks = blocks > 4096 ? 4096 : blocks;
+    hipLaunchKernelGGL(pad_results_kernel, dim3((unsigned)blocks), dim3(256), 0, st, rs, rr, B,
+                       L.k_eff, p->k, p->out_scores, p->out_rows);
+    rc = launch_check("pad_results_kernel");
+    if (rc) return rc;
+  }
+  return EBT_OK;
+}
+
+int ebt_cosine_topk(const ebt_catalog* cat, const void* q, int q_dtype, int64_t B, int64_t ldq,
+                    const int64_t* liked_off, const int64_t* liked_rows, int32_t k,
+                    const int64_t* excl_off, const int64_t* excl_rows, const ebt_options* opt,
+                    void* workspace, size_t ws_bytes, double* out_scores, int64_t* out_rows,
+                    void* timer, void* stream) {
+  std::vector<int32_t> cert((size_t)(B > 0 ? B : 0) + 1);
+  ebt_pending p{};
+  int rc = ebt_cosine_topk_submit(cat, q, q_dtype, B, ldq, liked_off, liked_rows, k, excl_off,
+                                  excl_rows, opt, workspace, ws_bytes, out_scores, out_rows,
+                                  cert.data(), &p, timer, stream);
+  if (rc) return rc;
+  rc = ebt_cosine_topk_finish(&p);
+  if (!rc) rc = hip_check(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
+  return rc;
+}
+
+}  // extern "C"

@@ -199,22 +199,25 @@ __global__ __launch_bounds__(256) void query_liked_kernel(const void* __restrict
                                                            const double* __restrict__ gnorm,
                                                            const int64_t* __restrict__ off,
                                                            const int64_t* __restrict__ rows,
+                                                           int64_t row_offset,
                                                            double* __restrict__ q64) {
   const int64_t b = blockIdx.x;
   const int64_t l0 = off[b], l1 = off[b + 1];
   for (int j = threadIdx.x; j < d; j += blockDim.x) {
     double acc = 0.0;
     for (int64_t l = l0; l < l1; ++l) {
-      const int64_t r = rows[l];
+      const int64_t r = rows[l] - row_offset;
       acc += load_as_f64<DT>(cat, r * ld + j) / gnorm[r];
     }
     q64[b * d + j] = acc;
   }
 }
 
+// rows are catalog rows + row_offset (the self-contained path passes GLOBAL rows; the caller
+// guarantees every row lies inside the catalog)
 int query_liked_sum(const void* cat, int dtype, int32_t d, int64_t ld, const double* gnorm,
                     int64_t B, const int64_t* off, const int64_t* rows, double* q64,
-                    hipStream_t st) {
+                    hipStream_t st, int64_t row_offset) {
   if (!cat || !gnorm || !off || !q64 || B < 0 || d <= 0 || ld < d || dtype < 0 || dtype > 3) {
     set_error("ebt_query_liked_sum: bad arguments");
     return EBT_EINVAL;
@@ -222,10 +225,10 @@ int query_liked_sum(const void* cat, int dtype, int32_t d, int64_t ld, const dou
   if (B == 0) return EBT_OK;
   dim3 grid((unsigned)B), block(256);
   switch (dtype) {
-    case EBT_F32: hipLaunchKernelGGL(query_liked_kernel<EBT_F32>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, q64); break;
-    case EBT_BF16: hipLaunchKernelGGL(query_liked_kernel<EBT_BF16>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, q64); break;
-    case EBT_F16: hipLaunchKernelGGL(query_liked_kernel<EBT_F16>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, q64); break;
-    default: hipLaunchKernelGGL(query_liked_kernel<EBT_F64>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, q64); break;
+    case EBT_F32: hipLaunchKernelGGL(query_liked_kernel<EBT_F32>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, row_offset, q64); break;
+    case EBT_BF16: hipLaunchKernelGGL(query_liked_kernel<EBT_BF16>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, row_offset, q64); break;
+    case EBT_F16: hipLaunchKernelGGL(query_liked_kernel<EBT_F16>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, row_offset, q64); break;
+    default: hipLaunchKernelGGL(query_liked_kernel<EBT_F64>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, row_offset, q64); break;
   }
   return launch_check("query_liked_kernel");
 }

@@ -75,7 +75,7 @@ def csr_from_lists(lists: Sequence[Sequence[int]], device) -> Tuple[torch.Tensor
     off = [0]
     flat = []
     for l in lists:
-        flat.extend(sorted(int(v) for v in l))  # sorted: ebt_cosine_topk binary-searches them
+        flat.extend(sorted(int(v) for v in l))  # sorted: ebt_cosine_topk_prepared binary-searches them
         off.append(len(flat))
     o = torch.tensor(off, dtype=torch.int64, device=device)
     r = torch.tensor(flat if flat else [0], dtype=torch.int64, device=device)
@@ -238,7 +238,7 @@ def run_pipeline(catalog: Catalog, qb: QueryBatch, k: int, kprime: int,
                  exclude: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
                  chunk_rows: Optional[int] = None, timer: Optional[_lib.Timer] = None,
                  workspace: Optional[torch.Tensor] = None, flags: int = 0):
-    """One ebt_cosine_topk call. Returns (scores f64 [B,k], rows i64 [B,k], certified i32 [B]);
+    """One ebt_cosine_topk_prepared call. Returns (scores f64 [B,k], rows i64 [B,k], certified i32 [B]);
     certified is 1 (exact), 0 (widen k') or -1 (fused candidate list overflowed: run unfused)."""
     dev = catalog.device
     st = stream_of(dev)
@@ -253,7 +253,7 @@ def run_pipeline(catalog: Catalog, qb: QueryBatch, k: int, kprime: int,
     out_r = torch.empty((B, k), dtype=torch.int64, device=dev)
     cert = torch.empty(B, dtype=torch.int32, device=dev)
     eo, er = (exclude if exclude is not None else (None, None))
-    call("ebt_cosine_topk", ptr(qb.q64), ptr(qb.qimg), ptr(qb.qscale), ptr(qb.eps), B, B_pad,
+    call("ebt_cosine_topk_prepared", ptr(qb.q64), ptr(qb.qimg), ptr(qb.qscale), ptr(qb.eps), B, B_pad,
          ptr(catalog.data), catalog.dtype_code, catalog.ld, ptr(catalog.gnorm), ptr(catalog.image),
          ptr(catalog.cscale), catalog.img_dtype, catalog.ld_img, catalog.n, catalog.d,
          catalog.d_pad, catalog.row_offset, ptr(eo), ptr(er), k, kprime, chunk, flags, ptr(workspace),
@@ -306,7 +306,7 @@ def sample_maxima(catalog: Catalog, qb: QueryBatch, tiles: int,
     """ebt_cosine_sample: `tiles` evenly spaced full 256-row tiles of this catalog (shard)
     through the screening GEMM, keeping the max of every 64-row subgroup: [B_pad, 4 tiles] f32."""
     stride = (catalog.n // 256) // tiles
-    if stride > 1 and stride % 2 == 0:  # odd, as ebt_cosine_topk's own sample (api.hip)
+    if stride > 1 and stride % 2 == 0:  # odd, as ebt_cosine_topk_prepared's own sample (api.hip)
         stride -= 1
     out = torch.empty((qb.B_pad, 4 * tiles), dtype=torch.float32, device=catalog.device)
     call("ebt_cosine_sample", ptr(qb.qimg), ptr(qb.qscale), qb.B_pad, ptr(catalog.image),
@@ -390,6 +390,10 @@ def score_topk_submit(catalog: Catalog, k: int, queries: Optional[torch.Tensor] 
     the fused wave-merge screen applies (k' <= 512), the shard is screened at theta
     (ebt_cosine_screen_at) and a query whose theta exceeds t_floor - eps is rerun unfused.
     """
+    if t_floor_hook is None and theta_hook is None and liked_sum_hook is None and \
+            liked_counts is None:
+        # one catalog (or a shard queried on its own): the C ABI's self-contained path
+        return _submit_c(catalog, k, queries, liked, exclude, kprime, chunk_rows, timer, fuse)
     g = score_topk_stages(catalog, k, queries=queries, liked=liked, exclude=exclude,
                           kprime=kprime, chunk_rows=chunk_rows, timer=timer,
                           liked_counts=liked_counts, liked_sum_hook=liked_sum_hook, fuse=fuse,
@@ -397,6 +401,79 @@ def score_topk_submit(catalog: Catalog, k: int, queries: Optional[torch.Tensor] 
     next(g)
     next(g)
     return next(g)
+
+
+@dataclass
+class PendingTopkC:
+    """A batch submitted through ebt_cosine_topk_submit (the C ABI's self-contained path): the
+    ebt_pending record plus every buffer it points at, kept alive until the finish."""
+    pending: "_lib.EbtPending"
+    catalog: Catalog
+    opt: "_lib.EbtOptions"
+    out_s: torch.Tensor
+    out_r: torch.Tensor
+    ws: torch.Tensor
+    cert_host: torch.Tensor
+    keep: tuple
+
+
+_SKLEARN_EMPTY = "Found array with 0 sample(s)"
+
+
+def _submit_c(catalog: Catalog, k: int, queries, liked, exclude, kprime, chunk_rows, timer,
+              fuse) -> PendingTopkC:
+    """score_topk_submit over ebt_cosine_topk_submit: query prep, the screen, the certificate
+    and every retry run inside libebert (include/ebert.h); Python only owns the buffers."""
+    import ctypes
+    if k < 1:
+        raise EbertError("k must be >= 1")
+    dev = catalog.device
+    if (queries is None) == (liked is None):
+        raise EbertError("pass exactly one of queries= or liked=")
+    if exclude is not None:
+        exclude = (csr_from_lists(exclude, dev) if not isinstance(exclude, tuple)
+                   else csr_sorted(*exclude))
+    q_ptr, q_dt, ldq, lo, lr = None, 0, 0, None, None
+    if queries is not None:
+        require_cuda(queries, "queries")
+        if queries.dim() != 2 or queries.shape[1] != catalog.d:
+            raise EbertError(f"queries must be [B, {catalog.d}], got {tuple(queries.shape)}")
+        if queries.dtype not in DTYPE_CODE:
+            raise EbertError(f"unsupported query dtype {queries.dtype}")
+        if queries.stride(1) != 1:
+            queries = queries.contiguous()
+        B = int(queries.shape[0])
+        q_ptr, q_dt, ldq = ptr(queries), DTYPE_CODE[queries.dtype], int(queries.stride(0))
+    else:
+        lo, lr = liked if isinstance(liked, tuple) else csr_from_lists(liked, dev)
+        B = int(lo.numel()) - 1
+    if B < 1:
+        raise EbertError("empty query batch")
+    opt = _lib.EbtOptions(kprime=int(kprime or 0), flags=0 if fuse else _lib.EBT_FLAG_NO_FUSE,
+                          chunk_rows=int(chunk_rows or 0))
+    lib = _lib.load()
+    need = lib.ebt_workspace_bytes(ctypes.byref(catalog.cstruct), B, k, ctypes.byref(opt))
+    if need == 0:
+        raise EbertError(f"k={k} over a {catalog.n}-row catalog is not supported "
+                         f"(k <= {KPRIME_MAX} or k >= n)")
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    out_s = torch.empty((B, k), dtype=torch.float64, device=dev)
+    out_r = torch.empty((B, k), dtype=torch.int64, device=dev)
+    cert_host = torch.empty(B + 1, dtype=torch.int32, pin_memory=True)
+    pend = _lib.EbtPending()
+    eo, er = exclude if exclude is not None else (None, None)
+    try:
+        call("ebt_cosine_topk_submit", ctypes.byref(catalog.cstruct), q_ptr, q_dt, B, ldq,
+             ptr(lo), ptr(lr), k, ptr(eo), ptr(er), ctypes.byref(opt), ptr(ws), need,
+             ptr(out_s), ptr(out_r), ptr(cert_host), ctypes.byref(pend),
+             timer.handle if timer is not None else None, stream_of(dev))
+    except EbertError as e:
+        msg = str(e)
+        if _SKLEARN_EMPTY in msg:   # lib.py:51 on a user without liked movies (sklearn)
+            raise ValueError(msg[msg.index(_SKLEARN_EMPTY):]) from None
+        raise
+    return PendingTopkC(pend, catalog, opt, out_s, out_r, ws, cert_host,
+                        (queries, lo, lr, eo, er))
 
 
 def score_topk_stages(catalog: Catalog, k: int, queries: Optional[torch.Tensor] = None,
@@ -452,8 +529,12 @@ def score_topk_stages(catalog: Catalog, k: int, queries: Optional[torch.Tensor] 
                       s, r, cert, cert_host, ready)
 
 
-def score_topk_finish(p: "PendingTopk") -> Tuple[torch.Tensor, torch.Tensor]:
+def score_topk_finish(p) -> Tuple[torch.Tensor, torch.Tensor]:
     """Wait for a submitted batch, run its retries, return (scores f64 [B, k], rows i64 [B, k])."""
+    if isinstance(p, PendingTopkC):
+        import ctypes
+        call("ebt_cosine_topk_finish", ctypes.byref(p.pending))
+        return p.out_s, p.out_r
     catalog, qb, k, k_eff, kp = p.catalog, p.qb, p.k, p.k_eff, p.kprime
     exclude, chunk_rows, timer, flags, n_cap = p.exclude, p.chunk_rows, p.timer, p.flags, p.n_cap
     s, r, cert = p.s, p.r, p.cert

@@ -50,6 +50,30 @@ def test_workspace_grows_with_chunks():
     assert fused < many  # the fused screen materialises only the head rows' scores
 
 
+def test_self_contained_sizing_without_gpu():
+    """ebt_catalog_state_bytes / ebt_workspace_bytes (the self-contained path's sizing) are host
+    arithmetic: the catalog struct's device pointers are never dereferenced here."""
+    import ctypes
+    from robot_ebert_amd import _lib
+    lib = _lib.load()
+    n, d = 1_000_000, 1536
+    f32 = lib.ebt_catalog_state_bytes(None, _lib.EBT_F32, n, d, d)
+    assert f32 >= n * 8 + n * 4 + n * d * 2          # norms + inverse norms + f16 image
+    aligned = 1 << 20                                # native f16, d % 64 == 0: no image copy
+    assert lib.ebt_catalog_state_bytes(aligned, _lib.EBT_F16, n, d, d) < n * 16
+    assert lib.ebt_catalog_state_bytes(None, _lib.EBT_F32, 0, d, d) == 0
+    fake = 1 << 30
+    cat = _lib.EbtCatalog(data=fake, dtype=_lib.EBT_F32, d=d, n=n, ld=d, row_offset=0,
+                          gnorm64=fake, inv32=fake, image=fake, cscale=None,
+                          img_dtype=_lib.EBT_F16, ld_img=d, d_pad=d, native=0, u_cat=2.0 ** -11)
+    ws = lib.ebt_workspace_bytes(ctypes.byref(cat), 4096, 100, None)
+    first = lib.ebt_cosine_topk_workspace(4096, 4096, n, 200, (4 << 30) // (4 * 4096) // 128 * 128, 0)
+    assert ws > first > 0                            # first pass + retry area + prepared queries
+    assert lib.ebt_workspace_bytes(ctypes.byref(cat), 4096, 5000, None) == 0   # k > 4096 < n
+    bad = _lib.EbtOptions(kprime=0, flags=0, chunk_rows=100)                   # not % 128
+    assert lib.ebt_workspace_bytes(ctypes.byref(cat), 4096, 100, ctypes.byref(bad)) == 0
+
+
 def test_no_cpu_fallback_on_cpu_tensors():
     import torch
     from robot_ebert_amd import EbertError, Catalog

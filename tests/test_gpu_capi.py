@@ -1,0 +1,162 @@
+"""GPU: the self-contained C ABI (include/ebert.h: ebt_catalog_init, ebt_workspace_bytes,
+ebt_cosine_topk) driven through a bare ctypes binding, the way a non-Python caller (cgo / JNI /
+N-API) would bind it -- no robot_ebert_amd import; torch only allocates device memory.
+
+Every golden case the reference produced (tests/golden: sklearn cosine_similarity + pandas sort
+top-k for nine seeded shapes / dtypes, and get_user_recs of /root/reference/src/backend/app/
+lib.py:32-63 for the 20 C1 users) must come out of ONE ebt_cosine_topk call per batch: rows
+bit-exact, scores within 1e-12, the sklearn ValueError text for a user without liked movies.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from inputs import COS_CASES, c1_catalog, cos_case_inputs
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+LIB = os.path.join(ROOT, "robot_ebert_amd", "libebert.so")
+TDT = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16, "f64": torch.float64}
+CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3}
+VP, I32, I64, SZ, F32 = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t,
+                         ctypes.c_float)
+
+
+class Catalog(ctypes.Structure):   # struct ebt_catalog
+    _fields_ = [("data", VP), ("dtype", I32), ("d", I32), ("n", I64), ("ld", I64),
+                ("row_offset", I64), ("gnorm64", VP), ("inv32", VP), ("image", VP),
+                ("cscale", VP), ("img_dtype", I32), ("ld_img", I32), ("d_pad", I32),
+                ("native", I32), ("u_cat", F32)]
+
+
+@pytest.fixture(scope="module")
+def lib():
+    h = ctypes.CDLL(LIB)
+    h.ebt_last_error.restype = ctypes.c_char_p
+    h.ebt_catalog_state_bytes.argtypes = [VP, ctypes.c_int, I64, I32, I64]
+    h.ebt_catalog_state_bytes.restype = SZ
+    h.ebt_catalog_init.argtypes = [ctypes.POINTER(Catalog), VP, ctypes.c_int, I64, I32, I64, I64,
+                                   VP, SZ, VP]
+    h.ebt_workspace_bytes.argtypes = [ctypes.POINTER(Catalog), I64, I32, VP]
+    h.ebt_workspace_bytes.restype = SZ
+    h.ebt_cosine_topk.argtypes = [ctypes.POINTER(Catalog), VP, ctypes.c_int, I64, I64, VP, VP,
+                                  I32, VP, VP, VP, VP, SZ, VP, VP, VP, VP]
+    return h
+
+
+def P(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def make_catalog(lib, emb: torch.Tensor):
+    st = torch.cuda.current_stream(emb.device).cuda_stream
+    n, d = emb.shape
+    need = lib.ebt_catalog_state_bytes(P(emb), CODE[emb.dtype], n, d, emb.stride(0))
+    state = torch.empty(need, dtype=torch.uint8, device=emb.device)
+    cat = Catalog()
+    rc = lib.ebt_catalog_init(ctypes.byref(cat), P(emb), CODE[emb.dtype], n, d, emb.stride(0), 0,
+                              P(state), need, st)
+    assert rc == 0, lib.ebt_last_error()
+    return cat, state
+
+
+def csr(lists, dev):
+    off = np.zeros(len(lists) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(x) for x in lists])
+    flat = np.concatenate([np.sort(np.asarray(x, dtype=np.int64)) for x in lists]) \
+        if off[-1] else np.zeros(1, dtype=np.int64)
+    return torch.from_numpy(off).to(dev), torch.from_numpy(flat).to(dev)
+
+
+def topk(lib, cat, k, dev, q=None, liked=None, excl=None):
+    """One ebt_cosine_topk call; returns (rc, scores, rows)."""
+    B = q.shape[0] if q is not None else liked[0].numel() - 1
+    ws_bytes = lib.ebt_workspace_bytes(ctypes.byref(cat), B, k, None)
+    assert ws_bytes > 0
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    s = torch.empty((B, k), dtype=torch.float64, device=dev)
+    r = torch.empty((B, k), dtype=torch.int64, device=dev)
+    lo, lr = liked if liked is not None else (None, None)
+    eo, er = excl if excl is not None else (None, None)
+    rc = lib.ebt_cosine_topk(ctypes.byref(cat), P(q), CODE[q.dtype] if q is not None else 0, B,
+                             q.stride(0) if q is not None else 0, P(lo), P(lr), k, P(eo), P(er),
+                             None, P(ws), ws_bytes, P(s), P(r), None,
+                             torch.cuda.current_stream(dev).cuda_stream)
+    return rc, s.cpu().numpy(), r.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", sorted(COS_CASES))
+def test_capi_cos_topk_golden(cuda_device, lib, name):
+    case = COS_CASES[name]
+    q, c, excl = cos_case_inputs(case)
+    gold = np.load(os.path.join(GOLD, "cos_topk_small.npz"))
+    dt = TDT[case["dtype"]]
+    emb = torch.from_numpy(c).to(cuda_device).to(dt)
+    qt = torch.from_numpy(q).to(cuda_device).to(dt)
+    cat, state = make_catalog(lib, emb)
+    rc, s, r = topk(lib, cat, case["k"], cuda_device, q=qt,
+                    excl=csr(excl, cuda_device) if excl is not None else None)
+    assert rc == 0, lib.ebt_last_error()
+    r_ref = gold[f"{name}_rows"].astype(np.int64)
+    np.testing.assert_array_equal(r, r_ref)
+    m = r_ref >= 0
+    np.testing.assert_allclose(s[m], gold[f"{name}_scores"][m], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("k", [10, 10000])
+def test_capi_user_recs_golden(cuda_device, lib, k):
+    """get_user_recs (lib.py:32-63) for the 20 C1 users: liked rows -> mean cosine query,
+    rated rows excluded; one batched call for every user with a liked movie, the sklearn
+    ValueError text (via ebt_last_error) for the user without one, [] for no ratings."""
+    with open(os.path.join(GOLD, "c1_collab.json")) as f:
+        gold = json.load(f)
+    ids, c = c1_catalog()
+    pos = {t: i for i, t in enumerate(ids)}
+    emb = torch.from_numpy(c).to(cuda_device)          # float64, as constants.py:56
+    cat, state = make_catalog(lib, emb)
+    users, liked, rated, want = [], [], [], []
+    for uid, rec in gold["users"].items():
+        ratings = [(t, r) for t, r in rec["ratings"] if t in pos]       # lib.py:44
+        w = rec[f"k{k}"]
+        if not rec["ratings"]:
+            assert w == []                                              # lib.py:39-40
+            continue
+        li = [pos[t] for t, r in ratings if r >= 3.5]                   # lib.py:47
+        ra = [pos[t] for t, r in ratings]                               # lib.py:48
+        if isinstance(w, dict):                                         # no liked movie
+            rc, _, _ = topk(lib, cat, k, cuda_device, liked=csr([li], cuda_device),
+                            excl=csr([ra], cuda_device))
+            assert rc == -1
+            assert lib.ebt_last_error().decode() == w["message"]
+            continue
+        users.append(uid)
+        liked.append(li)
+        rated.append(ra)
+        want.append(w)
+    rc, s, r = topk(lib, cat, k, cuda_device, liked=csr(liked, cuda_device),
+                    excl=csr(rated, cuda_device))
+    assert rc == 0, lib.ebt_last_error()
+    for b, (uid, w) in enumerate(zip(users, want)):
+        m = r[b] >= 0
+        got_ids = [ids[i] for i in r[b][m]]
+        assert got_ids == [x[0] for x in w], uid
+        np.testing.assert_allclose(s[b][m], [x[1] for x in w], rtol=0, atol=1e-12)
+        assert np.all(np.isnan(s[b][~m]))
+
+
+def test_capi_errors(cuda_device, lib):
+    """Unsorted exclusions and out-of-catalog liked rows fail loudly (EBT_EINVAL)."""
+    emb = torch.randn((1000, 64), device=cuda_device)
+    cat, state = make_catalog(lib, emb)
+    q = torch.randn((4, 64), device=cuda_device)
+    off = torch.tensor([0, 2, 2, 2, 2], dtype=torch.int64, device=cuda_device)
+    rows = torch.tensor([9, 3], dtype=torch.int64, device=cuda_device)   # unsorted segment
+    rc, _, _ = topk(lib, cat, 10, cuda_device, q=q, excl=(off, rows))
+    assert rc == -1 and b"sorted" in lib.ebt_last_error()
+    rc, _, _ = topk(lib, cat, 10, cuda_device, liked=csr([[1, 5000]], cuda_device))
+    assert rc == -1 and b"not in the catalog" in lib.ebt_last_error()

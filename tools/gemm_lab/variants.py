@@ -69,7 +69,7 @@ def build(name):
     subprocess.run(["/opt/rocm/bin/hipcc"] + flags + ["-c", os.path.join(work, "screen_gemm.hip"),
                                                       "-o", obj], check=True)
     others = [os.path.join(CSRC, "build", f) for f in
-              ("api.o", "select_topk.o", "prep.o", "rescore.o", "als.o")]
+              ("api.o", "driver.o", "select_topk.o", "prep.o", "rescore.o", "als.o")]
     os.makedirs(OUT, exist_ok=True)
     lib = os.path.join(OUT, f"libebert_{name}.so")
     subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "--offload-arch=gfx950", "-o", lib, obj]

@@ -1,4 +1,4 @@
-"""Debug: certificate histogram of one ebt_cosine_topk call at a bench shape (no retries)."""
+"""Debug: certificate histogram of one ebt_cosine_topk_prepared call at a bench shape (no retries)."""
 import os
 import sys
 
