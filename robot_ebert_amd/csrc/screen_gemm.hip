@@ -304,14 +304,6 @@ __device__ __forceinline__ void wait_vm() {
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else static_assert(N == 0, "unsupported vmcnt");
 }
-// s_waitcnt with an immediate chosen at run time (near the last tiles fewer loads follow).
-__device__ __forceinline__ void wait_vm_halves(int halves_after) {
-  if (halves_after >= 4) wait_vm<8>();
-  else if (halves_after == 3) wait_vm<6>();
-  else if (halves_after == 2) wait_vm<4>();
-  else if (halves_after == 1) wait_vm<2>();
-  else wait_vm<0>();
-}
 
 // s_barrier is a no-memory intrinsic to LLVM: the empty asm with a memory clobber keeps LDS
 // reads from being hoisted above it at IR level; sched_barrier(0) does the same for the
@@ -326,19 +318,33 @@ __device__ __forceinline__ void qp_barrier() {
 
 
 // =============================================================================================
-// Pipelined quadrant phases (qp2): ONE barrier per phase, and the fragments of the NEXT phase
-// are read while the current phase's 16 MFMAs run (interleaved by sched_group_barrier), so LDS
-// reads and barriers do not sit between MFMA clusters. Register sets: A0 / A1 fragments (32 VGPRs each) and two
-// B sets whose roles swap every K-tile (B0(t) is read in Q4(t-1) and kept until Q4(t), B1(t) is
-// read in Q1(t)), 224 VGPRs with the accumulators.
-// Half-tile schedule (phase P = 4t + quadrant issues sequence index P + 7, index = 4u + type
-// with type A0, B0, B1, A1): a region is restaged >= 2 phases after its last ds_read issue and
-// `s_waitcnt vmcnt(8)` before the barrier of every phase that reads retires exactly the half
-// that phase reads (A0/B0 of t+1 in Q4(t), B1(t) in Q1(t), A1(t) in Q2(t)).
+// Persistent pipelined quadrant phases (qp2): ONE barrier per phase, the fragments of the NEXT
+// phase are read while the current phase's 16 MFMAs run (interleaved by sched_group_barrier),
+// and each workgroup walks several output tiles with the LDS-DMA stream running straight across
+// the tile boundary: the last two K-tiles of tile s stage the first two K-tiles of tile s+1, so
+// the next tile's operands are in flight during the epilogue (no per-tile prologue latency, no
+// per-tile workgroup launch). Register sets: A0 / A1 fragments (32 VGPRs each) and two B sets
+// whose roles swap every K-tile (B0(t) is read in Q4(t-1) and kept until Q4(t), B1(t) is read in
+// Q1(t)), 224 VGPRs with the accumulators.
+// Half-tile schedule (K-tile t issues A1(t+1) in Q1 and A0/B0/B1(t+2) in Q2/Q3/Q4; K-tile
+// indices run on across tiles, an even K-tile count keeps buffer = K-tile & 1): a region is
+// restaged >= 2 phases after its last ds_read issue and `s_waitcnt vmcnt(8)` before the barrier
+// of every phase that reads retires exactly the half that phase reads (A0/B0 of t+1 in Q4(t),
+// B1(t) in Q1(t), A1(t) in Q2(t)); every other load in the stream (the epilogue parameters)
+// only makes a counted wait stricter. The last tile of a workgroup restages its own first
+// K-tiles into dead regions (no branch in the MFMA blocks) and drains the stream before exit.
+// Tile walk: the tiles of the launch are split into 8 contiguous ranges, one per XCD
+// (workgroup b runs on XCD b & 7), and the n_x workgroups of an XCD take its range round-robin,
+// so the tiles in flight on one XCD are consecutive -- groups of 4 catalog tiles walked
+// query-tile-major, a catalog tile fetched about once per XCD and re-read from its L2.
+// An odd K-tile count runs one extra all-zero K-tile (a descriptor with no records).
 // =============================================================================================
 enum { P_A0 = 0, P_B0 = 1, P_B1 = 2, P_A1 = 3 };
-__device__ __forceinline__ constexpr int p_half_off(int type) {
-  return type == P_A0 ? 0 : type == P_A1 ? QP_HALF : type == P_B0 ? 2 * QP_HALF : 3 * QP_HALF;
+// Ring layout by half-tile, buffer innermost: A0 | A1 | B0 | B1, each [buffer 0 | buffer 1] of
+// 16 KiB, so every catalog fragment lies within 64 KiB of one lane base and every query fragment
+// within 64 KiB of another (ds_read_b128's 16-bit immediate covers both buffers).
+__device__ __forceinline__ constexpr int p_half_addr(int type, int buf) {
+  return (type == P_A0 ? 0 : type == P_A1 ? 2 : type == P_B0 ? 4 : 6) * QP_HALF + buf * QP_HALF;
 }
 
 template <bool BF16>
@@ -357,275 +363,386 @@ __device__ __forceinline__ void qp2_mma(f32x4_t (&acc)[4][2], const u16x8_t (&a)
 // only the MAX score, S[q][4 ct + 2 ah + wa] -- 64x less output than the scores).
 enum { EPI_STORE = 0, EPI_FILTER = 1, EPI_POOL = 2 };
 
-template <bool BF16, int EPI>
-__global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
-    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ C, int64_t ld_img,
-    int64_t n_rows, int n_qtiles, int64_t n_ctiles, int ktiles,
-    const float* __restrict__ qscale, const float* __restrict__ cscale, EpiArgs e,
-    int64_t cstride) {
+// LDS after the 128 KiB ring: hit counters (1 KiB), the tile's query scales / thresholds / row
+// scales (3 KiB, LDS-DMA'd per tile), the filter epilogue's hit staging (QP_STG_SLOTS 16-byte
+// slots per lane).
+constexpr int QP_PARAM = 1024 + 3 * QP_TILE * 4;
+constexpr int QP_STG_SLOTS = 2;
+constexpr int QP_STG = QP_THREADS * QP_STG_SLOTS * 16;
+constexpr int QP_LDS_TOTAL = QP_LDS + QP_PARAM + QP_STG;
+static_assert(QP_LDS_TOTAL <= 160 * 1024, "LDS budget");
+
+// Epilogue LDS reads in inline asm (each completes before it returns). The compiler treats any
+// LDS read as possibly aliasing the LDS-DMA writes in flight and would put s_waitcnt vmcnt(0) in
+// front of it, draining the next tile's operand stream (and the hit stores) in the epilogue; the
+// parameter arrays and staging slots are disjoint from the ring by construction.
+__device__ __forceinline__ float lds_f32(const void* p) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(v) : "v"((uint32_t)(uintptr_t)p) : "memory");
+  return v;
+}
+__device__ __forceinline__ f32x4_t lds_f32x4(const void* p) {
+  f32x4_t v;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(v) : "v"((uint32_t)(uintptr_t)p) : "memory");
+  return v;
+}
+// Four query columns' scale and threshold (8 reads, one wait).
+__device__ __forceinline__ void lds_qs_th4(const float* qs, const float* th, const int (&ql)[4],
+                                           float (&q)[4], float (&t)[4]) {
+  asm volatile(
+      "ds_read_b32 %0, %8\n\tds_read_b32 %1, %9\n\tds_read_b32 %2, %10\n\tds_read_b32 %3, %11\n\t"
+      "ds_read_b32 %4, %12\n\tds_read_b32 %5, %13\n\tds_read_b32 %6, %14\n\tds_read_b32 %7, %15\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]),
+        "=&v"(t[3])
+      : "v"((uint32_t)(uintptr_t)(qs + ql[0])), "v"((uint32_t)(uintptr_t)(qs + ql[1])),
+        "v"((uint32_t)(uintptr_t)(qs + ql[2])), "v"((uint32_t)(uintptr_t)(qs + ql[3])),
+        "v"((uint32_t)(uintptr_t)(th + ql[0])), "v"((uint32_t)(uintptr_t)(th + ql[1])),
+        "v"((uint32_t)(uintptr_t)(th + ql[2])), "v"((uint32_t)(uintptr_t)(th + ql[3]))
+      : "memory");
+}
+// A staged hit block with its query's scale / threshold and the rows' scales (one wait).
+__device__ __forceinline__ void lds_hit_block(const void* stg, const float* qs, const float* th,
+                                              const float* cs, f32x4_t& a, float& q, float& t,
+                                              f32x4_t& c) {
+  asm volatile(
+      "ds_read_b128 %0, %4\n\tds_read_b32 %1, %5\n\tds_read_b32 %2, %6\n\tds_read_b128 %3, %7\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(a), "=&v"(q), "=&v"(t), "=&v"(c)
+      : "v"((uint32_t)(uintptr_t)stg), "v"((uint32_t)(uintptr_t)qs), "v"((uint32_t)(uintptr_t)th),
+        "v"((uint32_t)(uintptr_t)cs)
+      : "memory");
+}
+__device__ __forceinline__ uint32_t lds_add_rtn(uint32_t* p, uint32_t v) {
+  uint32_t r;
+  asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(r) : "v"((uint32_t)(uintptr_t)p), "v"(v) : "memory");
+  return r;
+}
+__device__ __forceinline__ float4 lds_float4(const void* p) {
+  const f32x4_t v = lds_f32x4(p);
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// One output tile of the walk: catalog tile ct (rows c0.., image rows c0s..), query tile q0.
+struct QpTile {
+  int64_t ct, c0, c0s, q0;
+};
+
+// The kernel's arguments. The kernel re-reads them from the kernarg segment where they are used
+// (scalar loads through an opaque copy of the segment pointer), so that none stays in SGPRs
+// through the K-loop and the epilogue: the filter epilogue needs most of the 102 SGPRs.
+struct QpArgs {
+  const uint16_t* Q;
+  const uint16_t* C;
+  int64_t ld_img;
+  int64_t n_rows;
+  const float* qscale;
+  const float* cscale;
+  int64_t cstride;
+  int n_qtiles, n_ctiles, ktiles, pad_;
+  EpiArgs e;
+};
+typedef const __attribute__((address_space(4))) QpArgs* QpArgsK;
+__device__ __forceinline__ QpArgsK qp_args() {
+  QpArgsK p = (QpArgsK)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+template <bool BF16, int EPI, bool ODD>
+__global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs args) {
+  (void)args;  // read through qp_args()
   constexpr bool FILTER = EPI == EPI_FILTER;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int64_t bid = blockIdx.x;
+  const int bid = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-  const int64_t nwg = (int64_t)n_qtiles * n_ctiles;
-  const int64_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int64_t L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int64_t per_group = (int64_t)QP_GROUP_C * n_qtiles;
-  const int64_t g = L / per_group, w = L - g * per_group;
-  const int64_t gc_rem = n_ctiles - g * QP_GROUP_C;
-  const int64_t gc = gc_rem < QP_GROUP_C ? gc_rem : QP_GROUP_C;
-  const int64_t ct = g * QP_GROUP_C + w % gc;
-  const int64_t qt = w / gc;
-  const int64_t c0 = ct * 256;
-  // catalog row of the tile's first row: c0, or ct * cstride for a strided sample of full tiles
-  // (store mode; n_rows then counts the sample's rows and the scores stay dense)
-  const int64_t c0s = ct * cstride;
-  const int64_t q0 = qt * 256;
-  // after the K-tile ring: hits per query of the tile (filter mode), then the epilogue's
-  // per-query scale / threshold and per-row scale, loaded before the prologue's LDS-DMA so they
-  // retire with its first wait instead of stalling the epilogue
+  // ---- the workgroup's tiles: L = Lbeg + j, + n_x, ... < Lend ----
+  const int nwg = qp_args()->n_qtiles * qp_args()->n_ctiles;
+  const int G = gridDim.x;
+  const int xcd = bid & 7, j = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int Lbeg = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int Lend = Lbeg + q8 + (xcd < r8 ? 1 : 0);
+  const int n_x = (G - xcd + 7) >> 3;  // workgroups on this XCD
+  int L = Lbeg + j;
+  if (L >= Lend) return;
+  auto tile_at = [&](int Lt) {
+    const QpArgsK A = qp_args();
+    const int per_group = QP_GROUP_C * A->n_qtiles, n_ctiles = A->n_ctiles;
+    QpTile T;
+    const int g = Lt / per_group, w = Lt - g * per_group;
+    const int gc_rem = n_ctiles - g * QP_GROUP_C;
+    const int gc = gc_rem < QP_GROUP_C ? gc_rem : QP_GROUP_C;
+    T.ct = g * QP_GROUP_C + w % gc;
+    const int qt = w / gc;
+    T.c0 = T.ct * QP_TILE;
+    // catalog row of the tile's first row: c0, or ct * cstride for a strided sample of full
+    // tiles (store / pool mode; n_rows then counts the sample's rows and the scores stay dense)
+    T.c0s = T.ct * A->cstride;
+    T.q0 = (int64_t)qt * QP_TILE;
+    return T;
+  };
+  // the buffer descriptors of a tile's operands (out-of-range catalog rows read as 0); only the
+  // current tile's pair stays live through the K-loop, the next tile's is made for the last two
+  // K-tiles, and the tile geometry is recomputed for the epilogue (SGPR budget)
+  auto rsrc_c = [&](const QpTile& T) {
+    const QpArgsK A = qp_args();
+    const int64_t c_rem = (A->n_rows - T.c0) * A->ld_img * 2;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(A->C + T.c0s * A->ld_img), 0,
+                                             (int)(c_rem < 0x7fffffffLL ? c_rem : 0x7fffffffLL),
+                                             0x00020000);
+  };
+  auto rsrc_q = [&](const QpTile& T) {
+    const QpArgsK A = qp_args();
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(A->Q + T.q0 * A->ld_img), 0,
+                                             (int)(QP_TILE * A->ld_img * 2), 0x00020000);
+  };
+
   uint32_t* lcnt = (uint32_t*)(smem + QP_LDS);
   float* lqs = (float*)(smem + QP_LDS + 1024);
   float* lth = lqs + QP_TILE;
   float* lcs = lth + QP_TILE;
-  if constexpr (FILTER) {
-    if (tid < QP_TILE) lcnt[tid] = 0u;
-  }
-  float pre_a = 1.f, pre_b = 0.f;
   if (tid < QP_TILE) {
-    pre_a = qscale[q0 + tid];
-    if constexpr (FILTER) pre_b = e.thr[q0 + tid];
-  } else {
-    const int64_t r = tid - QP_TILE;
-    pre_a = (cscale && c0 + r < n_rows) ? cscale[c0s + r] : 1.f;
+    lcnt[tid] = 0u;
+    if (!qp_args()->cscale) lcs[tid] = 1.f;
   }
+  // the tile's epilogue parameters by LDS-DMA (one 1 KiB piece per array, waves 0..2): they
+  // travel in the operand stream and are retired by its counted waits
+  auto issue_params = [&](const QpTile& T) {
+    const QpArgsK A = qp_args();
+    if (wave == 0) {
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(A->qscale + T.q0), 0, QP_TILE * 4, 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lqs, 16, lane * 16, 0, 0, 0);
+    } else if (wave == 1 && FILTER) {
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(A->e.thr + T.q0), 0, QP_TILE * 4, 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lth, 16, lane * 16, 0, 0, 0);
+    } else if (wave == 2 && A->cscale) {
+      const int64_t rem = A->n_rows - T.c0;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(A->cscale + T.c0s), 0, (int)(rem < QP_TILE ? rem * 4 : QP_TILE * 4), 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lcs, 16, lane * 16, 0, 0, 0);
+    }
+  };
 
   const int wa = wave >> 2;
   const int wb = wave & 3;
-  const int fr = lane & 15;
-  int a_off[4][2], b_off[2][2];
+  // Per-lane LDS fragment offsets (swizzled) and the LDS-DMA lane offset. They are recomputed at
+  // the top of every tile from an opaque copy of the lane id: live through the K-loop only, not
+  // through the epilogue (whose accumulators + temporaries need the rest of the 256 VGPRs).
+  // Fragment (i, ks) of a half at row base + 16 i has row & 7 == fr & 7, so its swizzled offset
+  // is base(ks) + i * 2048: one lane base per operand and k-step, the half, buffer and i are
+  // ds_read immediates (p_half_addr).
+  int a_base[2], b_base[2], voff, wdst, piece_step, half_step, kt, ktiles;
+  auto set_geom = [&]() {
+    // the wave's LDS-DMA destination offset, opaque too: the 16 destination addresses derived
+    // from it stay out of the SGPRs held through the epilogue
+    int w = wave * 2048;
+    asm volatile("" : "+s"(w));
+    wdst = w;
+    int l = tid;
+    asm volatile("" : "+v"(l));
+    l &= 63;
+    const int f = l & 15;
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const int c = ks * 4 + (lane >> 4);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = wa * 64 + i * 16 + fr;
-      a_off[i][ks] = r * 128 + ((c ^ (r & 7)) << 4);
+    for (int ks = 0; ks < 2; ++ks) {
+      const int sw = ((ks * 4 + (l >> 4)) ^ (f & 7)) << 4;
+      a_base[ks] = (int)(uintptr_t)smem + (wa * 64 + f) * 128 + sw;
+      b_base[ks] = (int)(uintptr_t)smem + p_half_addr(P_B0, 0) + (wb * 32 + f) * 128 + sw;
     }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r = wb * 32 + j * 16 + fr;
-      b_off[j][ks] = r * 128 + ((c ^ (r & 7)) << 4);
-    }
-  }
+    // LDS-DMA through buffer descriptors (T8): one 32-bit per-lane offset serves every
+    // half-tile. lane: row (wave*16 + (lane>>3)) of the half, 16-byte chunk (lane&7)^(lane>>3)
+    const QpArgsK A = qp_args();
+    voff = (int)((wave * 16 + (l >> 3)) * A->ld_img * 2) + (((l & 7) ^ (l >> 3)) << 4);
+    piece_step = (int)(8 * A->ld_img * 2);
+    half_step = (int)(128 * A->ld_img * 2);
+    kt = A->ktiles + (ODD ? 1 : 0);  // K-tiles per output tile (even)
+    ktiles = A->ktiles;
+  };
 
   f32x4_t acc0[4][2], acc1[4][2], acc2[4][2], acc3[4][2];
+  auto zero_acc = [&]() {
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      acc0[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      acc1[i][j] = acc0[i][j];
-      acc2[i][j] = acc0[i][j];
-      acc3[i][j] = acc0[i][j];
-    }
+      for (int jj = 0; jj < 2; ++jj) {
+        acc0[i][jj] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        acc1[i][jj] = acc0[i][jj];
+        acc2[i][jj] = acc0[i][jj];
+        acc3[i][jj] = acc0[i][jj];
+      }
+  };
 
-  // LDS-DMA through buffer descriptors (T8): one 32-bit per-lane offset serves every half-tile;
-  // rows past the end of the catalog fall outside num_records and read as 0 (never stored).
-  const int64_t row_bytes = ld_img * 2;
-  const int64_t c_rem = (n_rows - c0) * row_bytes;
-  const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(C + c0s * ld_img), 0, (int)(c_rem < 0x7fffffffLL ? c_rem : 0x7fffffffLL),
-      0x00020000);
-  const __amdgpu_buffer_rsrc_t rsQ = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(Q + q0 * ld_img), 0, (int)(256 * row_bytes), 0x00020000);
-  // lane: row (wave*16 + (lane>>3)) of the half, 16-byte chunk (lane&7)^(lane>>3)
-  const int voff = (int)((wave * 16 + (lane >> 3)) * row_bytes) + (((lane & 7) ^ (lane >> 3)) << 4);
-  const int piece_step = (int)(8 * row_bytes);
-  const int half_step = (int)(128 * row_bytes);
-  const int total = 4 * ktiles;
-  auto issue_u = [&](int idx) {  // no bounds check: the caller guarantees idx < total
-    const int tile = idx >> 2, type = idx & 3;
-    char* dst = smem + (tile & 1) * QP_BUF + p_half_off(type) + wave * 2048;
-    const int soff = tile * 128 + ((type == P_A1 || type == P_B1) ? half_step : 0);
-    const __amdgpu_buffer_rsrc_t rs = (type == P_A0 || type == P_A1) ? rsC : rsQ;
+  // half `type` of local K-tile kl of the tile with descriptors (rc, rq) into buffer `buf`
+  auto issue_h = [&](const __amdgpu_buffer_rsrc_t& rc, const __amdgpu_buffer_rsrc_t& rq, int kl,
+                     int type, int buf) {
+    char* dst = smem + p_half_addr(type, buf) + wdst;
+    const int soff = kl * 128 + ((type == P_A1 || type == P_B1) ? half_step : 0);
+    __amdgpu_buffer_rsrc_t rs = (type == P_A0 || type == P_A1) ? rc : rq;
+    if constexpr (ODD) rs = kl < ktiles ? rs : __builtin_amdgcn_make_buffer_rsrc((void*)0, 0, 0, 0x00020000);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)dst, 16, voff, soff, 0, 0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + 1024), 16, voff,
                                              soff + piece_step, 0, 0);
   };
-  auto issue = [&](int idx) {
-    if (idx < total) {
-      const int tile = idx >> 2, type = idx & 3;
-      char* dst = smem + (tile & 1) * QP_BUF + p_half_off(type) + wave * 2048;
-      const int soff = tile * 128 + ((type == P_A1 || type == P_B1) ? half_step : 0);
-      const __amdgpu_buffer_rsrc_t rs = (type == P_A0 || type == P_A1) ? rsC : rsQ;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)dst, 16, voff, soff, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + 1024), 16, voff,
-                                               soff + piece_step, 0, 0);
-    }
-  };
-  auto wait_for = [&](int needed, int last_issued) {
-    const int last = last_issued < total - 1 ? last_issued : total - 1;
-    const int n = last - needed;
-    wait_vm_halves(n > 0 ? n : 0);
-  };
-  auto read_a = [&](u16x8_t (&a)[4][2], const char* half) {
+  // fragments of half-tile `type` of buffer P (compile time)
+  auto read_a = [&](u16x8_t (&a)[4][2], int P, int type) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i][ks] = *(const u16x8_t*)(half + a_off[i][ks]);
+      for (int i = 0; i < 4; ++i)
+        a[i][ks] = *(const u16x8_t*)((lds_void*)(uintptr_t)(a_base[ks] + p_half_addr(type, P) + i * 2048));
   };
-  auto read_b = [&](u16x8_t (&b)[2][2], const char* half) {
+  auto read_b = [&](u16x8_t (&b)[2][2], int P, int type) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j][ks] = *(const u16x8_t*)(half + b_off[j][ks]);
+      for (int jj = 0; jj < 2; ++jj)
+        b[jj][ks] = *(const u16x8_t*)((lds_void*)(uintptr_t)(b_base[ks] + p_half_addr(type, P) - p_half_addr(P_B0, 0) + jj * 2048));
   };
 
   u16x8_t fa0[4][2], fa1[4][2], fbx[2][2], fby[2][2];
-  // prologue: sequence indices 0..6; A0(0), B0(0) into the A0 / X sets
-#pragma unroll
-  for (int idx = 0; idx < 7; ++idx) issue(idx);
-  wait_for(1, 6);
-  if (tid < QP_TILE) {
-    lqs[tid] = pre_a;
-    lth[tid] = pre_b;
-  } else {
-    lcs[tid - QP_TILE] = pre_a;
+  // prologue: the first tile's parameters, then K-tile 0 (A0, B0, B1, A1) and K-tile 1 (A0, B0,
+  // B1) in stream order
+  {
+    set_geom();
+    const QpTile T = tile_at(L);
+    issue_params(T);
+    const __amdgpu_buffer_rsrc_t rc = rsrc_c(T), rq = rsrc_q(T);
+    issue_h(rc, rq, 0, P_A0, 0);
+    issue_h(rc, rq, 0, P_B0, 0);
+    issue_h(rc, rq, 0, P_B1, 0);
+    issue_h(rc, rq, 0, P_A1, 0);
+    issue_h(rc, rq, 1, P_A0, 1);
+    issue_h(rc, rq, 1, P_B0, 1);
+    issue_h(rc, rq, 1, P_B1, 1);
   }
+  wait_vm<8>();  // A0(0), B0(0), B1(0)
+  zero_acc();
   qp_barrier();
-  read_a(fa0, smem + p_half_off(P_A0));
-  read_b(fbx, smem + p_half_off(P_B0));
-  wait_for(2, 6);  // B1(0), read in Q1(0)
 
-  // One tile of four phases. B0(t) lives in `s0`, B1(t) in `s1`; Q4 reads B0(t+1) into s1.
-// GUARD = false in the steady state (every issued half-tile exists): the LDS-DMA pieces then
-// live in the same basic block as the MFMAs and are spread between them by the
-// sched_group_barrier patterns (masks: 0x008 MFMA, 0x100 DS read, 0x020 VMEM read) instead of
-// sitting in front of the phase's first MFMA, where both waves of a SIMD stalled on their DMA
-// issue at once.
-#define QP2_ISSUE(IDX, GUARD)                                                                    \
-  {                                                                                              \
-    if (GUARD) issue(IDX);                                                                       \
-    else issue_u(IDX);                                                                           \
-  }
-#define QP2_TILE(T, s0, s1, GUARD)                                                                \
-  {                                                                                              \
-    const int t_ = (T);                                                                          \
-    const char* buf = smem + (t_ & 1) * QP_BUF;                                                  \
-    const char* nbuf = smem + ((t_ + 1) & 1) * QP_BUF;                                           \
-    /* Q1 (A0, B0): read B1(t) */                                                                \
-    qp_barrier();                                                                                \
-    QP2_ISSUE(4 * t_ + 7, GUARD);                                                                \
-    qp2_mma<BF16>(acc0, fa0, s0);                                                                \
-    read_b(s1, buf + p_half_off(P_B1));                                                          \
-    if (!(GUARD)) {                                                                              \
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
-      _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                         \
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                       \
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
-      }                                                                                          \
-    } else {                                                                                     \
-      _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_) {                                         \
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                       \
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
-      }                                                                                          \
-    }                                                                                            \
-    if (GUARD) wait_for(4 * t_ + 3, 4 * t_ + 7); else wait_vm<8>(); /* A1(t) for Q2 */           \
-    /* Q2 (A0, B1): read A1(t) */                                                                \
-    qp_barrier();                                                                                \
-    QP2_ISSUE(4 * t_ + 8, GUARD);                                                                \
-    qp2_mma<BF16>(acc1, fa0, s1);                                                                \
-    read_a(fa1, buf + p_half_off(P_A1));                                                         \
-    if (!(GUARD)) {                                                                              \
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
-      _Pragma("unroll") for (int i_ = 0; i_ < 5; ++i_) {                                         \
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                       \
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
-      }                                                                                          \
-    } else {                                                                                     \
-      _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                         \
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                       \
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
-      }                                                                                          \
-    }                                                                                            \
-    /* Q3 (A1, B1): no reads */                                                                  \
-    qp_barrier();                                                                                \
-    QP2_ISSUE(4 * t_ + 9, GUARD);                                                                \
-    qp2_mma<BF16>(acc2, fa1, s1);                                                                \
-    if (!(GUARD)) {                                                                              \
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x008, 10, 0);                                        \
-    }                                                                                            \
-    if (GUARD) wait_for(4 * t_ + 5, 4 * t_ + 9); else wait_vm<8>(); /* A0(t+1), B0(t+1) for Q4 */\
-    /* Q4 (A1, B0): read A0(t+1), B0(t+1) */                                                     \
-    qp_barrier();                                                                                \
-    QP2_ISSUE(4 * t_ + 10, GUARD);                                                               \
-    qp2_mma<BF16>(acc3, fa1, s0);                                                                \
-    if (!(GUARD) || t_ + 1 < ktiles) {                                                           \
-      read_a(fa0, nbuf + p_half_off(P_A0));                                                      \
-      read_b(s1, nbuf + p_half_off(P_B0));                                                       \
-    }                                                                                            \
-    if (!(GUARD)) {                                                                              \
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
-      _Pragma("unroll") for (int i_ = 0; i_ < 3; ++i_) {                                         \
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                       \
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
-      }                                                                                          \
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                         \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
-      _Pragma("unroll") for (int i_ = 0; i_ < 7; ++i_) {                                         \
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                       \
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
-      }                                                                                          \
-    } else {                                                                                     \
-      _Pragma("unroll") for (int i_ = 0; i_ < 12; ++i_) {                                        \
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                       \
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                       \
-      }                                                                                          \
-    }                                                                                            \
-    if (GUARD) wait_for(4 * t_ + 6, 4 * t_ + 10); else wait_vm<8>(); /* B1(t+1) for Q1(t+1) */   \
+  // One K-tile of four phases: P = buffer of this K-tile (compile time); (RC1, RQ1, K1): the tile
+  // and local index of K-tile t+1 (its A1 is issued in Q1), (RC2, RQ2, K2): of K-tile t+2.
+  // The LDS-DMA pieces live in the same basic block as the MFMAs and are spread between them by
+  // the sched_group_barrier patterns (masks: 0x008 MFMA, 0x100 DS read, 0x020 VMEM read).
+#define QP2_KTILE(P, s0, s1, RC1, RQ1, K1, RC2, RQ2, K2, READ_NEXT)                             \
+  {                                                                                             \
+    /* Q1 (A0, B0): read B1(t) */                                                               \
+    qp_barrier();                                                                               \
+    issue_h(RC1, RQ1, K1, P_A1, 1 - (P));                                                       \
+    qp2_mma<BF16>(acc0, fa0, s0);                                                               \
+    read_b(s1, (P), P_B1);                                                                      \
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                          \
+    _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                          \
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                        \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                        \
+    }                                                                                           \
+    wait_vm<8>(); /* A1(t) for Q2 */                                                            \
+    /* Q2 (A0, B1): read A1(t) */                                                               \
+    qp_barrier();                                                                               \
+    issue_h(RC2, RQ2, K2, P_A0, (P));                                                           \
+    qp2_mma<BF16>(acc1, fa0, s1);                                                               \
+    read_a(fa1, (P), P_A1);                                                                     \
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                          \
+    _Pragma("unroll") for (int i_ = 0; i_ < 5; ++i_) {                                          \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                        \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                        \
+    }                                                                                           \
+    /* Q3 (A1, B1): no reads */                                                                 \
+    qp_barrier();                                                                               \
+    issue_h(RC2, RQ2, K2, P_B0, (P));                                                           \
+    qp2_mma<BF16>(acc2, fa1, s1);                                                               \
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                          \
+    __builtin_amdgcn_sched_group_barrier(0x008, 10, 0);                                         \
+    wait_vm<8>(); /* A0(t+1), B0(t+1) for Q4 */                                                 \
+    /* Q4 (A1, B0): read A0(t+1), B0(t+1) */                                                    \
+    qp_barrier();                                                                               \
+    issue_h(RC2, RQ2, K2, P_B1, (P));                                                           \
+    qp2_mma<BF16>(acc3, fa1, s0);                                                               \
+    if (READ_NEXT) {                                                                            \
+      read_a(fa0, 1 - (P), P_A0);                                                               \
+      read_b(s1, 1 - (P), P_B0);                                                                \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                        \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                        \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                        \
+      _Pragma("unroll") for (int i_ = 0; i_ < 3; ++i_) {                                        \
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                      \
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                      \
+      }                                                                                         \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                        \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                        \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                        \
+      _Pragma("unroll") for (int i_ = 0; i_ < 7; ++i_) {                                        \
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                      \
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                      \
+      }                                                                                         \
+    } else {                                                                                    \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                                        \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                        \
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                        \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                        \
+      __builtin_amdgcn_sched_group_barrier(0x008, 10, 0);                                       \
+    }                                                                                           \
+    wait_vm<8>(); /* B1(t+1) for Q1(t+1) */                                                     \
   }
 
-  int t = 0;
-  // steady state: the last half-tile issued by the pair (t, t+1) is 4 (t+1) + 10 < 4 ktiles
-  for (; t + 4 < ktiles; t += 2) {
-    QP2_TILE(t, fbx, fby, false);
-    QP2_TILE(t + 1, fby, fbx, false);
-  }
-  for (; t + 1 < ktiles; t += 2) {
-    QP2_TILE(t, fbx, fby, true);
-    QP2_TILE(t + 1, fby, fbx, true);
-  }
-  if (t < ktiles) QP2_TILE(t, fbx, fby, true);
-#undef QP2_TILE
-#undef QP2_ISSUE
-
-  // ---- epilogue: quadrant (ah, bh) = catalog half ah x query half bh ----
-  const bool full = c0 + QP_TILE <= n_rows;  // uniform
+  for (;;) {
+    const bool last = !(L + n_x < Lend);  // uniform
+    // A0(0) / B0(0) of this tile landed before the last barrier (the prologue's, or the
+    // previous tile's last phase)
+    set_geom();
+    read_a(fa0, 0, P_A0);
+    read_b(fbx, 0, P_B0);
+    {
+      const QpTile T = tile_at(L);
+      const __amdgpu_buffer_rsrc_t rc = rsrc_c(T), rq = rsrc_q(T);
+      // K-tiles 0 .. kt-3 of the tile (pairs), then the boundary pair that stages the next tile
+      for (int t = 0; t < kt - 2; t += 2) {
+        QP2_KTILE(0, fbx, fby, rc, rq, t + 1, rc, rq, t + 2, true);
+        QP2_KTILE(1, fby, fbx, rc, rq, t + 2, rc, rq, t + 3, true);
+      }
+      const QpTile N = tile_at(last ? L : L + n_x);
+      const __amdgpu_buffer_rsrc_t nc = rsrc_c(N), nq = rsrc_q(N);
+      QP2_KTILE(0, fbx, fby, rc, rq, kt - 1, nc, nq, 0, true);
+      QP2_KTILE(1, fby, fbx, nc, nq, 0, nc, nq, 1, false);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // the epilogue's lane geometry is recomputed from an opaque copy of the lane id, so that
+    // none of it is hoisted into registers held through the K-loop
+    int lane_e = tid;
+    asm volatile("" : "+v"(lane_e));
+    const QpTile cur = tile_at(L);
+    const QpArgsK A = qp_args();
+    const int64_t n_rows = A->n_rows;
+    const int tid_ = lane_e, lane_ = tid_ & 63, fr_ = lane_ & 15;
+  // ---- epilogue helpers (quadrant (ah, bh) = catalog half ah x query half bh) ----
+  // acc0 (0, 0), acc1 (0, 1), acc2 (1, 1), acc3 (1, 0)
+  auto acc_of = [&](int ah, int bh) -> const f32x4_t (&)[4][2] {
+    return ah == 0 ? (bh == 0 ? acc0 : acc1) : (bh == 0 ? acc3 : acc2);
+  };
   // Filter mode. Each lane holds 4 query columns (bh, j) x 32 catalog rows (2 halves x 4
   // accumulators x 4 rows); a block is one accumulator (4 consecutive rows of one query).
   //   1. column test (every tile): the max of each column's 32 values against the query's
@@ -634,48 +751,25 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
   //      scale is applied once per column; NaNs drop out of fmaxf as they do out of >=.
   //   2. only if some lane of the wave passed: block bits m (bit c*8 + ah*4 + i) for the flagged
   //      columns.
-  //   3. the lane's flagged blocks go to its 8 LDS slots in the dead K-tile ring (rounds of 8
-  //      when a lane has more; only the wave's flagged columns are visited), and a ROLLED loop over the lane's own blocks computes the exact
-  //      values, claims slots with one LDS atomic per block and writes the hits: the work
-  //      follows the lane's hits, not the union of the wave's blocks (the earlier form executed
-  //      every block any lane had flagged: ~600 VALU per wave with 2 hits, ~1500 with 60).
-  // Every wave passed the last tile's final barrier after its last LDS read of the ring.
-  auto filter_tile = [&](auto simple_tag) {
+  //   3. the lane's flagged blocks go to its QP_STG_SLOTS LDS slots (rounds when a lane has
+  //      more; only the wave's flagged columns are visited), and a ROLLED loop over the lane's
+  //      own blocks computes the exact values, claims slots with one LDS atomic per block and
+  //      writes the hits: the work follows the lane's hits, not the union of the wave's blocks.
+  auto filter_tile = [&](const QpTile& T, auto simple_tag) {
     constexpr bool SIMPLE = decltype(simple_tag)::value;
+    const bool full = T.c0 + QP_TILE <= n_rows;  // uniform
     float qs_r[2][2], th_r[2][2];
+    {
+      const int ql[4] = {wb * 32 + fr_, wb * 32 + 16 + fr_, 128 + wb * 32 + fr_,
+                         128 + wb * 32 + 16 + fr_};
+      float q4[4], t4[4];
+      lds_qs_th4(lqs, lth, ql, q4, t4);
 #pragma unroll
-    for (int bh = 0; bh < 2; ++bh)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int ql = bh * 128 + wb * 32 + j * 16 + fr;
-        qs_r[bh][j] = lqs[ql];
-        th_r[bh][j] = lth[ql];
+      for (int c = 0; c < 4; ++c) {
+        qs_r[c >> 1][c & 1] = q4[c];
+        th_r[c >> 1][c & 1] = t4[c];
       }
-    // quadrant q = (ah, bh): acc0 (0, 0), acc1 (0, 1), acc2 (1, 1), acc3 (1, 0)
-    auto acc_of = [&](int ah, int bh) -> const f32x4_t (&)[4][2] {
-      return ah == 0 ? (bh == 0 ? acc0 : acc1) : (bh == 0 ? acc3 : acc2);
-    };
-    // row scales, register-resident (read from LDS once; 1 without scales)
-    float4 cs_r[2][4];
-    if constexpr (!SIMPLE) {
-#pragma unroll
-      for (int ah = 0; ah < 2; ++ah)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          cs_r[ah][i] = *(const float4*)(lcs + ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4));
     }
-    // the exact epilogue values of block (ah, bh, i, j). Rows past n_rows are NOT masked here
-    // (they read 0 through the buffer descriptor): the block bits are a superset, the exact
-    // per-row test in the hit loop drops them.
-    auto val4 = [&](int ah, int bh, int i, int j, float (&v)[4]) {
-      const f32x4_t& a = acc_of(ah, bh)[i][j];
-      const float qs = qs_r[bh][j];
-      const float4 cs = cs_r[ah][i];
-      v[0] = a[0] * qs * cs.x;
-      v[1] = a[1] * qs * cs.y;
-      v[2] = a[2] * qs * cs.z;
-      v[3] = a[3] * qs * cs.w;
-    };
     auto max4 = [](float a, float b, float c, float d) { return fmaxf(fmaxf(a, b), fmaxf(c, d)); };
     uint32_t m = 0;
     if constexpr (SIMPLE) {
@@ -683,48 +777,52 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
 #pragma unroll
       for (int bh = 0; bh < 2; ++bh)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int jj = 0; jj < 2; ++jj) {
           float mx = -__builtin_inff();
 #pragma unroll
           for (int ah = 0; ah < 2; ++ah)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const f32x4_t& a = acc_of(ah, bh)[i][j];
+              const f32x4_t& a = acc_of(ah, bh)[i][jj];
               mx = fmaxf(mx, max4(a[0], a[1], a[2], a[3]));
             }
-          colm |= (mx * qs_r[bh][j] >= th_r[bh][j] ? 1u : 0u) << (bh * 2 + j);
+          colm |= (mx * qs_r[bh][jj] >= th_r[bh][jj] ? 1u : 0u) << (bh * 2 + jj);
         }
       if (__builtin_expect(__ballot(colm != 0u) == 0ull, 1)) return;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const int bh = c >> 1, j = c & 1;
+        const int bh = c >> 1, jj = c & 1;
         if (__ballot((colm >> c) & 1u) == 0ull) continue;
 #pragma unroll
         for (int ah = 0; ah < 2; ++ah)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const f32x4_t& a = acc_of(ah, bh)[i][j];
-            const float mx = max4(a[0], a[1], a[2], a[3]) * qs_r[bh][j];
-            m |= (mx >= th_r[bh][j] ? 1u : 0u) << (c * 8 + ah * 4 + i);
+            const f32x4_t& a = acc_of(ah, bh)[i][jj];
+            const float mx = max4(a[0], a[1], a[2], a[3]) * qs_r[bh][jj];
+            m |= (mx >= th_r[bh][jj] ? 1u : 0u) << (c * 8 + ah * 4 + i);
           }
       }
     } else {
       // row scales or a partial tile: the block bits directly (each block's values are used
-      // at once; a column pass first would keep all 128 values live and spill)
+      // at once; a column pass first would keep all 128 values live and spill). Rows past
+      // n_rows are NOT masked here (they read 0): the block bits are a superset, the exact
+      // per-row test in the hit loop drops them.
 #pragma unroll
       for (int c = 0; c < 4; ++c)
 #pragma unroll
         for (int ah = 0; ah < 2; ++ah)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            float v[4];
-            val4(ah, c >> 1, i, c & 1, v);
-            m |= (max4(v[0], v[1], v[2], v[3]) >= th_r[c >> 1][c & 1] ? 1u : 0u)
-                 << (c * 8 + ah * 4 + i);
+            const f32x4_t& a = acc_of(ah, c >> 1)[i][c & 1];
+            const float qs = qs_r[c >> 1][c & 1];
+            const float4 cs = lds_float4(lcs + ah * 128 + wa * 64 + i * 16 + 4 * (lane_ >> 4));
+            const float mx = max4(a[0] * qs * cs.x, a[1] * qs * cs.y, a[2] * qs * cs.z,
+                                  a[3] * qs * cs.w);
+            m |= (mx >= th_r[c >> 1][c & 1] ? 1u : 0u) << (c * 8 + ah * 4 + i);
           }
       if (__builtin_expect(__ballot(m != 0u) == 0ull, 1)) return;
     }
-    char* stg = smem + wave * 8192 + lane * 128;  // this lane's 8 slots of 16 B
+    char* stg = smem + QP_LDS + QP_PARAM + tid_ * (QP_STG_SLOTS * 16);  // this lane's slots
     // columns with a flagged block in some lane of the wave (uniform): only their 8 blocks are
     // visited when staging
     uint32_t cols = 0;
@@ -744,97 +842,132 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
           for (int i = 0; i < 4; ++i) {
             const int g = c * 8 + ah * 4 + i;
             const int rank = __popc(m & ((1u << g) - 1u));
-            if (((m >> g) & 1u) && (rank >> 3) == round)
-              *(f32x4_t*)(stg + (rank & 7) * 16) = acc_of(ah, c >> 1)[i][c & 1];
+            if (((m >> g) & 1u) && rank / QP_STG_SLOTS == round)
+              *(f32x4_t*)(stg + (rank % QP_STG_SLOTS) * 16) = acc_of(ah, c >> 1)[i][c & 1];
           }
       }
 #pragma unroll 1
-      for (int s2 = 0; s2 < 8; ++s2) {
+      for (int s2 = 0; s2 < QP_STG_SLOTS; ++s2) {
         if (__ballot(rest != 0u) == 0ull) break;
-        if (rest != 0u && (nblk - __popc(rest)) >> 3 == round) {
+        if (rest != 0u && (nblk - __popc(rest)) / QP_STG_SLOTS == round) {
           const int g = __builtin_ctz(rest);
           rest &= rest - 1u;
-          const f32x4_t a = *(const f32x4_t*)(stg + s2 * 16);
           const int c = g >> 3, ah = (g >> 2) & 1, i = g & 3;
-          const int ql = (c >> 1) * 128 + wb * 32 + (c & 1) * 16 + fr;
-          const int il = ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
-          const float qs = lqs[ql], th = lth[ql];
-          const float4 cs = *(const float4*)(lcs + il);
+          const int ql = (c >> 1) * 128 + wb * 32 + (c & 1) * 16 + fr_;
+          const int il = ah * 128 + wa * 64 + i * 16 + 4 * (lane_ >> 4);
+          f32x4_t a, csv;
+          float qs, th;
+          lds_hit_block(stg + s2 * 16, lqs + ql, lth + ql, lcs + il, a, qs, th, csv);
+          const float4 cs = make_float4(csv[0], csv[1], csv[2], csv[3]);
           const float v[4] = {a[0] * qs * cs.x, a[1] * qs * cs.y, a[2] * qs * cs.z,
                               a[3] * qs * cs.w};
           uint32_t hb = 0;
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            hb |= (v[r] >= th && (full || c0 + il + r < n_rows) ? 1u : 0u) << r;
+            hb |= (v[r] >= th && (full || T.c0 + il + r < n_rows) ? 1u : 0u) << r;
           if (hb) {
-            const uint32_t base = atomicAdd(lcnt + ql, (uint32_t)__popc(hb));
-            uint64_t* dst = e.cand + (q0 + ql) * e.ld_cand + ct * e.slots;
+            const uint32_t base = lds_add_rtn(lcnt + ql, (uint32_t)__popc(hb));
+            uint64_t* dst = A->e.cand + (T.q0 + ql) * A->e.ld_cand + T.ct * A->e.slots;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const uint32_t p = base + (uint32_t)__popc(hb & ((1u << r) - 1u));
-              if (((hb >> r) & 1u) && p < (uint32_t)e.slots) {
-                const uint32_t row = (uint32_t)(e.idx_base + c0 + il + r);
+              if (((hb >> r) & 1u) && p < (uint32_t)A->e.slots) {
+                const uint32_t row = (uint32_t)(A->e.idx_base + T.c0 + il + r);
                 dst[p] = ((uint64_t)f2key(v[r]) << 32) | (uint64_t)(~row);
               }
             }
           }
         }
       }
-      if (__ballot(nblk > 8 * (round + 1)) == 0ull) break;
+      if (__ballot(nblk > QP_STG_SLOTS * (round + 1)) == 0ull) break;
     }
   };
-  auto store_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh) {
+  auto store_quadrant = [&](const QpTile& T, const f32x4_t (&acc)[4][2], int ah, int bh) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int ql = bh * 128 + wb * 32 + j * 16 + fr;
-      const float qs = lqs[ql];
-      const float th = FILTER ? lth[ql] : 0.f;
+    for (int jj = 0; jj < 2; ++jj) {
+      const int ql = bh * 128 + wb * 32 + jj * 16 + fr_;
+      const float qs = lds_f32(lqs + ql);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int il = ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
-        const float4 cs = *(const float4*)(lcs + il);
-        epilogue4v<FILTER>(e, q0 + ql, c0 + il, n_rows, acc[i][j], qs, th, cs, lcnt + ql, ct);
+        const int il = ah * 128 + wa * 64 + i * 16 + 4 * (lane_ >> 4);
+        const float4 cs = lds_float4(lcs + il);
+        const f32x4_t& a = acc[i][jj];
+        const float v[4] = {a[0] * qs * cs.x, a[1] * qs * cs.y, a[2] * qs * cs.z, a[3] * qs * cs.w};
+        float* srow = A->e.S + (T.q0 + ql) * A->e.ld_s;
+        const int64_t i0 = T.c0 + il;
+        if (i0 + 3 < n_rows) {
+          *(float4*)(srow + i0) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (i0 + r < n_rows) srow[i0 + r] = v[r];
+        }
       }
     }
   };
   // pool mode: max over the 64 rows (ah, wa) of each query: 4 accumulators x 4 values in the
-  // lane, then the 4 lanes of the same fr (lane ^ 16, ^ 32); rows past n_rows are skipped
-  auto pool_quadrant = [&](const f32x4_t (&acc)[4][2], int ah, int bh) {
+  // lane, then the 4 lanes of the same fr_ (lane ^ 16, ^ 32); rows past n_rows are skipped
+  auto pool_quadrant = [&](const QpTile& T, const f32x4_t (&acc)[4][2], int ah, int bh) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int ql = bh * 128 + wb * 32 + j * 16 + fr;
-      const float qs = lqs[ql];
+    for (int jj = 0; jj < 2; ++jj) {
+      const int ql = bh * 128 + wb * 32 + jj * 16 + fr_;
+      const float qs = lds_f32(lqs + ql);
       float mx = -__builtin_inff();
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int il = ah * 128 + wa * 64 + i * 16 + 4 * (lane >> 4);
-        const float4 cs = *(const float4*)(lcs + il);
-        const f32x4_t& a = acc[i][j];
+        const int il = ah * 128 + wa * 64 + i * 16 + 4 * (lane_ >> 4);
+        const float4 cs = lds_float4(lcs + il);
+        const f32x4_t& a = acc[i][jj];
         const float v[4] = {a[0] * qs * cs.x, a[1] * qs * cs.y, a[2] * qs * cs.z, a[3] * qs * cs.w};
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (c0 + il + r < n_rows) mx = fmaxf(mx, v[r]);
+          if (T.c0 + il + r < n_rows) mx = fmaxf(mx, v[r]);
       }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      if ((lane >> 4) == 0) e.S[(q0 + ql) * e.ld_s + ct * 4 + ah * 2 + wa] = mx;
+      if ((lane_ >> 4) == 0) A->e.S[(T.q0 + ql) * A->e.ld_s + T.ct * 4 + ah * 2 + wa] = mx;
     }
   };
-  if constexpr (EPI == EPI_POOL) {
-    pool_quadrant(acc0, 0, 0);
-    pool_quadrant(acc1, 0, 1);
-    pool_quadrant(acc2, 1, 1);
-    pool_quadrant(acc3, 1, 0);
-  } else if constexpr (FILTER) {
-    if (!cscale && full) filter_tile(std::true_type{});
-    else filter_tile(std::false_type{});
-  } else {
-    store_quadrant(acc0, 0, 0);
-    store_quadrant(acc1, 0, 1);
-    store_quadrant(acc2, 1, 1);
-    store_quadrant(acc3, 1, 0);
+
+
+    // ---- epilogue of `cur` (every wave passed the last phase's barrier after its last LDS
+    // read of the tile's parameters' previous contents; the parameters landed: counted waits)
+    if constexpr (EPI == EPI_POOL) {
+      pool_quadrant(cur, acc0, 0, 0);
+      pool_quadrant(cur, acc1, 0, 1);
+      pool_quadrant(cur, acc2, 1, 1);
+      pool_quadrant(cur, acc3, 1, 0);
+    } else if constexpr (FILTER) {
+      if (!A->cscale && cur.c0 + QP_TILE <= n_rows) filter_tile(cur, std::true_type{});
+      else filter_tile(cur, std::false_type{});
+    } else {
+      store_quadrant(cur, acc0, 0, 0);
+      store_quadrant(cur, acc1, 0, 1);
+      store_quadrant(cur, acc2, 1, 1);
+      store_quadrant(cur, acc3, 1, 0);
+    }
+    // every wave is past its reads of lcnt / lqs / lth / lcs (LDS-only barrier: the hit and
+    // score stores need not drain here)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if constexpr (FILTER) {
+      if (tid_ < QP_TILE) {
+        const uint32_t c = lcnt[tid_];
+        const int64_t q = cur.q0 + tid_;
+        A->e.counts[q * A->e.ld_counts + cur.ct] = (uint8_t)(c < 255u ? c : 255u);
+        if (c > (uint32_t)A->e.slots) A->e.ovf[q] = 1;
+        lcnt[tid_] = 0u;
+      }
+    }
+    if (last) break;
+    L += n_x;
+    issue_params(tile_at(L));
+    zero_acc();
   }
-  if constexpr (FILTER) filter_finish(e, lcnt, q0, QP_TILE, ct);
+#undef QP2_KTILE
+  // the last tile restaged its own first K-tiles: drain before the LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 
@@ -843,6 +976,21 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(
 // MI355X ("screening GEMM"): a 4-slot ring with k32 slices, one barrier per phase
 // with two barriers (qp), a persistent one-workgroup-per-CU walk of the same tiles, and a
 // 4-wave 128 x 128-per-wave tile (LDS-DMA issue cost with one wave per SIMD).
+// Compute units of the current device (the persistent grid size), cached per device.
+static int64_t n_cus() {
+  static int64_t cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cache[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    cache[dev] = cus;
+  }
+  return cache[dev];
+}
+
 template <int EPI>
 static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
                        int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
@@ -860,13 +1008,29 @@ static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_
   const uint16_t* Q = (const uint16_t*)qimg;
   const uint16_t* C = (const uint16_t*)cimg;
   if (big) {
-    dim3 grid((unsigned)nwg), block(QP_THREADS);
-    auto k = img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, EPI>
-                                   : screen_gemm_qp2_kernel<false, EPI>;
-    const int lds = QP_LDS + 1024 + 3 * QP_TILE * 4;
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(k, grid, block, lds, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
-                       n_ctiles, d_pad / 64, qscale, cscale, e, cstride);
+    // persistent: one 148 KiB-LDS workgroup per CU walks ceil(tiles / CUs) tiles
+    const int64_t G = nwg < n_cus() ? nwg : n_cus();
+    const int ktiles = d_pad / 64;
+    dim3 grid((unsigned)G), block(QP_THREADS);
+    auto k = (ktiles & 1) ? (img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, EPI, true>
+                                                   : screen_gemm_qp2_kernel<false, EPI, true>)
+                          : (img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, EPI, false>
+                                                   : screen_gemm_qp2_kernel<false, EPI, false>);
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              QP_LDS_TOTAL);
+    QpArgs a{};
+    a.Q = Q;
+    a.C = C;
+    a.ld_img = ld_img;
+    a.n_rows = n_rows;
+    a.qscale = qscale;
+    a.cscale = cscale;
+    a.cstride = cstride;
+    a.n_qtiles = n_qtiles;
+    a.n_ctiles = (int)n_ctiles;
+    a.ktiles = ktiles;
+    a.e = e;
+    hipLaunchKernelGGL(k, grid, block, QP_LDS_TOTAL, stream, a);
     return launch_check("screen_gemm_qp2_kernel");
   }
   if (cstride != GBM || EPI == EPI_POOL) {

@@ -24,6 +24,9 @@ def load(name):
     f = lib.ebt_screen_filter
     f.argtypes = [VP, I64, VP, I64, I32, I32, INT, VP, VP, VP, VP, I64, I32, VP, I64, VP, I64, VP]
     f.restype = INT
+    g = lib.ebt_screen_scores
+    g.argtypes = [VP, I64, VP, I64, I32, I32, INT, VP, VP, VP, I64, VP]
+    g.restype = INT
     lib.ebt_last_error.restype = ctypes.c_char_p
     return lib
 
@@ -71,6 +74,24 @@ def main():
         torch.cuda.synchronize()
         return s.elapsed_time(e) / a.iters
 
+    # store mode on a ragged catalog with row scales: bitwise equal across variants
+    ns = 65536 + 77
+    cs_ = torch.rand(((ns + 255) // 256) * 256, device=dev) + 0.5
+    qs_ = torch.rand(B, device=dev) + 0.5
+    store_ref, store_eq = None, {}
+    for n in a.names:
+        S = torch.full((B, ns + 3), float("nan"), device=dev)
+        rc = libs[n].ebt_screen_scores(P(q), B, P(c), ns, d, d, 2, P(qs_), P(cs_), P(S), ns + 3, st)
+        if rc:
+            raise RuntimeError(libs[n].ebt_last_error().decode())
+        torch.cuda.synchronize()
+        S = S[:, :ns]
+        if store_ref is None:
+            store_ref = S.clone()
+            ref32 = (q.float() @ c[:ns].float().T) * qs_[:, None] * cs_[None, :ns]
+            store_eq["_vs_fp32_maxrel"] = float(((S - ref32).abs().max() / ref32.abs().max()))
+        store_eq[n] = bool(torch.equal(S, store_ref))
+    print(json.dumps({"store_bitwise_equal": store_eq}), flush=True)
     res = {n: {"hits": [], "nohit": []} for n in a.names}
     hits_per_q = None
     ref = None

@@ -48,12 +48,59 @@ def grp(n):
     return f
 
 
-VARIANTS = {"grp2": grp(2), "grp8": grp(8), "grp16": grp(16),"base": lambda s: s, "nosleep": nosleep, "prio_static": prio_static,
+def l2only(src):
+    # diagnostic: every workgroup reads one of 4 catalog tiles (all catalog fetches hit L2)
+    return _sub(src, "const int64_t ct = g * QP_GROUP_C + w % gc;",
+                "const int64_t ct = (g * QP_GROUP_C + w % gc) & 3;", 1)
+
+
+def nobar(src):
+    # diagnostic (wrong results): no s_barrier between phases
+    return _sub(src, "  asm volatile(\"\" ::: \"memory\");\n  __builtin_amdgcn_s_barrier();\n"
+                "  asm volatile(\"\" ::: \"memory\");\n  __builtin_amdgcn_sched_barrier(0);",
+                "  asm volatile(\"\" ::: \"memory\");\n"
+                "  asm volatile(\"\" ::: \"memory\");\n  __builtin_amdgcn_sched_barrier(0);", 1)
+
+
+def nowait(src):
+    # diagnostic (wrong results): steady-state vmcnt waits dropped
+    return _sub(src, "else if constexpr (N == 8) asm volatile(\"s_waitcnt vmcnt(8)\" ::: \"memory\");",
+                "else if constexpr (N == 8) asm volatile(\"\" ::: \"memory\");", 1)
+
+
+def noepi(src):
+    # diagnostic: filter epilogue skipped (counts still published)
+    return _sub(src, "    if (!cscale && full) filter_tile(std::true_type{});\n"
+                "    else filter_tile(std::false_type{});\n", "", 1)
+
+
+def noepi_nofin(src):
+    src = noepi(src)
+    return _sub(src, "  if constexpr (FILTER) filter_finish(e, lcnt, q0, QP_TILE, ct);\n}\n", "}\n", 1)
+
+
+def trivepi(src):
+    # diagnostic (wrong results) for the persistent kernel: the epilogue is one sum per lane
+    a = src.index("    if constexpr (EPI == EPI_POOL) {\n      pool_quadrant(cur, acc0")
+    b = src.index("    // every wave is past its reads of lcnt")
+    return src[:a] + """    { float sm = 0.f;
+      for (int i = 0; i < 4; ++i) for (int jj = 0; jj < 2; ++jj) for (int r = 0; r < 4; ++r)
+        sm += acc0[i][jj][r] + acc1[i][jj][r] + acc2[i][jj][r] + acc3[i][jj][r];
+      if (sm == 1234.5f) e.ovf[0] = 1; }
+""" + src[b:]
+
+
+VARIANTS = {"trivepi": trivepi, "noepi": noepi, "noepi_nofin": noepi_nofin, "l2only": l2only, "nobar": nobar, "nowait": nowait, "grp2": grp(2), "grp8": grp(8), "grp16": grp(16),"base": lambda s: s, "nosleep": nosleep, "prio_static": prio_static,
             "prio_static_sleep": prio_static_sleep}
 
 
 def build(name):
-    src = open(os.path.join(CSRC, "screen_gemm.hip")).read()
+    ref = os.environ.get("GEMM_LAB_REF")  # e.g. HEAD: patch the committed source instead
+    if ref:
+        src = subprocess.run(["git", "-C", ROOT, "show", f"{ref}:robot_ebert_amd/csrc/screen_gemm.hip"],
+                             check=True, capture_output=True, text=True).stdout
+    else:
+        src = open(os.path.join(CSRC, "screen_gemm.hip")).read()
     src = VARIANTS[name](src)
     base = os.path.join("/tmp", "gemm_lab", name)
     work = os.path.join(base, "x", "csrc")   # common.h includes ../../include/ebert.h
