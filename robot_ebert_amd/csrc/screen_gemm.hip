@@ -355,7 +355,8 @@ __device__ __forceinline__ void qp2_mma(f32x4_t (&acc)[4][2], const u16x8_t (&a)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = mfma16<BF16>(a[i][ks], b[j][ks], acc[i][j]);
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = mfma16<BF16>(a[i][ks], b[j][ks], acc[i][j]);
 }
 
 // Epilogue modes of the quadrant-phase kernel: EPI_STORE (score rows), EPI_FILTER (the fused
@@ -364,11 +365,13 @@ __device__ __forceinline__ void qp2_mma(f32x4_t (&acc)[4][2], const u16x8_t (&a)
 enum { EPI_STORE = 0, EPI_FILTER = 1, EPI_POOL = 2 };
 
 // LDS after the 128 KiB ring: hit counters (1 KiB), the tile's query scales / thresholds / row
-// scales (3 KiB, LDS-DMA'd per tile), the filter epilogue's hit staging (QP_STG_SLOTS 16-byte
-// slots per lane).
+// scales (3 KiB, LDS-DMA'd per tile), the filter epilogue's hit staging: per wave QP_STG_COLS
+// flagged (lane, query column) pairs per round, each its 32 raw accumulators (128 B) and a
+// 16-byte record {local query | row group << 8, query scale, threshold, -}.
 constexpr int QP_PARAM = 1024 + 3 * QP_TILE * 4;
-constexpr int QP_STG_SLOTS = 2;
-constexpr int QP_STG = QP_THREADS * QP_STG_SLOTS * 16;
+constexpr int QP_STG_COLS = 16;
+constexpr int QP_STG_WAVE = QP_STG_COLS * (128 + 16);
+constexpr int QP_STG = 8 * QP_STG_WAVE;
 constexpr int QP_LDS_TOTAL = QP_LDS + QP_PARAM + QP_STG;
 static_assert(QP_LDS_TOTAL <= 160 * 1024, "LDS budget");
 
@@ -403,17 +406,52 @@ __device__ __forceinline__ void lds_qs_th4(const float* qs, const float* th, con
         "v"((uint32_t)(uintptr_t)(th + ql[2])), "v"((uint32_t)(uintptr_t)(th + ql[3]))
       : "memory");
 }
-// A staged hit block with its query's scale / threshold and the rows' scales (one wait).
-__device__ __forceinline__ void lds_hit_block(const void* stg, const float* qs, const float* th,
-                                              const float* cs, f32x4_t& a, float& q, float& t,
-                                              f32x4_t& c) {
+// The 8 row-scale vectors of a lane (rows base + ah * 128 + i * 16 .. + 3: byte offsets
+// ah * 512 + i * 64 from one address, one wait).
+__device__ __forceinline__ void lds_rowscales8(const float* p, f32x4_t (&c)[2][4]) {
   asm volatile(
-      "ds_read_b128 %0, %4\n\tds_read_b32 %1, %5\n\tds_read_b32 %2, %6\n\tds_read_b128 %3, %7\n\t"
+      "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:64\n\t"
+      "ds_read_b128 %2, %8 offset:128\n\tds_read_b128 %3, %8 offset:192\n\t"
+      "ds_read_b128 %4, %8 offset:512\n\tds_read_b128 %5, %8 offset:576\n\t"
+      "ds_read_b128 %6, %8 offset:640\n\tds_read_b128 %7, %8 offset:704\n\t"
       "s_waitcnt lgkmcnt(0)"
-      : "=&v"(a), "=&v"(q), "=&v"(t), "=&v"(c)
-      : "v"((uint32_t)(uintptr_t)stg), "v"((uint32_t)(uintptr_t)qs), "v"((uint32_t)(uintptr_t)th),
-        "v"((uint32_t)(uintptr_t)cs)
+      : "=&v"(c[0][0]), "=&v"(c[0][1]), "=&v"(c[0][2]), "=&v"(c[0][3]), "=&v"(c[1][0]),
+        "=&v"(c[1][1]), "=&v"(c[1][2]), "=&v"(c[1][3])
+      : "v"((uint32_t)(uintptr_t)p)
       : "memory");
+}
+// Staging writes (in asm: a plain LDS store would get the same vmcnt(0) as a plain read).
+__device__ __forceinline__ void lds_put_col(uint32_t dst, const f32x4_t& a0, const f32x4_t& a1,
+                                            const f32x4_t& a2, const f32x4_t& a3,
+                                            const f32x4_t& a4, const f32x4_t& a5,
+                                            const f32x4_t& a6, const f32x4_t& a7,
+                                            uint32_t meta_dst, const f32x4_t& meta) {
+  asm volatile(
+      "ds_write_b128 %0, %2\n\tds_write_b128 %0, %3 offset:16\n\t"
+      "ds_write_b128 %0, %4 offset:32\n\tds_write_b128 %0, %5 offset:48\n\t"
+      "ds_write_b128 %0, %6 offset:64\n\tds_write_b128 %0, %7 offset:80\n\t"
+      "ds_write_b128 %0, %8 offset:96\n\tds_write_b128 %0, %9 offset:112\n\t"
+      "ds_write_b128 %1, %10"
+      :
+      : "v"(dst), "v"(meta_dst), "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5), "v"(a6),
+        "v"(a7), "v"(meta)
+      : "memory");
+}
+// A staged column's record and 8 of its values (one wait).
+__device__ __forceinline__ void lds_staged(uint32_t meta, uint32_t vals, f32x4_t& m, f32x4_t& v0,
+                                          f32x4_t& v1) {
+  asm volatile(
+      "ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %4 offset:16\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(m), "=&v"(v0), "=&v"(v1)
+      : "v"(meta), "v"(vals)
+      : "memory");
+}
+__device__ __forceinline__ void lds_f32x4x2(const void* p, f32x4_t& c0, f32x4_t& c1) {
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:64\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(c0), "=&v"(c1)
+               : "v"((uint32_t)(uintptr_t)p)
+               : "memory");
 }
 __device__ __forceinline__ uint32_t lds_add_rtn(uint32_t* p, uint32_t v) {
   uint32_t r;
@@ -516,19 +554,24 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
   // travel in the operand stream and are retired by its counted waits
   auto issue_params = [&](const QpTile& T) {
     const QpArgsK A = qp_args();
+    // the lane offset from an opaque lane id: hoisted out of the tile loop, it would be spilled
+    // at the K-loop's register peak and reloaded with a vmcnt(0) that drains the operand stream
+    int lo = tid;
+    asm volatile("" : "+v"(lo));
+    lo = (lo & 63) * 16;
     if (wave == 0) {
       const __amdgpu_buffer_rsrc_t rs =
           __builtin_amdgcn_make_buffer_rsrc((void*)(A->qscale + T.q0), 0, QP_TILE * 4, 0x00020000);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lqs, 16, lane * 16, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lqs, 16, lo, 0, 0, 0);
     } else if (wave == 1 && FILTER) {
       const __amdgpu_buffer_rsrc_t rs =
           __builtin_amdgcn_make_buffer_rsrc((void*)(A->e.thr + T.q0), 0, QP_TILE * 4, 0x00020000);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lth, 16, lane * 16, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lth, 16, lo, 0, 0, 0);
     } else if (wave == 2 && A->cscale) {
       const int64_t rem = A->n_rows - T.c0;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(A->cscale + T.c0s), 0, (int)(rem < QP_TILE ? rem * 4 : QP_TILE * 4), 0x00020000);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lcs, 16, lane * 16, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lcs, 16, lo, 0, 0, 0);
     }
   };
 
@@ -624,7 +667,6 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
     issue_h(rc, rq, 1, P_B1, 1);
   }
   wait_vm<8>();  // A0(0), B0(0), B1(0)
-  zero_acc();
   qp_barrier();
 
   // One K-tile of four phases: P = buffer of this K-tile (compile time); (RC1, RQ1, K1): the tile
@@ -720,6 +762,7 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
       const QpTile T = tile_at(L);
       const __amdgpu_buffer_rsrc_t rc = rsrc_c(T), rq = rsrc_q(T);
       // K-tiles 0 .. kt-3 of the tile (pairs), then the boundary pair that stages the next tile
+      zero_acc();
       for (int t = 0; t < kt - 2; t += 2) {
         QP2_KTILE(0, fbx, fby, rc, rq, t + 1, rc, rq, t + 2, true);
         QP2_KTILE(1, fby, fbx, rc, rq, t + 2, rc, rq, t + 3, true);
@@ -743,143 +786,133 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
   auto acc_of = [&](int ah, int bh) -> const f32x4_t (&)[4][2] {
     return ah == 0 ? (bh == 0 ? acc0 : acc1) : (bh == 0 ? acc3 : acc2);
   };
-  // Filter mode. Each lane holds 4 query columns (bh, j) x 32 catalog rows (2 halves x 4
-  // accumulators x 4 rows); a block is one accumulator (4 consecutive rows of one query).
-  //   1. column test (every tile): the max of each column's 32 values against the query's
-  //      threshold -- 4 compares per lane, no per-block branches. SIMPLE (no row scales, a full
-  //      tile): max_r fl(a_r qs) = fl(max_r(a_r) qs) for qs >= 0 (rounding is monotone), so the
-  //      scale is applied once per column; NaNs drop out of fmaxf as they do out of >=.
-  //   2. only if some lane of the wave passed: block bits m (bit c*8 + ah*4 + i) for the flagged
-  //      columns.
-  //   3. the lane's flagged blocks go to its QP_STG_SLOTS LDS slots (rounds when a lane has
-  //      more; only the wave's flagged columns are visited), and a ROLLED loop over the lane's
-  //      own blocks computes the exact values, claims slots with one LDS atomic per block and
-  //      writes the hits: the work follows the lane's hits, not the union of the wave's blocks.
+  // Filter mode. Each lane holds 4 query columns c = bh * 2 + jj, each 32 catalog rows (2 halves
+  // x 4 accumulators x 4 rows).
+  //   1. column test (every tile): one max per column against the query's threshold, 4 compares
+  //      per lane. SIMPLE (no row scales): max_r fl(a_r qs) = fl(max_r(a_r) qs) for qs >= 0
+  //      (rounding is monotone), exact. With row scales the max is over fl(a_r cs_r), and the
+  //      threshold is lowered by a relative 2^-20 (+2^-120): fl(fl(a qs) cs) and fl(fl(a cs) qs)
+  //      are both within (1 +- 2^-24)^2 of a qs cs, so the test is a superset of the exact one.
+  //      NaNs drop out of fmaxf as they do out of >=; a column whose qs is not >= 0 is flagged.
+  //   2. only if some lane passed: the wave's flagged (lane, column) pairs get consecutive
+  //      indices (ballot + mbcnt per column) and are staged, QP_STG_COLS per round, into the
+  //      wave's LDS region: the column's 32 raw accumulators + {query, row group, qs, th}.
+  //   3. the whole wave processes the staged columns, 4 lanes x 8 values per column: exact
+  //      values fl(fl(a qs) cs) (the store mode's), the exact test, one LDS atomic per lane with
+  //      hits claims its slots, the hit stores. The cost follows the flagged columns, not the
+  //      32 blocks of every lane.
   auto filter_tile = [&](const QpTile& T, auto simple_tag) {
     constexpr bool SIMPLE = decltype(simple_tag)::value;
     const bool full = T.c0 + QP_TILE <= n_rows;  // uniform
-    float qs_r[2][2], th_r[2][2];
-    {
-      const int ql[4] = {wb * 32 + fr_, wb * 32 + 16 + fr_, 128 + wb * 32 + fr_,
-                         128 + wb * 32 + 16 + fr_};
-      float q4[4], t4[4];
-      lds_qs_th4(lqs, lth, ql, q4, t4);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        qs_r[c >> 1][c & 1] = q4[c];
-        th_r[c >> 1][c & 1] = t4[c];
-      }
-    }
+    const int g_ = lane_ >> 4;
+    const int ql4[4] = {wb * 32 + fr_, wb * 32 + 16 + fr_, 128 + wb * 32 + fr_,
+                        128 + wb * 32 + 16 + fr_};
+    float q4[4], t4[4];
+    lds_qs_th4(lqs, lth, ql4, q4, t4);
     auto max4 = [](float a, float b, float c, float d) { return fmaxf(fmaxf(a, b), fmaxf(c, d)); };
-    uint32_t m = 0;
+    uint32_t colm = 0;
     if constexpr (SIMPLE) {
-      uint32_t colm = 0;
-#pragma unroll
-      for (int bh = 0; bh < 2; ++bh)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          float mx = -__builtin_inff();
-#pragma unroll
-          for (int ah = 0; ah < 2; ++ah)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const f32x4_t& a = acc_of(ah, bh)[i][jj];
-              mx = fmaxf(mx, max4(a[0], a[1], a[2], a[3]));
-            }
-          colm |= (mx * qs_r[bh][jj] >= th_r[bh][jj] ? 1u : 0u) << (bh * 2 + jj);
-        }
-      if (__builtin_expect(__ballot(colm != 0u) == 0ull, 1)) return;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const int bh = c >> 1, jj = c & 1;
-        if (__ballot((colm >> c) & 1u) == 0ull) continue;
-#pragma unroll
-        for (int ah = 0; ah < 2; ++ah)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const f32x4_t& a = acc_of(ah, bh)[i][jj];
-            const float mx = max4(a[0], a[1], a[2], a[3]) * qs_r[bh][jj];
-            m |= (mx >= th_r[bh][jj] ? 1u : 0u) << (c * 8 + ah * 4 + i);
-          }
-      }
-    } else {
-      // row scales or a partial tile: the block bits directly (each block's values are used
-      // at once; a column pass first would keep all 128 values live and spill). Rows past
-      // n_rows are NOT masked here (they read 0): the block bits are a superset, the exact
-      // per-row test in the hit loop drops them.
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
+        float mx = -__builtin_inff();
 #pragma unroll
         for (int ah = 0; ah < 2; ++ah)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const f32x4_t& a = acc_of(ah, c >> 1)[i][c & 1];
-            const float qs = qs_r[c >> 1][c & 1];
-            const float4 cs = lds_float4(lcs + ah * 128 + wa * 64 + i * 16 + 4 * (lane_ >> 4));
-            const float mx = max4(a[0] * qs * cs.x, a[1] * qs * cs.y, a[2] * qs * cs.z,
-                                  a[3] * qs * cs.w);
-            m |= (mx >= th_r[c >> 1][c & 1] ? 1u : 0u) << (c * 8 + ah * 4 + i);
+            mx = fmaxf(mx, max4(a[0], a[1], a[2], a[3]));
           }
-      if (__builtin_expect(__ballot(m != 0u) == 0ull, 1)) return;
-    }
-    char* stg = smem + QP_LDS + QP_PARAM + tid_ * (QP_STG_SLOTS * 16);  // this lane's slots
-    // columns with a flagged block in some lane of the wave (uniform): only their 8 blocks are
-    // visited when staging
-    uint32_t cols = 0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      cols |= (__ballot(((m >> (8 * c)) & 0xffu) != 0u) != 0ull ? 1u : 0u) << c;
-    const int nblk = __popc(m);
-    uint32_t rest = m;
-#pragma unroll 1
-    for (int round = 0;; ++round) {
+        colm |= (mx * q4[c] >= t4[c] || !(q4[c] >= 0.f) ? 1u : 0u) << c;
+      }
+    } else {
+      f32x4_t cs[2][4];
+      lds_rowscales8(lcs + wa * 64 + 4 * g_, cs);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        if (!((cols >> c) & 1u)) continue;
+        float mx = -__builtin_inff();
 #pragma unroll
         for (int ah = 0; ah < 2; ++ah)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int g = c * 8 + ah * 4 + i;
-            const int rank = __popc(m & ((1u << g) - 1u));
-            if (((m >> g) & 1u) && rank / QP_STG_SLOTS == round)
-              *(f32x4_t*)(stg + (rank % QP_STG_SLOTS) * 16) = acc_of(ah, c >> 1)[i][c & 1];
+            const f32x4_t& a = acc_of(ah, c >> 1)[i][c & 1];
+            const f32x4_t& s = cs[ah][i];
+            mx = fmaxf(mx, max4(a[0] * s[0], a[1] * s[1], a[2] * s[2], a[3] * s[3]));
           }
+        const float th_lo = t4[c] - fabsf(t4[c]) * 0x1p-20f - 0x1p-120f;
+        colm |= (mx * q4[c] >= th_lo || !(q4[c] >= 0.f) ? 1u : 0u) << c;
       }
+    }
+    if (__builtin_expect(__ballot(colm != 0u) == 0ull, 1)) return;
+    // 2. compact indices: columns in order, lanes in order within a column (n: uniform)
+    int idx[4];
+    int n = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint64_t bc = __ballot((colm >> c) & 1u);
+      idx[c] = n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bc >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bc, 0u));
+      n += __popcll(bc);
+    }
+    const uint32_t wst = (uint32_t)(uintptr_t)(smem + QP_LDS + QP_PARAM + wave * QP_STG_WAVE);
+    const uint32_t wmeta = wst + QP_STG_COLS * 128;
+    uint64_t* cand = A->e.cand;
+    const int64_t ld_cand = A->e.ld_cand;
+    const int slots = A->e.slots;
+    const int64_t rbase = A->e.idx_base + T.c0;
 #pragma unroll 1
-      for (int s2 = 0; s2 < QP_STG_SLOTS; ++s2) {
-        if (__ballot(rest != 0u) == 0ull) break;
-        if (rest != 0u && (nblk - __popc(rest)) / QP_STG_SLOTS == round) {
-          const int g = __builtin_ctz(rest);
-          rest &= rest - 1u;
-          const int c = g >> 3, ah = (g >> 2) & 1, i = g & 3;
-          const int ql = (c >> 1) * 128 + wb * 32 + (c & 1) * 16 + fr_;
-          const int il = ah * 128 + wa * 64 + i * 16 + 4 * (lane_ >> 4);
-          f32x4_t a, csv;
-          float qs, th;
-          lds_hit_block(stg + s2 * 16, lqs + ql, lth + ql, lcs + il, a, qs, th, csv);
-          const float4 cs = make_float4(csv[0], csv[1], csv[2], csv[3]);
-          const float v[4] = {a[0] * qs * cs.x, a[1] * qs * cs.y, a[2] * qs * cs.z,
-                              a[3] * qs * cs.w};
-          uint32_t hb = 0;
+    for (int r0 = 0; r0 < n; r0 += QP_STG_COLS) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            hb |= (v[r] >= th && (full || T.c0 + il + r < n_rows) ? 1u : 0u) << r;
-          if (hb) {
-            const uint32_t base = lds_add_rtn(lcnt + ql, (uint32_t)__popc(hb));
-            uint64_t* dst = A->e.cand + (T.q0 + ql) * A->e.ld_cand + T.ct * A->e.slots;
+      for (int c = 0; c < 4; ++c) {
+        const int s = idx[c] - r0;
+        if (((colm >> c) & 1u) && s >= 0 && s < QP_STG_COLS) {
+          const f32x4_t(&ac0)[4][2] = acc_of(0, c >> 1);
+          const f32x4_t(&ac1)[4][2] = acc_of(1, c >> 1);
+          const int jj = c & 1;
+          const f32x4_t meta = {__builtin_bit_cast(float, (uint32_t)(ql4[c] | (g_ << 8))), q4[c],
+                                t4[c], 0.f};
+          lds_put_col(wst + s * 128, ac0[0][jj], ac0[1][jj], ac0[2][jj], ac0[3][jj], ac1[0][jj],
+                      ac1[1][jj], ac1[2][jj], ac1[3][jj], wmeta + s * 16, meta);
+        }
+      }
+      // 3. lane: staged column s, values u * 8 .. u * 8 + 7 = half ah = u >> 1, accumulators
+      // i0, i0 + 1 (i0 = (u & 1) * 2), rows il0 .. il0 + 3 and il0 + 16 .. il0 + 19
+      const int nr = n - r0 < QP_STG_COLS ? n - r0 : QP_STG_COLS;
+      const int s = lane_ >> 2, u = lane_ & 3;
+      if (s < nr) {
+        f32x4_t m, v0, v1;
+        lds_staged(wmeta + s * 16, wst + s * 128 + u * 32, m, v0, v1);
+        const uint32_t mw = __builtin_bit_cast(uint32_t, m[0]);
+        const int ql = (int)(mw & 255u), g = (int)(mw >> 8);
+        const float qs = m[1], th = m[2];
+        const int il0 = (u >> 1) * 128 + wa * 64 + (u & 1) * 32 + 4 * g;
+        f32x4_t c0 = {1.f, 1.f, 1.f, 1.f}, c1 = c0;
+        if constexpr (!SIMPLE) lds_f32x4x2(lcs + il0, c0, c1);
+        float v[8];
+        uint32_t hb = 0;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const uint32_t p = base + (uint32_t)__popc(hb & ((1u << r) - 1u));
-              if (((hb >> r) & 1u) && p < (uint32_t)A->e.slots) {
-                const uint32_t row = (uint32_t)(A->e.idx_base + T.c0 + il + r);
-                dst[p] = ((uint64_t)f2key(v[r]) << 32) | (uint64_t)(~row);
-              }
+        for (int k = 0; k < 8; ++k) {
+          const float a = k < 4 ? v0[k] : v1[k - 4];
+          v[k] = SIMPLE ? a * qs : a * qs * (k < 4 ? c0[k] : c1[k - 4]);
+          const int il = il0 + (k < 4 ? k : 12 + k);
+          hb |= (v[k] >= th && (full || T.c0 + il < n_rows) ? 1u : 0u) << k;
+        }
+        if (hb) {
+          const uint32_t base = lds_add_rtn(lcnt + ql, (uint32_t)__popc(hb));
+          uint64_t* dst = cand + (T.q0 + ql) * ld_cand + T.ct * slots;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t p = base + (uint32_t)__popc(hb & ((1u << k) - 1u));
+            if (((hb >> k) & 1u) && p < (uint32_t)slots) {
+              const uint32_t row = (uint32_t)(rbase + il0 + (k < 4 ? k : 12 + k));
+              // opaque key: otherwise the compiler hoists a 64-bit constant of f2key's zero case
+              // out of the tile loop, and at the K-loop's register peak spills it
+              uint32_t key = f2key(v[k]);
+              asm volatile("" : "+v"(key));
+              dst[p] = ((uint64_t)key << 32) | (uint64_t)(~row);
             }
           }
         }
       }
-      if (__ballot(nblk > QP_STG_SLOTS * (round + 1)) == 0ull) break;
     }
   };
   auto store_quadrant = [&](const QpTile& T, const f32x4_t (&acc)[4][2], int ah, int bh) {
@@ -963,7 +996,6 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
     if (last) break;
     L += n_x;
     issue_params(tile_at(L));
-    zero_acc();
   }
 #undef QP2_KTILE
   // the last tile restaged its own first K-tiles: drain before the LDS is released

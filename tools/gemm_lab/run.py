@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--d", type=int, default=1536)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--cscale", action="store_true", help="row scales in [0.5, 1.5) (the non-SIMPLE epilogue)")
     ap.add_argument("names", nargs="+")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -46,6 +47,7 @@ def main():
     q = torch.randn((B, d), generator=g, device=dev).half()
     c = torch.randn((N, d), generator=g, device=dev).half()
     qs = torch.ones(B, device=dev)
+    csf = (torch.rand(((N + 255) // 256) * 256, generator=g, device=dev) + 0.5) if a.cscale else None
     thr3 = torch.full((B,), 3.0 * d ** 0.5, device=dev)
     thri = torch.full((B,), float("inf"), device=dev)
     G, slots = 256, 32
@@ -58,7 +60,7 @@ def main():
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
 
     def launch(lib, thr):
-        rc = lib.ebt_screen_filter(P(q), B, P(c), N, d, d, 2, P(qs), None, P(thr), P(cand),
+        rc = lib.ebt_screen_filter(P(q), B, P(c), N, d, d, 2, P(qs), P(csf) if csf is not None else None, P(thr), P(cand),
                                    groups * slots, slots, P(counts), groups, P(ovf), 0, st)
         if rc:
             raise RuntimeError(lib.ebt_last_error().decode())
@@ -101,15 +103,19 @@ def main():
             res[n]["hits"].append(timed(libs[n], thr3))
             if hits_per_q is None:
                 hits_per_q = float(counts.float().sum(1).mean())
-            if r == 0:   # the per-(query, group) hit counts must not depend on the variant
+            if r == 0:   # the per-(query, group) hit counts and hit sets must not depend on the variant
+                cv = cand.view(B, groups, slots)
+                live = torch.arange(slots, device=dev)[None, None, :] < counts[:, :, None].long()
+                hs = torch.where(live, cv, torch.zeros_like(cv)).sort(dim=2).values
                 if ref is None:
-                    ref = counts.clone()
-                same[n] = bool(torch.equal(ref, counts))
+                    ref = (counts.clone(), hs)
+                same[n] = bool(torch.equal(ref[0], counts)) and bool(torch.equal(ref[1], hs))
+                cand.fill_(-1)
             res[n]["nohit"].append(timed(libs[n], thri))
     fl = 2.0 * B * N * d
     for n in a.names:
-        out = {"variant": n, "shape": [B, N, d], "hits_per_query": hits_per_q,
-               "counts_equal_first": same.get(n)}
+        out = {"variant": n, "shape": [B, N, d], "cscale": a.cscale, "hits_per_query": hits_per_q,
+               "hits_equal_first": same.get(n)}
         for kind, v in res[n].items():
             med = statistics.median(v)
             out[kind] = {"median_ms": round(med, 4), "min_ms": round(min(v), 4),
