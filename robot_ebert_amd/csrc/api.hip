@@ -187,7 +187,8 @@ static double poisson_tail(double lam, int m) {
 }
 
 // Speculative screen parameters (see run_screen). The sample: P evenly spaced full 256-row tiles
-// (P = min(64, tiles / 24), so at most ~4 % of the rows are screened twice); lambda = the expected
+// (P = min(64, tiles / 24), so at most ~4 % of the rows are screened twice, or one workgroup per
+// CU for small batches); lambda = the expected
 // number of sample rows at or above the rank-k' score, taking the sample as a uniform draw of
 // the rows; j = the smallest rank with P(Poisson(lambda) >= j) <= 1e-6, so a speculative
 // threshold is too high (caught by the VERIFY check -> unfused rerun) about once per million
@@ -202,6 +203,11 @@ static bool spec_params(int64_t B_pad, int64_t n_rows, int32_t kprime, int64_t* 
   if (!enabled || B_pad % 256 != 0 || kprime > SPEC_KPRIME_MAX) return false;
   const int64_t full = n_rows / 256;
   int64_t P = full / 24;
+  // a sample that leaves CUs idle costs one tile's latency whatever its size: with few query
+  // tiles take up to one workgroup per CU (MI355X: 256) while that stays within 1/6 of the rows
+  // (C2: 64 tiles instead of 16 -> ~300 instead of ~565 hits per query, one filter launch)
+  const int64_t fill = 256 / (B_pad / 256 > 0 ? B_pad / 256 : 1);
+  if (P < fill && fill <= full / 6) P = fill;
   P = P > 64 ? 64 : P;
   // whole rounds of workgroups: P x (query tiles) a multiple of 256 when that keeps >= 8 tiles
   const int64_t per = 256 / (B_pad / 256) > 0 ? 256 / (B_pad / 256) : 1;

@@ -86,11 +86,29 @@ def trivepi(src):
     return src[:a] + """    { float sm = 0.f;
       for (int i = 0; i < 4; ++i) for (int jj = 0; jj < 2; ++jj) for (int r = 0; r < 4; ++r)
         sm += acc0[i][jj][r] + acc1[i][jj][r] + acc2[i][jj][r] + acc3[i][jj][r];
-      if (sm == 1234.5f) e.ovf[0] = 1; }
+      if (sm == 1234.5f) A->e.ovf[0] = 1; }
 """ + src[b:]
 
 
-VARIANTS = {"trivepi": trivepi, "noepi": noepi, "noepi_nofin": noepi_nofin, "l2only": l2only, "nobar": nobar, "nowait": nowait, "grp2": grp(2), "grp8": grp(8), "grp16": grp(16),"base": lambda s: s, "nosleep": nosleep, "prio_static": prio_static,
+def nozero(src):
+    # diagnostic (wrong results): the accumulators are not cleared between tiles
+    return _sub(src, "      zero_acc();\n      for (int t = 0; t < kt - 2; t += 2) {",
+                "      for (int t = 0; t < kt - 2; t += 2) {", 1)
+
+
+def nocoltest(src):
+    # diagnostic (wrong results): the SIMPLE column test is one compare per column on a single
+    # accumulator value
+    a = src.index("    if constexpr (SIMPLE) {\n#pragma unroll\n      for (int c = 0; c < 4; ++c) {\n        float mx")
+    b = src.index("    } else {\n      f32x4_t cs[2][4];")
+    return src[:a] + """    if constexpr (SIMPLE) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        colm |= (acc_of(0, c >> 1)[0][c & 1][0] * q4[c] >= t4[c] ? 1u : 0u) << c;
+""" + src[b:]
+
+
+VARIANTS = {"nozero": nozero, "nocoltest": nocoltest, "trivepi": trivepi, "noepi": noepi, "noepi_nofin": noepi_nofin, "l2only": l2only, "nobar": nobar, "nowait": nowait, "grp2": grp(2), "grp8": grp(8), "grp16": grp(16),"base": lambda s: s, "nosleep": nosleep, "prio_static": prio_static,
             "prio_static_sleep": prio_static_sleep}
 
 
