@@ -58,7 +58,8 @@ int spec_threshold(const float*, int64_t, int64_t, int64_t, int, const float*, c
                    int*, int, hipStream_t);
 int kth_threshold(const float*, int64_t, int64_t, int64_t, int, const float*, float*,
                   hipStream_t);
-int pool_kth(const float*, int64_t, int64_t, int64_t, int, int, float*, hipStream_t);
+int pool_kth(const float*, int64_t, int64_t, int64_t, int, int, float*, hipStream_t,
+             float* fv = nullptr, int64_t* fi = nullptr, int kprime = 0, int* ovf = nullptr);
 int screen_gemm_pool(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
                      const float*, const float*, int64_t, float*, int64_t, hipStream_t);
 int merge_segment(float*, int64_t*, int64_t, int, const uint64_t*, int64_t, int, const uint8_t*,
@@ -672,20 +673,24 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
     if (rc) return rc;
     {
       StageScope s(timer, EBT_STAGE_SELECT, st);
-      rc = pool_kth(pooled, L.ld_s, B, B_pad, (int)(m / 64), L.spec_j, tspec, st);
+      // theta_spec, and the empty list (-inf / -1) with no overflow yet
+      rc = pool_kth(pooled, L.ld_s, B, B_pad, (int)(m / 64), L.spec_j, tspec, st, fv, fi, kprime,
+                    ovf);
     }
     if (rc) return rc;
   }
   const double spec_hits = given ? (a.hits > 0.0 ? a.hits : 1.0) : L.spec_hits;
-  // empty list (-inf / -1), no overflow yet
-  const float ninf = -__builtin_inff();
-  uint32_t bits;
-  memcpy(&bits, &ninf, 4);
-  rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)fv, (int)bits, (size_t)B * kprime, st),
-                 "hipMemsetD32Async");
-  if (!rc) rc = hip_check(hipMemsetAsync(fi, 0xff, (size_t)B * kprime * 8, st), "hipMemsetAsync");
-  if (!rc) rc = hip_check(hipMemsetAsync(ovf, 0, (size_t)B_pad * 4, st), "hipMemsetAsync");
-  if (rc) return rc;
+  if (given) {  // empty list (-inf / -1), no overflow yet
+    const float ninf = -__builtin_inff();
+    uint32_t bits;
+    memcpy(&bits, &ninf, 4);
+    rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)fv, (int)bits, (size_t)B * kprime, st),
+                   "hipMemsetD32Async");
+    if (!rc)
+      rc = hip_check(hipMemsetAsync(fi, 0xff, (size_t)B * kprime * 8, st), "hipMemsetAsync");
+    if (!rc) rc = hip_check(hipMemsetAsync(ovf, 0, (size_t)B_pad * 4, st), "hipMemsetAsync");
+    if (rc) return rc;
+  }
   // hits per group ~ H group_rows / n (per query; its threshold's own spread ~ 1/sqrt(j) on
   // top): slots for 4x that + 4, and at least enough that a group overflow (which costs its
   // query an unfused rerun of the whole catalog) is expected less than once per thousand batches

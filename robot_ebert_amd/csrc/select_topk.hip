@@ -925,13 +925,26 @@ __global__ void spec_threshold_kernel(const float* __restrict__ vals, int64_t ld
 // -> -inf (keep everything: the merge overflows and the query is rerun unfused). E = maxima per
 // lane (G <= 64 E): 4 for one shard's sample, up to 32 for the maxima of all shards
 // (ebt_pool_kth over the all-gathered samples of a row-sharded catalog).
+// Optionally (fv != null) the same wave also starts query b's empty list for the speculative
+// screen (fv -inf / fi -1 over k' entries, ovf 0): three memsets fewer per batch.
 template <int E>
 __global__ __launch_bounds__(256) void pool_kth_kernel(const float* __restrict__ pool, int64_t ld,
                                                        int64_t B, int64_t B_pad, int G, int j,
-                                                       float* __restrict__ thr) {
+                                                       float* __restrict__ thr,
+                                                       float* __restrict__ fv,
+                                                       int64_t* __restrict__ fi, int kprime,
+                                                       int* __restrict__ ovf) {
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B_pad) return;
+  if (fv) {
+    if (lane == 0) ovf[b] = 0;
+    if (b < B)
+      for (int i = lane; i < kprime; i += 64) {
+        fv[b * kprime + i] = -__builtin_inff();
+        fi[b * kprime + i] = -1;
+      }
+  }
   if (b >= B) {
     if (lane == 0) thr[b] = __builtin_inff();
     return;
@@ -961,16 +974,19 @@ __global__ __launch_bounds__(256) void pool_kth_kernel(const float* __restrict__
   if (lane == 0) thr[b] = key2f((uint32_t)lo);
 }
 int pool_kth(const float* pool, int64_t ld, int64_t B, int64_t B_pad, int G, int j, float* thr,
-             hipStream_t st) {
-  if (!pool || !thr || B < 0 || B_pad < B || G < 1 || G > 2048 || j < 1 || ld < G) {
+             hipStream_t st, float* fv, int64_t* fi, int kprime, int* ovf) {
+  if (!pool || !thr || B < 0 || B_pad < B || G < 1 || G > 2048 || j < 1 || ld < G ||
+      (fv && (!fi || !ovf || kprime < 1))) {
     set_error("pool_kth: bad arguments (G=%d j=%d ld=%lld)", G, j, (long long)ld);
     return EBT_EINVAL;
   }
   const dim3 grid((unsigned)ceil_div(B_pad, 4)), block(256);
   if (G <= 256)
-    hipLaunchKernelGGL(pool_kth_kernel<4>, grid, block, 0, st, pool, ld, B, B_pad, G, j, thr);
+    hipLaunchKernelGGL(pool_kth_kernel<4>, grid, block, 0, st, pool, ld, B, B_pad, G, j, thr, fv,
+                       fi, kprime, ovf);
   else
-    hipLaunchKernelGGL(pool_kth_kernel<32>, grid, block, 0, st, pool, ld, B, B_pad, G, j, thr);
+    hipLaunchKernelGGL(pool_kth_kernel<32>, grid, block, 0, st, pool, ld, B, B_pad, G, j, thr, fv,
+                       fi, kprime, ovf);
   return launch_check("pool_kth_kernel");
 }
 

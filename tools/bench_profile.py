@@ -9,12 +9,14 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DOMINANT = "screen_gemm_qp2_kernel<false, 1>"  # f16 image, EPI_FILTER epilogue
+# the filter-epilogue screening GEMM (EPI_FILTER = 1), f16 or bf16 image, even or odd K-tiles
+DOMINANT_RX = re.compile(r"screen_gemm_qp2_kernel<(true|false), 1")
 
 
 def per_kernel(path, counter):
@@ -50,9 +52,11 @@ def main(d, cfg, rnd):
         kernels[k] = {"fetch_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                       "hbm_bytes_per_launch": rd + wr, "launches": fn,
                       "avg_ns": avg_ns.get(k)}
+    dom = [k for k in kernels if DOMINANT_RX.match(k)]
+    dom = max(dom, key=lambda k: kernels[k]["launches"]) if dom else None
     out = {"config": cfg, "round": rnd, "kernels": kernels,
-           "dominant": DOMINANT,
-           "hbm_bytes_per_launch": kernels.get(DOMINANT, {}).get("hbm_bytes_per_launch"),
+           "dominant": dom,
+           "hbm_bytes_per_launch": kernels.get(dom, {}).get("hbm_bytes_per_launch"),
            "note": "FETCH_SIZE x 2 + WRITE_SIZE (KiB -> bytes), Infinity-Cache hits included; "
                    "collected by tools/prof_bench.sh (separate --pmc passes, kernel filter "
                    "screen_gemm) on the bench.py command of this config"}

@@ -114,6 +114,9 @@ VARIANTS = {"nozero": nozero, "nocoltest": nocoltest, "trivepi": trivepi, "noepi
 
 def build(name):
     ref = os.environ.get("GEMM_LAB_REF")  # e.g. HEAD: patch the committed source instead
+    if ":" in name:  # NAME:REF builds variant `base` of commit REF under NAME
+        name, ref = name.split(":", 1)
+        VARIANTS.setdefault(name, lambda s: s)
     if ref:
         src = subprocess.run(["git", "-C", ROOT, "show", f"{ref}:robot_ebert_amd/csrc/screen_gemm.hip"],
                              check=True, capture_output=True, text=True).stdout
