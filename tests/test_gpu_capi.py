@@ -160,3 +160,58 @@ def test_capi_errors(cuda_device, lib):
     assert rc == -1 and b"sorted" in lib.ebt_last_error()
     rc, _, _ = topk(lib, cat, 10, cuda_device, liked=csr([[1, 5000]], cuda_device))
     assert rc == -1 and b"not in the catalog" in lib.ebt_last_error()
+
+
+def test_capi_memory_errors(cuda_device, lib):
+    """Every buffer is the caller's: an undersized state or workspace fails with EBT_ENOMEM
+    (-3) and the needed size in the message, before any kernel runs; an unsupported k
+    (min(k, n) > 4096) makes ebt_workspace_bytes return 0; the catalog stays usable afterwards."""
+    dev = cuda_device
+    emb = torch.randn((6000, 64), device=dev)
+    n, d = emb.shape
+    st = torch.cuda.current_stream(dev).cuda_stream
+    need = lib.ebt_catalog_state_bytes(P(emb), CODE[emb.dtype], n, d, d)
+    small = torch.empty(need - 256, dtype=torch.uint8, device=dev)
+    c0 = Catalog()
+    rc = lib.ebt_catalog_init(ctypes.byref(c0), P(emb), CODE[emb.dtype], n, d, d, 0, P(small),
+                              need - 256, st)
+    assert rc == -3 and b"state" in lib.ebt_last_error()
+    cat, state = make_catalog(lib, emb)
+    # min(k, n) <= 4096 is supported (k >= n on a small catalog returns every row)
+    assert lib.ebt_workspace_bytes(ctypes.byref(cat), 4, 5000, None) == 0
+    assert lib.ebt_workspace_bytes(ctypes.byref(cat), 4, 6000, None) == 0
+    assert lib.ebt_workspace_bytes(ctypes.byref(cat), 4, 4096, None) > 0
+    q = torch.randn((4, d), device=dev)
+    k = 10
+    ws_bytes = lib.ebt_workspace_bytes(ctypes.byref(cat), 4, k, None)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    s = torch.full((4, k), -7.0, dtype=torch.float64, device=dev)
+    r = torch.full((4, k), -7, dtype=torch.int64, device=dev)
+    rc = lib.ebt_cosine_topk(ctypes.byref(cat), P(q), CODE[q.dtype], 4, d, None, None, k, None,
+                             None, None, P(ws), ws_bytes - 1, P(s), P(r), None, st)
+    assert rc == -3 and b"workspace" in lib.ebt_last_error()
+    torch.cuda.synchronize(dev)
+    assert (s == -7.0).all() and (r == -7).all()          # nothing was written
+    rc, s2, r2 = topk(lib, cat, k, dev, q=q)
+    assert rc == 0 and (r2 >= 0).all()
+
+
+def test_workspace_allocation_failure_is_loud(cuda_device):
+    """The Python surface allocates the workspace with torch: when it cannot, the caller gets
+    torch's OutOfMemoryError (no partial result, no fallback), and the next call succeeds."""
+    import robot_ebert_amd as ebt
+    dev = cuda_device
+    cat = ebt.Catalog(torch.randn((200_000, 256), device=dev))
+    q = torch.randn((4096, 256), device=dev)
+    free, total = torch.cuda.mem_get_info(dev)
+    used = torch.cuda.memory_allocated(dev)
+    torch.cuda.empty_cache()
+    # leave room for what is allocated now plus 1 MiB: the batch's workspace cannot fit
+    torch.cuda.set_per_process_memory_fraction((used + (1 << 20)) / total, dev)
+    try:
+        with pytest.raises(torch.OutOfMemoryError):
+            ebt.score_topk(cat, 100, queries=q)
+    finally:
+        torch.cuda.set_per_process_memory_fraction(1.0, dev)
+    s, r = ebt.score_topk(cat, 100, queries=q[:8])
+    assert (r >= 0).all()
