@@ -24,6 +24,10 @@ namespace ebt {
 
 int query_liked_sum(const void*, int, int32_t, int64_t, const double*, int64_t, const int64_t*,
                     const int64_t*, double*, hipStream_t, int64_t row_offset);
+size_t large_topk_bytes(int64_t B, int64_t n, int64_t* Bg_out);
+int large_topk(const double*, int64_t, int32_t, const void*, int, int64_t, const double*, int64_t,
+               int64_t, const int64_t*, const int64_t*, int32_t, double*, int64_t*, void*, size_t,
+               hipStream_t);
 
 namespace {
 
@@ -89,12 +93,14 @@ PrepLayout prep_layout(const ebt_catalog& c, int64_t rows) {
 // The whole workspace of one batch:
 //   [prep B] [pass: max(first pass, every retry pass)] [results k_eff < k] [cert B + flag]
 //   [retry: prep R, results R x k_eff, cert R, gather indices, exclusion CSR of the group]
+// large: min(k, n) > 4096, the full-sort path (large_k.hip): [prep B] [sort buffers] [cert B + flag]
 struct DriverLayout {
   int64_t B, B_pad, R, chunk, chunk_r;
   int32_t k_eff, kprime, flags;
+  bool large;
   PrepLayout prep, prep_r;
   size_t off_prep, off_pass, pass_bytes, off_res_s, off_res_r, off_cert, off_rprep, off_rs,
-      off_rr, off_rcert, off_idx, off_roff, off_rrows, bytes;
+      off_rr, off_rcert, off_idx, off_roff, off_rrows, off_big, big_bytes, bytes;
 };
 
 bool driver_layout(const ebt_catalog& c, int64_t B, int32_t k, const ebt_options& opt,
@@ -107,7 +113,23 @@ bool driver_layout(const ebt_catalog& c, int64_t B, int32_t k, const ebt_options
   D.B = B;
   D.B_pad = pad_batch(B);
   D.k_eff = (int32_t)(k < c.n ? k : c.n);
-  if (D.k_eff > KPRIME_MAX) return false;
+  if (D.k_eff > KPRIME_MAX) {  // beyond the screen's k' range: every score, a full sort
+    const size_t big = large_topk_bytes(B, c.n, nullptr);
+    if (big == 0) return false;
+    D.large = true;
+    D.flags = opt.flags;
+    D.prep = prep_layout(c, B);
+    size_t o = 0;
+    D.off_prep = o;
+    o = al(o + D.prep.bytes);
+    D.off_big = o;
+    D.big_bytes = big > (size_t)B * 8 ? big : (size_t)B * 8;  // also the liked path's scratch
+    o = al(o + D.big_bytes);
+    D.off_cert = o;
+    o = al(o + (size_t)(B + 1) * 4);
+    D.bytes = o;
+    return true;
+  }
   D.kprime = default_kprime(c, D.k_eff);
   if (opt.kprime) {  // search.py's clamp: [round_up(k, 4), min(round_up(n, 4), 4096)]
     int64_t kp = round_up(opt.kprime, 4), hi = round_up(c.n, 4), lo = round_up(D.k_eff, 4);
@@ -416,8 +438,8 @@ int ebt_cosine_topk_submit(const ebt_catalog* cat, const void* q, int q_dtype, i
   const ebt_options o = opt ? *opt : ebt_options{};
   DriverLayout L;
   if (!driver_layout(*cat, B, k, o, &L)) {
-    set_error("ebt_cosine_topk: unsupported sizes or options (B=%lld k=%d n=%lld: k <= 4096 "
-              "or k >= n; chunk_rows % 128 == 0; flags EBT_FLAG_NO_FUSE only)",
+    set_error("ebt_cosine_topk: unsupported sizes or options (B=%lld k=%d n=%lld: n < 2^31; "
+              "chunk_rows % 128 == 0; flags EBT_FLAG_NO_FUSE only)",
               (long long)B, k, (long long)cat->n);
     return EBT_EINVAL;
   }
@@ -429,15 +451,24 @@ int ebt_cosine_topk_submit(const ebt_catalog* cat, const void* q, int q_dtype, i
   char* ws = (char*)workspace;
   char* prep = ws + L.off_prep;
   int rc = q ? prep_dense(*cat, q, q_dtype, B, ldq, L.prep, prep, st)
-             : prep_liked(*cat, liked_off, liked_rows, B, L.prep, prep, ws + L.off_pass,
-                          L.pass_bytes, st);
+             : prep_liked(*cat, liked_off, liked_rows, B, L.prep, prep,
+                          ws + (L.large ? L.off_big : L.off_pass),
+                          L.large ? L.big_bytes : L.pass_bytes, st);
   if (rc) return rc;
   int32_t* cert = (int32_t*)(ws + L.off_cert);
-  const bool padded = L.k_eff < k;
-  double* rs = padded ? (double*)(ws + L.off_res_s) : out_scores;
-  int64_t* rr = padded ? (int64_t*)(ws + L.off_res_r) : out_rows;
-  rc = run_prepared(*cat, L.prep, prep, B, excl_off, excl_rows, L.k_eff, L.kprime, L.chunk,
-                    L.flags, ws + L.off_pass, L.pass_bytes, rs, rr, cert, timer, st);
+  if (L.large) {  // exact: every certificate is 1, the results are final
+    rc = large_topk((const double*)(prep + L.prep.q64), B, cat->d, cat->data, cat->dtype,
+                    cat->ld, cat->gnorm64, cat->n, cat->row_offset, excl_off, excl_rows, k,
+                    out_scores, out_rows, ws + L.off_big, L.big_bytes, st);
+    if (!rc) rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)cert, 1, (size_t)B, st),
+                            "hipMemsetD32Async");
+  } else {
+    const bool padded = L.k_eff < k;
+    double* rs = padded ? (double*)(ws + L.off_res_s) : out_scores;
+    int64_t* rr = padded ? (int64_t*)(ws + L.off_res_r) : out_rows;
+    rc = run_prepared(*cat, L.prep, prep, B, excl_off, excl_rows, L.k_eff, L.kprime, L.chunk,
+                      L.flags, ws + L.off_pass, L.pass_bytes, rs, rr, cert, timer, st);
+  }
   if (rc) return rc;
   // the exclusion check's flag sits right after the certificates: one copy brings both
   rc = hip_check(hipMemsetAsync(cert + B, 0, 4, st), "hipMemsetAsync");
@@ -504,6 +535,7 @@ int ebt_cosine_topk_finish(ebt_pending* p) {
     set_error("ebt_cosine_topk: exclusion rows must be sorted ascending within each query");
     return EBT_EINVAL;
   }
+  if (L.large) return EBT_OK;  // the full-sort path is exact: nothing to retry or pad
   char* ws = p->ws;
   const bool padded = L.k_eff < p->k;
   double* rs = padded ? (double*)(ws + L.off_res_s) : p->out_scores;

@@ -124,9 +124,9 @@ def _hydrate(s: np.ndarray, r: np.ndarray) -> List[Recommendation]:
 def get_user_recs(user_id: str, k: int = 10) -> List[Recommendation]:
     """GPU drop-in for lib.py:32-63 (same inputs, same outputs, same errors).
 
-    Limit: min(k, catalog rows) <= 4096 (a larger k raises EbertError; the reference's pandas
-    `[:k]` takes any k, its route defaults to k = 10, api/users.py:150-155). On a row-sharded
-    catalog the cross-shard merge needs ranks * k <= 8192 (k <= 1024 at 8 GPUs)."""
+    Any k, as the reference's pandas `[:k]` (min(k, rows) > 4096 runs the full-sort path of
+    csrc/large_k.hip). On a row-sharded catalog min(k, rows) <= 4096 and the cross-shard merge
+    needs ranks * k <= 8192 (k <= 1024 at 8 GPUs)."""
     req = _user_request(user_id)
     if req is None:
         return []

@@ -164,8 +164,8 @@ def test_capi_errors(cuda_device, lib):
 
 def test_capi_memory_errors(cuda_device, lib):
     """Every buffer is the caller's: an undersized state or workspace fails with EBT_ENOMEM
-    (-3) and the needed size in the message, before any kernel runs; an unsupported k
-    (min(k, n) > 4096) makes ebt_workspace_bytes return 0; the catalog stays usable afterwards."""
+    (-3) and the needed size in the message, before any kernel runs; invalid sizes make
+    ebt_workspace_bytes return 0; the catalog stays usable afterwards."""
     dev = cuda_device
     emb = torch.randn((6000, 64), device=dev)
     n, d = emb.shape
@@ -177,10 +177,11 @@ def test_capi_memory_errors(cuda_device, lib):
                               need - 256, st)
     assert rc == -3 and b"state" in lib.ebt_last_error()
     cat, state = make_catalog(lib, emb)
-    # min(k, n) <= 4096 is supported (k >= n on a small catalog returns every row)
-    assert lib.ebt_workspace_bytes(ctypes.byref(cat), 4, 5000, None) == 0
-    assert lib.ebt_workspace_bytes(ctypes.byref(cat), 4, 6000, None) == 0
+    # any k: min(k, n) > 4096 takes the full-sort path (tests/test_gpu_large_k.py)
+    assert lib.ebt_workspace_bytes(ctypes.byref(cat), 4, 5000, None) > 0
+    assert lib.ebt_workspace_bytes(ctypes.byref(cat), 4, 7000, None) > 0
     assert lib.ebt_workspace_bytes(ctypes.byref(cat), 4, 4096, None) > 0
+    assert lib.ebt_workspace_bytes(ctypes.byref(cat), 0, 10, None) == 0    # invalid batch
     q = torch.randn((4, d), device=dev)
     k = 10
     ws_bytes = lib.ebt_workspace_bytes(ctypes.byref(cat), 4, k, None)
