@@ -455,7 +455,7 @@ def _submit_c(catalog: Catalog, k: int, queries, liked, exclude, kprime, chunk_r
     need = lib.ebt_workspace_bytes(ctypes.byref(catalog.cstruct), B, k, ctypes.byref(opt))
     if need == 0:
         raise EbertError(f"k={k}, batch {B} over a {catalog.n}-row catalog is not supported "
-                         f"({_lib.load().ebt_last_error().decode() or 'ebt_workspace_bytes = 0'})")
+                         f"(ebt_workspace_bytes returned 0)")
     ws = torch.empty(need, dtype=torch.uint8, device=dev)
     out_s = torch.empty((B, k), dtype=torch.float64, device=dev)
     out_r = torch.empty((B, k), dtype=torch.int64, device=dev)
