@@ -185,7 +185,7 @@ int ebt_merge_hits(float* fv, int64_t* fi, int64_t B, int32_t kprime, int32_t k,
                    const int64_t* excl_off, const int64_t* excl_rows, int32_t* ovf, void* stream);
 
 /* Merge R partial top-k lists (scores/rows [R][B][k], each sorted) into the global top-k per
- * query -- the post-all-gather step of a row-sharded catalog. R*k <= 8192. */
+ * query -- the post-all-gather step of a row-sharded catalog. k <= 4096, any R. */
 int ebt_merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, int32_t k,
                    double* out_scores, int64_t* out_rows, void* stream);
 

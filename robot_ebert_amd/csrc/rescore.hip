@@ -309,6 +309,12 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
 }
 
 // ------------------------------------------------------------------------------- merge -----
+// The k best of R sorted partial lists per query, (score desc, row asc). Up to MERGE_CAP
+// entries are sorted in LDS at once: R k <= MERGE_CAP in one bitonic sort; more ranks in rounds
+// that keep the running top k in slots [0, k) and bring the next (MERGE_CAP - k) / k ranks in
+// behind it (k <= MERGE_CAP / 2).
+constexpr int MERGE_CAP = 8192;
+
 __global__ __launch_bounds__(RTHREADS) void merge_topk_kernel(const double* __restrict__ scores,
                                                                const int64_t* __restrict__ rows,
                                                                int R, int64_t B, int k, int P,
@@ -318,25 +324,38 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_kernel(const double* __re
   double* sc = (double*)smem;
   int64_t* rw = (int64_t*)(sc + P);
   const int64_t b = blockIdx.x;
-  const int n = R * k;
-  for (int i = threadIdx.x; i < P; i += RTHREADS) {
-    double s = -__builtin_inf();
-    int64_t r = INT64_MAX;
-    if (i < n) {
-      const int rr = i / k, j = i - rr * k;
-      const int64_t off = ((int64_t)rr * B + b) * k + j;
-      const int64_t row = rows[off];
-      if (row >= 0) {
-        const double v = scores[off];
-        s = (v == v) ? v : -__builtin_inf();
-        r = row;
+  // fill slots [base, P) with ranks [r0, r0 + m), -inf past them
+  auto fill = [&](int base, int r0, int m) {
+    const int n = m * k;
+    for (int i = base + threadIdx.x; i < P; i += RTHREADS) {
+      double s = -__builtin_inf();
+      int64_t r = INT64_MAX;
+      const int e = i - base;
+      if (e < n) {
+        const int rr = r0 + e / k, j = e % k;
+        const int64_t off = ((int64_t)rr * B + b) * k + j;
+        const int64_t row = rows[off];
+        if (row >= 0) {
+          const double v = scores[off];
+          s = (v == v) ? v : -__builtin_inf();
+          r = row;
+        }
       }
+      sc[i] = s;
+      rw[i] = r;
     }
-    sc[i] = s;
-    rw[i] = r;
-  }
-  __syncthreads();
+    __syncthreads();
+  };
+  int r0 = R * k <= P ? R : P / k;
+  fill(0, 0, r0);
   bitonic_pairs(sc, rw, P);
+  const int per = (P - k) / k;
+  while (r0 < R) {
+    const int m = R - r0 < per ? R - r0 : per;
+    fill(k, r0, m);
+    bitonic_pairs(sc, rw, P);
+    r0 += m;
+  }
   for (int j = threadIdx.x; j < k; j += RTHREADS) {
     const int64_t r = rw[j];
     out_s[b * k + j] = r == INT64_MAX ? __builtin_nan("") : sc[j];
@@ -346,13 +365,13 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_kernel(const double* __re
 
 int merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, int32_t k,
                double* out_s, int64_t* out_r, hipStream_t st) {
-  if (!scores || !rows || !out_s || !out_r || R < 1 || B < 0 || k < 1 ||
-      (int64_t)R * k > 8192) {
-    set_error("ebt_merge_topk: bad arguments (R=%d k=%d; R*k must be <= 8192)", R, k);
+  if (!scores || !rows || !out_s || !out_r || R < 1 || B < 0 || k < 1 || k > MERGE_CAP / 2) {
+    set_error("ebt_merge_topk: bad arguments (R=%d k=%d; k must be <= %d)", R, k, MERGE_CAP / 2);
     return EBT_EINVAL;
   }
   if (B == 0) return EBT_OK;
-  const int P = next_pow2_h(R * k);
+  const int64_t n = (int64_t)R * k;
+  const int P = next_pow2_h((int)(n < MERGE_CAP ? n : MERGE_CAP));
   (void)hipFuncSetAttribute((const void*)merge_topk_kernel,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)(P * 16));
   hipLaunchKernelGGL(merge_topk_kernel, dim3((unsigned)B), dim3(RTHREADS), (size_t)P * 16, st,

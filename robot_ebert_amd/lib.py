@@ -125,8 +125,7 @@ def get_user_recs(user_id: str, k: int = 10) -> List[Recommendation]:
     """GPU drop-in for lib.py:32-63 (same inputs, same outputs, same errors).
 
     Any k, as the reference's pandas `[:k]` (min(k, rows) > 4096 runs the full-sort path of
-    csrc/large_k.hip). On a row-sharded catalog min(k, rows) <= 4096 and the cross-shard merge
-    needs ranks * k <= 8192 (k <= 1024 at 8 GPUs)."""
+    csrc/large_k.hip). On a row-sharded catalog min(k, rows) <= 4096."""
     req = _user_request(user_id)
     if req is None:
         return []

@@ -79,3 +79,44 @@ def test_filter_matches_store(cuda_device, density, d, scaled):
     mean_hits = float(want_cnt.sum()) / B
     print(f"d={d} scaled={scaled} density={density}: {mean_hits:.0f} hits per query, "
           f"{int((~fits).sum())} overflowing groups")
+
+
+@pytest.mark.parametrize("R,k", [(2, 100), (8, 1000), (16, 1000), (3, 4096), (64, 128)])
+def test_merge_topk_any_rank_count(cuda_device, R, k):
+    """ebt_merge_topk (the post-all-gather merge) for R * k above one LDS sort (8192): rounds
+    that keep the running top k; equals a numpy (score desc, row asc) merge, with ties across
+    ranks, empty (-1) slots and NaN scores sorting last."""
+    from robot_ebert_amd import _lib as L
+    dev = cuda_device
+    B = 6
+    rng = np.random.default_rng(R * 7 + k)
+    s = np.round(rng.standard_normal((R, B, k)), 2)          # many exact ties across ranks
+    rows = rng.permutation(R * B * k * 2)[:R * B * k].reshape(R, B, k).astype(np.int64)
+    s[:, :, -3:] = np.nan
+    rows[:, :, -1] = -1
+    s[:, 0, :] = 0.5                                          # one query all tied
+    # each rank's list sorted (score desc, row asc), NaN / -1 last
+    for r in range(R):
+        for b in range(B):
+            key = np.where(rows[r, b] < 0, -np.inf, np.where(np.isnan(s[r, b]), -np.inf, s[r, b]))
+            o = np.lexsort((np.where(rows[r, b] < 0, np.iinfo(np.int64).max, rows[r, b]), -key))
+            s[r, b], rows[r, b] = s[r, b][o], rows[r, b][o]
+    ts = torch.tensor(s, device=dev)
+    tr = torch.tensor(rows, device=dev)
+    os_ = torch.empty((B, k), dtype=torch.float64, device=dev)
+    or_ = torch.empty((B, k), dtype=torch.int64, device=dev)
+    L.call("ebt_merge_topk", L.ptr(ts), L.ptr(tr), R, B, k, L.ptr(os_), L.ptr(or_),
+           L.stream_of(dev))
+    torch.cuda.synchronize(dev)
+    got_s, got_r = os_.cpu().numpy(), or_.cpu().numpy()
+    for b in range(B):
+        fs, fr = s[:, b].ravel(), rows[:, b].ravel()
+        ok = fr >= 0
+        key = np.where(np.isnan(fs[ok]), -np.inf, fs[ok])
+        o = np.lexsort((fr[ok], -key))[:k]
+        want_r = fr[ok][o]
+        want_s = np.where(np.isnan(fs[ok][o]), -np.inf, fs[ok][o])
+        m = len(want_r)
+        assert np.array_equal(got_r[b, :m], want_r), b
+        assert np.array_equal(got_s[b, :m], want_s), b
+        assert (got_r[b, m:] == -1).all()
