@@ -168,11 +168,27 @@ def cpu_baseline_and_parity(cfg, cat_gpu: torch.Tensor, q_gpu: torch.Tensor, s_g
     # parity sample over the full catalog (>= 64 queries per config; 32 at
     # the multi-GPU-sized catalogs, where the host oracle streams 10M-50M rows)
     n_par = n_parity or (128 if n_all <= BASE_ROWS_MAX else 32)
+    return base, oracle_parity(k, host_blocks(cat_gpu, n_all), Q, s_gpu, r_gpu, n_par,
+                               "full catalog, streamed in row blocks")
+
+
+def global_blocks(cfg, device, block: int = 1 << 17):
+    """Row blocks of the WHOLE global catalog as host float32 arrays, regenerated on `device`
+    from the same seeds every rank's shard came from (N > 1: rank 0 holds only its shard)."""
+    for r0 in range(0, cfg["n"], block):
+        r1 = min(cfg["n"], r0 + block)
+        yield r0, make_catalog_shard(cfg, r0, r1, device).float().cpu().numpy()
+
+
+def oracle_parity(k: int, blocks, Q: np.ndarray, s_gpu, r_gpu, n_par: int, what: str):
+    """n_par evenly spaced queries of the batch against the host float64 oracle streamed over
+    the catalog blocks (oracle.restatement.cosine_topk_stream): rows bit-exact, |ds| <= 1e-5."""
+    from oracle import restatement as R
     n_par = min(Q.shape[0], n_par)
     idx = np.unique(np.linspace(0, Q.shape[0] - 1, n_par).astype(np.int64))
     t0 = time.perf_counter()
-    ref_s, ref_r = R.cosine_topk_stream(Q[idx], host_blocks(cat_gpu, n_all), k + 1,
-                                        workers=min(8, max(1, hi["nproc"] // 2)))
+    ref_s, ref_r = R.cosine_topk_stream(Q[idx], blocks, k + 1,
+                                        workers=min(8, max(1, host_info()["nproc"] // 2)))
     t_par = time.perf_counter() - t0
     g_s = s_gpu[torch.from_numpy(idx).to(s_gpu.device)].cpu().numpy()
     g_r = r_gpu[torch.from_numpy(idx).to(r_gpu.device)].cpu().numpy()
@@ -183,11 +199,11 @@ def cpu_baseline_and_parity(cfg, cat_gpu: torch.Tensor, q_gpu: torch.Tensor, s_g
     parity = {"queries_checked": int(len(idx)), "rows_bit_exact": rows_equal,
               "max_abs_score_diff": max_diff, "tolerance": 1e-5,
               "oracle": "float64 restatement (oracle.restatement.cosine_topk_stream) over the "
-                        "full catalog, streamed in row blocks",
+                        + what,
               "sample": f"{len(idx)} evenly spaced queries of the batch",
               "boundary_risk_queries": int(np.sum(gap < 1e-6)),
               "min_k_gap": float(np.min(gap)), "seconds": round(t_par, 1)}
-    return base, parity
+    return parity
 
 
 def pmc_traffic(config: str, world: int):
@@ -372,6 +388,9 @@ def main() -> None:
                     help="(N = 1) also check this many queries against torch float64 on the GPU")
     ap.add_argument("--n", type=int, default=None, help="override catalog rows (experiments)")
     ap.add_argument("--b", type=int, default=None, help="override batch (experiments)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal on a one-GPU box: every rank on GPU 0, gloo instead of RCCL "
+                         "(checks the multi-process sharded path and its parity; not scaling)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.n:
@@ -394,10 +413,15 @@ def main() -> None:
     if args.dry_run:
         return dry_run(args, world, rank)
     dist = None
+    if args.share_gpu:
+        local_rank = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.share_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         if dist.get_world_size() != args.gpus:
             log(f"error: RCCL process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
             sys.exit(3)
@@ -503,7 +527,8 @@ def main() -> None:
             "value": round(value, 3),
             "unit": "queries/s",
             "n_gpus": world,
-            "rccl_world_size": dist.get_world_size() if dist is not None else 1,
+            "rccl_world_size": (dist.get_world_size() if dist is not None and not args.share_gpu
+                                else (1 if dist is None else 0)),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3),
@@ -517,7 +542,8 @@ def main() -> None:
                             f"batch={cfg['b']}, top-{k}",
                 "n_items": cfg["n"], "d": cfg["d"], "catalog_dtype": cfg["dtype"], "batch": cfg["b"],
                 "k": k, "parallelism": f"catalog row-sharded x{world}" +
-                (", RCCL all-gather of per-shard top-k + merge" if world > 1 else ""),
+                ((", gloo" if args.share_gpu else ", RCCL") +
+                 " all-gather of per-shard top-k + merge" if world > 1 else ""),
                 "arith": "f16/bf16 MFMA screen (f32 acc) + exact f64 rescore of certified candidates",
             },
             "roofline": {
@@ -547,6 +573,17 @@ def main() -> None:
             out["parity"] = parity
         else:
             out["cpu_baseline"] = None
+            if world > 1 and not args.no_cpu_baseline:
+                # N > 1: the merged global top-k of the last timed batch against the host oracle
+                # over the whole catalog, regenerated block by block on rank 0's GPU
+                log("parity: regenerating the global catalog on rank 0 for the host oracle")
+                out["parity"] = oracle_parity(
+                    k, global_blocks(cfg, dev), q.to(torch.float64).cpu().numpy(), s, r,
+                    args.parity or 32, "whole global catalog (every shard), regenerated "
+                    "from its seeds on rank 0 and streamed in row blocks")
+        if args.share_gpu and world > 1:
+            out["rehearsal"] = (f"{world} ranks sharing GPU 0 over gloo: the multi-process "
+                                "sharded path end to end, NOT a scaling measurement")
         if world == 1 and args.device_check > 0:
             out["device_parity"] = device_f64_check(emb, q, s, r, args.device_check)
         print(json.dumps(out), flush=True)
