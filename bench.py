@@ -388,6 +388,8 @@ def main() -> None:
                     help="(N = 1) also check this many queries against torch float64 on the GPU")
     ap.add_argument("--n", type=int, default=None, help="override catalog rows (experiments)")
     ap.add_argument("--b", type=int, default=None, help="override batch (experiments)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="(N = 1) HIP streams the consecutive batches alternate over")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal on a one-GPU box: every rank on GPU 0, gloo instead of RCCL "
                          "(checks the multi-process sharded path and its parity; not scaling)")
@@ -453,13 +455,20 @@ def main() -> None:
     def finish(p):
         return ebt.score_topk_finish(p)
 
+    # --streams S (N = 1): consecutive batches go to S HIP streams in turn, so that the next
+    # batch's query prep and sample GEMM can start on CUs the current batch's last GEMM round,
+    # merge and rescore leave idle (each batch keeps its own workspace and outputs)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
+                                                  for _ in range(max(1, args.streams) - 1)]
+
     def run_steps(n, log_every=0):
         if world > 1:
             return run_sharded_steps(
                 lambda: score_topk_sharded_local_stages(cat, k, queries=q, timer=timer), n)
         pending, out = None, None
         for i in range(n):
-            p = submit()
+            with torch.cuda.stream(streams[i % len(streams)]):
+                p = submit()
             if pending is not None:
                 out = finish(pending)
             pending = p
