@@ -640,15 +640,22 @@ __device__ void wave_topk_write(const uint64_t (&x)[WTOP_E], int kprime, int k, 
                                 int64_t* oi, int lane, uint32_t key_lo) {
   uint32_t kx[WTOP_E];
   int nvalid = 0;
-  uint32_t kmax = 0u;
+  uint32_t kmax = 0u, kmin = 0xffffffffu;  // over the valid entries
 #pragma unroll
   for (int j = 0; j < WTOP_E; ++j) {
     kx[j] = (uint32_t)(x[j] >> 32);
     nvalid += __popcll(__ballot(x[j] != 0ull));
     kmax = max(kmax, kx[j]);
+    if (x[j] != 0ull) kmin = min(kmin, kx[j]);
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+  for (int o = 32; o > 0; o >>= 1) {
+    kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+    kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o, 64));
+  }
+  // every valid entry has key >= kmin, so count(key >= kmin) = nvalid >= want: a valid lower
+  // end for the first bisection, ~8 steps shorter than 1 when the list started empty
+  key_lo = key_lo > kmin ? key_lo : kmin;
   const int want = nvalid < kprime ? nvalid : kprime;
   const uint64_t below = (1ull << lane) - 1ull;
   if (want > 0) {
@@ -725,11 +732,18 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
       return lo < ehi && er[lo] == gr;
     };
     key_lo = f2key(fv[b * kprime + kprime - 1]);
-    // the list: U[0..kprime)
-    for (int i = lane; i < kprime; i += 64) {
-      const uint32_t key = f2key(fv[b * kprime + i]);
-      const int64_t ix = fi[b * kprime + i];
-      U[i] = (key != 0u && ix >= 0) ? (((uint64_t)key << 32) | (uint64_t)(~(uint32_t)ix)) : 0ull;
+    // the list (U[0..kprime) below) and the hit counts are loaded together, before any of
+    // them is used: one memory round trip instead of one per 64 list entries
+    constexpr int LPL = WMERGE_K / 64;
+    float lv[LPL];
+    int64_t li[LPL];
+#pragma unroll
+    for (int u = 0; u < LPL; ++u) {
+      const int i = lane + 64 * u;
+      if (64 * u < kprime) {  // uniform
+        lv[u] = i < kprime ? fv[b * kprime + i] : -__builtin_inff();
+        li[u] = i < kprime ? fi[b * kprime + i] : -1;
+      }
     }
     // the hits: U[kprime..), lane l owning groups [l*per, (l+1)*per), per a multiple of 16 so
     // its counts arrive as up to WCNT independent 16-byte loads (ld_counts is a multiple of 16)
@@ -743,6 +757,15 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
     for (int v = 0; v < WCNT; ++v) {
       const int g = g0 + 16 * v;
       cv4[v] = (v < nv && g < n_groups) ? *(const uint4*)(cr + g) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < LPL; ++u) {
+      const int i = lane + 64 * u;
+      if (64 * u < kprime && i < kprime) {
+        const uint32_t key = f2key(lv[u]);
+        U[i] = (key != 0u && li[u] >= 0)
+                   ? (((uint64_t)key << 32) | (uint64_t)(~(uint32_t)li[u])) : 0ull;
+      }
     }
     auto cnt_at = [&](int v, int e) -> int {  // count of group g0 + 16 v + e (0 past the end)
       const uint32_t w4 = e < 4 ? cv4[v].x : e < 8 ? cv4[v].y : e < 12 ? cv4[v].z : cv4[v].w;
@@ -788,17 +811,18 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
     const int mh = kprime + m < WTOP_N ? m : WTOP_N - kprime;
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    for (int h0 = 0; h0 < mh; h0 += 4 * 64) {
-      uint64_t comp[4];
+    {  // every hit load issued before the first is used (mh <= WTOP_N: WTOP_E per lane)
+      uint64_t comp[WTOP_E];
 #pragma unroll
-      for (int u4 = 0; u4 < 4; ++u4) {
-        const int h = h0 + u4 * 64 + lane;
-        comp[u4] = h < mh ? cb[(int64_t)U[kprime + h]] : 0ull;
+      for (int u = 0; u < WTOP_E; ++u) {
+        const int h = u * 64 + lane;
+        if (u * 64 < mh) comp[u] = h < mh ? cb[(int64_t)U[kprime + h]] : 0ull;  // uniform if
       }
 #pragma unroll
-      for (int u4 = 0; u4 < 4; ++u4) {
-        const int h = h0 + u4 * 64 + lane;
-        if (h < mh) U[kprime + h] = (ehi > elo && excluded(comp[u4])) ? 0ull : comp[u4];
+      for (int u = 0; u < WTOP_E; ++u) {
+        const int h = u * 64 + lane;
+        if (u * 64 < mh && h < mh)
+          U[kprime + h] = (ehi > elo && excluded(comp[u])) ? 0ull : comp[u];
       }
     }
     const int used = kprime + m < WTOP_N ? kprime + m : WTOP_N;
