@@ -471,9 +471,10 @@ int ebt_cosine_topk_submit(const ebt_catalog* cat, const void* q, int q_dtype, i
   }
   if (rc) return rc;
   // the exclusion check's flag sits right after the certificates: one copy brings both
-  rc = hip_check(hipMemsetAsync(cert + B, 0, 4, st), "hipMemsetAsync");
-  if (rc) return rc;
+  // (without exclusions the flag is neither set nor read)
   if (excl_off) {
+    rc = hip_check(hipMemsetAsync(cert + B, 0, 4, st), "hipMemsetAsync");
+    if (rc) return rc;
     hipLaunchKernelGGL(csr_sorted_kernel, dim3((unsigned)B), dim3(256), 0, st, excl_off,
                        excl_rows, cert + B);
     rc = launch_check("csr_sorted_kernel");
@@ -531,7 +532,7 @@ int ebt_cosine_topk_finish(ebt_pending* p) {
     set_error("ebt_cosine_topk_finish: bad pending batch");
     return EBT_EINVAL;
   }
-  if (p->cert_host[B] != 0) {
+  if (p->excl_off && p->cert_host[B] != 0) {
     set_error("ebt_cosine_topk: exclusion rows must be sorted ascending within each query");
     return EBT_EINVAL;
   }
