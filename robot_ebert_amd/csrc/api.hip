@@ -71,7 +71,8 @@ int merge_block_capacity(int);
 int64_t merge_wave_max_groups();
 int merge_segment_wave(float*, int64_t*, int64_t, int, int, const uint64_t*, int64_t, int,
                        const uint8_t*, int64_t, int64_t, int64_t, const int64_t*, const int64_t*,
-                       int*, hipStream_t);
+                       int*, hipStream_t, const float* veps = nullptr,
+                       const float* vspec = nullptr);
 int pilot_topk(const float*, int64_t, int64_t, int, int64_t, int, int, float*, int64_t*,
                hipStream_t);
 constexpr int64_t PILOT_ROWS = 1024;  // = WMERGE_H (select_topk.hip)
@@ -727,6 +728,7 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
     f_spread = f_spread < 2.5 ? 2.5 : f_spread;
   }
   int64_t r0 = 0;
+  bool verified = false;
   while (r0 < n_rows) {
     // expected hits <= 1 / f_spread of the merge's room beside the list. Hits per row: at
     // theta_spec H / n; after r0 rows the raised threshold (the list's k-th - 2 eps) keeps at
@@ -755,12 +757,16 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
                               counts, L.ld_counts, ovf, r0, st);
     }
     if (rc) return rc;
+    // the last wave merge also runs the final VERIFY of theta_spec (no separate launch)
+    const bool fuse_verify = wave && !given && r0 + seg == n_rows;
+    verified |= fuse_verify;
     {
       StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
       if (wave)
         rc = merge_segment_wave(fv, fi, B, kprime, k, cand, L.ld_cand, slots, counts,
                                 L.ld_counts, ceil_div(seg, L.group_rows), a.row_offset,
-                                a.excl_off, a.excl_rows, ovf, st);
+                                a.excl_off, a.excl_rows, ovf, st,
+                                fuse_verify ? a.eps : nullptr, fuse_verify ? tspec : nullptr);
       else  // sorted lists (the block merge sorts the union)
         rc = merge_segment(fv, fi, B, kprime, cand, L.ld_cand, slots, counts, L.ld_counts,
                            ceil_div(seg, L.group_rows), a.row_offset, a.excl_off, a.excl_rows,
@@ -771,7 +777,7 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
   }
   // a caller's threshold is verified by the caller against the catalog-wide floor (the local
   // list may hold fewer than k rows: most of the global top k live on other shards)
-  if (given) return EBT_OK;
+  if (given || verified) return EBT_OK;
   return spec_threshold(fv, kprime, B, B_pad, k, a.eps, tspec, nullptr, ovf, 1, st);
 }
 

@@ -636,8 +636,10 @@ __device__ __forceinline__ uint64_t wave_min_at_least(const uint64_t (&x)[WTOP_E
 
 // The k' largest of the wave's composites x (0 = empty), written partitioned at k (see above)
 // to ov/oi[0..kprime).
-__device__ void wave_topk_write(const uint64_t (&x)[WTOP_E], int kprime, int k, float* ov,
-                                int64_t* oi, int lane, uint32_t key_lo) {
+// Returns the value it wrote to position k-1 (uniform): the k-th best, -inf when fewer than k.
+__device__ float wave_topk_write(const uint64_t (&x)[WTOP_E], int kprime, int k, float* ov,
+                                 int64_t* oi, int lane, uint32_t key_lo) {
+  float kth = -__builtin_inff();
   uint32_t kx[WTOP_E];
   int nvalid = 0;
   uint32_t kmax = 0u, kmin = 0xffffffffu;  // over the valid entries
@@ -669,6 +671,7 @@ __device__ void wave_topk_write(const uint64_t (&x)[WTOP_E], int kprime, int k, 
       const uint64_t ck_cut = wave_cut(x, kx, kk, (uint32_t)(cw_cut >> 32), kmax);
       ck = wave_min_at_least(x, ck_cut);
     }
+    if (kk == k) kth = key2f((uint32_t)(ck >> 32));
     int na = 0, nb = kk;
 #pragma unroll
     for (int j = 0; j < WTOP_E; ++j) {
@@ -693,6 +696,18 @@ __device__ void wave_topk_write(const uint64_t (&x)[WTOP_E], int kprime, int k, 
     ov[i] = -__builtin_inff();
     oi[i] = -1;
   }
+  return kth;
+}
+
+// (double)kth - 2 eps rounded down to a float (the segment threshold / speculative check value)
+__device__ __forceinline__ float kth_minus_2eps_down(float kth, float eps) {
+  const double t = (double)kth - 2.0 * (double)eps;
+  float f = (float)t;
+  if ((double)f > t && f == f && f != -__builtin_inff()) {  // one float step down
+    const uint32_t u = __float_as_uint(f);
+    f = f == 0.f ? -__uint_as_float(1u) : __uint_as_float(f > 0.f ? u - 1u : u + 1u);
+  }
+  return f;
 }
 
 template <bool DENSE>
@@ -702,7 +717,7 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
     const uint8_t* __restrict__ counts, int64_t ld_counts, int n_groups,
     const float* __restrict__ dense, int64_t ld_dense, int n_dense, int64_t idx_base,
     int64_t row_offset, const int64_t* __restrict__ eo, const int64_t* __restrict__ er,
-    int* __restrict__ ovf) {
+    int* __restrict__ ovf, const float* __restrict__ veps, const float* __restrict__ vspec) {
   __shared__ uint64_t stage[WMERGE_Q][WTOP_N];  // the union
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t b = (int64_t)blockIdx.x * WMERGE_Q + w;
@@ -836,8 +851,15 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
-  wave_topk_write(x, kprime, k, fv + b * kprime, fi + b * kprime, lane, key_lo);
-  if (__ballot(over) != 0ull && lane == 0) ovf[b] = 1;
+  const float kth = wave_topk_write(x, kprime, k, fv + b * kprime, fi + b * kprime, lane, key_lo);
+  const bool any_over = __ballot(over) != 0ull;
+  if (lane == 0) {
+    // vspec: the speculative screen's VERIFY on the final list (spec_threshold_kernel,
+    // SPEC_VERIFY) fused into the last merge: theta_spec > the k-th - 2 eps (rounded down), a
+    // NaN or fewer than k entries fail with 2, as the separate launch would set after the merge
+    if (vspec && !(vspec[b] <= kth_minus_2eps_down(kth, veps[b]))) ovf[b] = 2;
+    else if (any_over) ovf[b] = 1;
+  }
 }
 
 bool merge_wave_fits(int kprime) { return kprime <= WMERGE_K; }
@@ -849,7 +871,8 @@ int merge_wave_capacity() { return WTOP_N; }
 int merge_segment_wave(float* fv, int64_t* fi, int64_t B, int kprime, int k, const uint64_t* cand,
                        int64_t ld_cand, int slots, const uint8_t* counts, int64_t ld_counts,
                        int64_t n_groups, int64_t row_offset, const int64_t* eo,
-                       const int64_t* er, int* ovf, hipStream_t st) {
+                       const int64_t* er, int* ovf, hipStream_t st, const float* veps,
+                       const float* vspec) {
   if (B < 0 || kprime < 1 || kprime > WMERGE_K || k < 1 || k > kprime || n_groups < 1 ||
       n_groups > 64 * 16 * WCNT ||
       ld_counts < n_groups || ld_counts % 16 != 0 || ((uintptr_t)counts & 15) ||
@@ -860,7 +883,7 @@ int merge_segment_wave(float* fv, int64_t* fi, int64_t B, int kprime, int k, con
   if (B == 0) return EBT_OK;
   hipLaunchKernelGGL(merge_wave_kernel<false>, dim3((unsigned)ceil_div(B, WMERGE_Q)),
                      dim3(STHREADS), 0, st, fv, fi, B, kprime, k, cand, ld_cand, slots, counts, ld_counts, (int)n_groups, nullptr,
-                     0, 0, 0, row_offset, eo, er, ovf);
+                     0, 0, 0, row_offset, eo, er, ovf, veps, vspec);
   return launch_check("merge_wave_kernel");
 }
 
@@ -876,7 +899,7 @@ int pilot_topk(const float* S, int64_t ld_s, int64_t B, int n, int64_t idx_base,
   if (B == 0) return EBT_OK;
   hipLaunchKernelGGL(merge_wave_kernel<true>, dim3((unsigned)ceil_div(B, WMERGE_Q)),
                      dim3(STHREADS), 0, st, fv, fi, B, kprime, k, nullptr, 0, 1, nullptr, 0, 0, S, ld_s, n, idx_base, 0, nullptr,
-                     nullptr, nullptr);
+                     nullptr, nullptr, nullptr, nullptr);
   return launch_check("merge_wave_kernel");
 }
 
@@ -890,13 +913,7 @@ __global__ void kth_threshold_kernel(const float* __restrict__ vals, int64_t ld,
                                      float* __restrict__ thr) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b < B) {
-    const double t = (double)vals[b * ld + k - 1] - 2.0 * (double)eps[b];
-    float f = (float)t;
-    if ((double)f > t && f == f && f != -__builtin_inff()) {  // one float step down
-      const uint32_t u = __float_as_uint(f);
-      f = f == 0.f ? -__uint_as_float(1u) : __uint_as_float(f > 0.f ? u - 1u : u + 1u);
-    }
-    thr[b] = f;
+    thr[b] = kth_minus_2eps_down(vals[b * ld + k - 1], eps[b]);
   } else if (b < B_pad) {
     thr[b] = __builtin_inff();
   }
@@ -929,12 +946,7 @@ __global__ void spec_threshold_kernel(const float* __restrict__ vals, int64_t ld
     return;
   }
   if (b < B) {
-    const double t = (double)vals[b * ld + k - 1] - 2.0 * (double)eps[b];
-    float f = (float)t;
-    if ((double)f > t && f == f && f != -__builtin_inff()) {  // one float step down
-      const uint32_t u = __float_as_uint(f);
-      f = f == 0.f ? -__uint_as_float(1u) : __uint_as_float(f > 0.f ? u - 1u : u + 1u);
-    }
+    const float f = kth_minus_2eps_down(vals[b * ld + k - 1], eps[b]);
     const float s = thr_spec[b];
     if (mode == SPEC_RAISE) thr[b] = f > s ? f : s;  // NaN f keeps s
     else if (!(s <= f)) ovf[b] = 2;
