@@ -497,7 +497,6 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int bid = blockIdx.x;
   const int tid = threadIdx.x;
-  const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
   // ---- the workgroup's tiles: L = Lbeg + j, + n_x, ... < Lend ----
