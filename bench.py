@@ -105,8 +105,9 @@ def host_blocks(emb: torch.Tensor, rows: int, block: int = 1 << 17):
 BASE_ROWS_MAX = 1_000_000
 
 
-def cpu_baseline_and_parity(cfg, cat_gpu: torch.Tensor, q_gpu: torch.Tensor, s_gpu, r_gpu,
-                            budget_s: float, n_parity: int = 0):
+def cpu_baseline_and_parity(cfg, blocks, n_all: int, q_gpu: torch.Tensor, s_gpu, r_gpu,
+                            budget_s: float, n_parity: int = 0,
+                            what: str = "full catalog, streamed in row blocks"):
     """CPU baselines and the parity sample.
 
     (i)  reference-faithful, the value reported: the float64 oracle restatement of lib.py:51-55
@@ -117,14 +118,15 @@ def cpu_baseline_and_parity(cfg, cat_gpu: torch.Tensor, q_gpu: torch.Tensor, s_g
     Both on a bounded sample (about budget_s / 2 seconds each). Parity: n_parity evenly spaced
     queries (128 by default, 32 above BASE_ROWS_MAX rows) against the host float64 oracle over
     the FULL catalog, streamed from the device in row blocks (oracle.restatement.
-    cosine_topk_stream): rows bit-exact, |score diff| <= 1e-5."""
+    cosine_topk_stream): rows bit-exact, |score diff| <= 1e-5.
+    blocks(rows) yields (first row, host float32 block) over the first `rows` global rows: the
+    resident catalog at N = 1, the catalog regenerated from its seeds on rank 0 at N > 1."""
     import pandas as pd
     from oracle import restatement as R
-    n_all = cat_gpu.shape[0]
     rows = min(n_all, BASE_ROWS_MAX)
     scale = rows / n_all
     log(f"copying {rows} catalog rows to host (float64) for the CPU baselines")
-    C = np.concatenate([b for _, b in host_blocks(cat_gpu, rows)]).astype(np.float64)
+    C = np.concatenate([b for _, b in blocks(rows)]).astype(np.float64)
     Q = q_gpu.to(torch.float64).cpu().numpy()
     k = cfg["k"]
     threads = blas_threads()
@@ -168,15 +170,16 @@ def cpu_baseline_and_parity(cfg, cat_gpu: torch.Tensor, q_gpu: torch.Tensor, s_g
     # parity sample over the full catalog (>= 64 queries per config; 32 at
     # the multi-GPU-sized catalogs, where the host oracle streams 10M-50M rows)
     n_par = n_parity or (128 if n_all <= BASE_ROWS_MAX else 32)
-    return base, oracle_parity(k, host_blocks(cat_gpu, n_all), Q, s_gpu, r_gpu, n_par,
-                               "full catalog, streamed in row blocks")
+    return base, oracle_parity(k, blocks(n_all), Q, s_gpu, r_gpu, n_par, what)
 
 
-def global_blocks(cfg, device, block: int = 1 << 17):
-    """Row blocks of the WHOLE global catalog as host float32 arrays, regenerated on `device`
-    from the same seeds every rank's shard came from (N > 1: rank 0 holds only its shard)."""
-    for r0 in range(0, cfg["n"], block):
-        r1 = min(cfg["n"], r0 + block)
+def global_blocks(cfg, device, block: int = 1 << 17, rows: int = None):
+    """Row blocks of the first `rows` (default all) rows of the WHOLE global catalog as host
+    float32 arrays, regenerated on `device` from the same seeds every rank's shard came from
+    (N > 1: rank 0 holds only its shard)."""
+    n = cfg["n"] if rows is None else min(rows, cfg["n"])
+    for r0 in range(0, n, block):
+        r1 = min(n, r0 + block)
         yield r0, make_catalog_shard(cfg, r0, r1, device).float().cpu().numpy()
 
 
@@ -207,15 +210,19 @@ def oracle_parity(k: int, blocks, Q: np.ndarray, s_gpu, r_gpu, n_par: int, what:
 
 
 def pmc_traffic(config: str, world: int):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
-    (profiles/pmc_<config>.json, FETCH_SIZE*2 + WRITE_SIZE, gfx950 correction applied when it
-    was written by tools/pmc_summary.py); null when no summary exists for this config."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{config}_n{world}.json")
+    """(HBM bytes per launch of the dominant kernel, note) from the committed rocprofv3 PMC
+    summary (profiles/pmc_<config>_n<N>.json, FETCH_SIZE*2 + WRITE_SIZE, gfx950 correction
+    applied by tools/pmc_summary.py); (None, reason) when no summary exists for this config/N."""
+    name = f"pmc_{config}_n{world}.json"
+    path = os.path.join(ROOT, "profiles", name)
     try:
         with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            v = json.load(f).get("hbm_bytes_per_launch")
+        return v, f"profiles/{name}: separate --pmc FETCH_SIZE / WRITE_SIZE passes of this command"
     except (OSError, ValueError):
-        return None
+        why = ("no PMC summary for this config and N: rocprofv3 --pmc runs on the one-GPU box "
+               "only (one rank), the driver's multi-GPU runs are not profiled")
+        return None, why
 
 
 def device_f64_check(emb: torch.Tensor, q: torch.Tensor, s, r, nq: int, chunk: int = 1 << 18):
@@ -279,6 +286,24 @@ def host_boundary(cat, k, q, timer, steps=3):
                     "one step at a time (no overlap); never `value`"}
 
 
+def stage_breakdown(st: dict, ms_per_step: float, world: int) -> dict:
+    """The extra (untimed) step's per-stage GPU time against the timed steps' ms_per_step:
+    the sum of the recorded stages and the rest. The stages are disjoint regions of the launch
+    stream; the rest is GPU-idle time between them (host work, launch gaps) plus, at N = 1, the
+    query prep inside the C ABI (not bracketed there). The timed loop overlaps consecutive
+    batches (and at N > 1 their collectives), the extra step runs one batch alone, so the sum
+    can exceed ms_per_step."""
+    total = sum(v[0] for v in st.values())
+    return {"sum_ms": round(total, 4), "ms_per_step": round(ms_per_step, 4),
+            "rest_ms": round(ms_per_step - total, 4),
+            "stages": "gemm (sample / score GEMM), gemm_filter, merge_select (fused-list merges), "
+                      "rescore, select, mask; at N > 1 also prep, small (threshold, floor, "
+                      "certificate kernels), collective_wait (stream stalls on the all-gathers), "
+                      "shard_merge (ebt_merge_topk)",
+            "note": "one extra batch after the timed steps, run alone" +
+                    (", collectives not overlapped" if world > 1 else "")}
+
+
 def _free_port() -> int:
     import socket
     s = socket.socket()
@@ -288,13 +313,14 @@ def _free_port() -> int:
     return port
 
 
-def launch_ranks(n: int, argv) -> int:
+def launch_ranks(n: int, argv, budget_s: float, grace_s: float = 10.0) -> int:
     """`bench.py --gpus N` without an external launcher: start N child processes of this same
     script, one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (the
     environment torch.distributed.run would give them). Nothing here has touched the GPU: the
-    children are started, never exec'd into. Rank 0's stdout carries the JSON line; the exit
-    status is the first non-zero child status (the remaining ranks are then stopped, since they
-    would wait in a collective forever)."""
+    children are started, never exec'd into. Rank 0's stdout carries the JSON line. Fails fast:
+    the first non-zero child status stops the other ranks (they would wait in a collective), and
+    so does a run that outlives `budget_s` seconds of wall clock (exit status 124). Stopping =
+    SIGTERM to every rank's process group, SIGKILL after `grace_s`."""
     import signal
     import subprocess
     port = _free_port()
@@ -304,9 +330,26 @@ def launch_ranks(n: int, argv) -> int:
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
                                       env=env, start_new_session=True))
-    log(f"launched {n} ranks (pids {[p.pid for p in procs]}), rendezvous 127.0.0.1:{port}")
+    log(f"launched {n} ranks (pids {[p.pid for p in procs]}), rendezvous 127.0.0.1:{port}, "
+        f"wall-clock budget {budget_s:.0f} s")
+
+    def stop(live):
+        for sig, wait_s in ((signal.SIGTERM, grace_s), (signal.SIGKILL, grace_s)):
+            for q in live:
+                try:
+                    os.killpg(q.pid, sig)
+                except ProcessLookupError:
+                    pass
+            t_end = time.monotonic() + wait_s
+            while time.monotonic() < t_end and any(q.poll() is None for q in live):
+                time.sleep(0.1)
+            live = [q for q in live if q.poll() is None]
+            if not live:
+                return
+
     rc = 0
     live = list(procs)
+    t_stop = time.monotonic() + budget_s
     while live:
         for p in list(live):
             code = p.poll()
@@ -316,13 +359,43 @@ def launch_ranks(n: int, argv) -> int:
             if code != 0 and rc == 0:
                 rc = code
                 log(f"rank pid {p.pid} exited with {code}: stopping the other ranks")
-                for q in live:
-                    try:
-                        os.killpg(q.pid, signal.SIGTERM)
-                    except ProcessLookupError:
-                        pass
+                stop(live)
+                live = [q for q in live if q.poll() is None]
+        if live and time.monotonic() > t_stop:
+            log(f"error: the ranks are still running after the {budget_s:.0f} s budget "
+                f"(a collective that never completes?): stopping pids {[q.pid for q in live]}")
+            stop(live)
+            return 124
         time.sleep(0.2)
     return rc
+
+
+def init_group(backend: str, world: int, rank: int, timeout_s: float, device=None):
+    """init_process_group with a timeout (rendezvous and every collective after it: a rank that
+    never joins a collective makes the others fail with an error instead of hanging), then ONE
+    verified all-gather of the rank ids: every rank must see [0, 1, ..., world-1], else exit 4.
+    The gathered tensor lives on `device` (RCCL) or the CPU (gloo)."""
+    import datetime
+    import torch.distributed as dist
+    kw = {"timeout": datetime.timedelta(seconds=timeout_s)}
+    if device is not None:
+        kw["device_id"] = device
+    dist.init_process_group(backend, **kw)
+    if dist.get_world_size() != world:
+        log(f"error: the {backend} process group has {dist.get_world_size()} ranks, expected "
+            f"{world}")
+        sys.exit(3)
+    dev = device if device is not None else torch.device("cpu")
+    mine = torch.tensor([rank], dtype=torch.int64, device=dev)
+    got = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(got, mine)
+    ids = got.cpu().tolist()
+    if ids != list(range(world)):
+        log(f"error: rank {rank}: the rank-id all-gather over {backend} returned {ids}, "
+            f"expected {list(range(world))}")
+        sys.exit(4)
+    log(f"rank {rank}: {backend} group of {world} verified (rank-id all-gather {ids})")
+    return dist
 
 
 def dry_run(args, world: int, rank: int) -> None:
@@ -332,15 +405,19 @@ def dry_run(args, world: int, rank: int) -> None:
     the ranks that reported). CPU test coverage of the launcher (tests/test_bench_launch.py)."""
     import torch.distributed as dist
     if world > 1:
-        dist.init_process_group("gloo")
-        if dist.get_world_size() != args.gpus:
-            log(f"error: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
-            sys.exit(3)
+        init_group("gloo", world, rank, args.collective_timeout)
     got = [rank]
     t = torch.tensor([float(rank)])
+    calls = [0]
 
     def step():
         if world > 1:
+            calls[0] += 1
+            if rank == args.skip_collective_rank and calls[0] == 1:
+                # test hook: this rank leaves out one collective; the others must fail with the
+                # collective timeout, and the launcher must stop the job, instead of hanging
+                log(f"rank {rank}: skipping a collective (--skip-collective-rank)")
+                return t.clone()
             out = torch.empty(world)
             dist.all_gather_into_tensor(out, t)
             return out
@@ -393,6 +470,14 @@ def main() -> None:
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal on a one-GPU box: every rank on GPU 0, gloo instead of RCCL "
                          "(checks the multi-process sharded path and its parity; not scaling)")
+    ap.add_argument("--collective-timeout", type=float, default=300.0,
+                    help="seconds before a rendezvous or collective that never completes fails "
+                         "the rank (init_process_group timeout)")
+    ap.add_argument("--launch-timeout", type=float, default=1200.0,
+                    help="wall-clock budget of a self-launched N > 1 run; the ranks are stopped "
+                         "and the exit status is 124 when it is exceeded")
+    ap.add_argument("--skip-collective-rank", type=int, default=-1,
+                    help=argparse.SUPPRESS)   # --dry-run test hook (tests/test_bench_launch.py)
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.n:
@@ -405,7 +490,7 @@ def main() -> None:
         sys.exit(2)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # no external launcher: this process only starts the ranks (before any GPU call)
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -418,15 +503,12 @@ def main() -> None:
     if args.share_gpu:
         local_rank = 0
     if world > 1:
-        import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         if args.share_gpu:
-            dist.init_process_group("gloo")
+            dist = init_group("gloo", world, rank, args.collective_timeout)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        if dist.get_world_size() != args.gpus:
-            log(f"error: RCCL process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
-            sys.exit(3)
+            dist = init_group("nccl", world, rank, args.collective_timeout,
+                              torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
 
     import robot_ebert_amd as ebt
@@ -508,8 +590,8 @@ def main() -> None:
     timer.only()
     run_steps(1)
     torch.cuda.synchronize(dev)
-    st = {name: timer.query(name) for name in ("gemm", "gemm_filter", "mask", "select",
-                                               "merge_select", "rescore")}
+    from robot_ebert_amd._lib import STAGES
+    st = {name: timer.query(name) for name in STAGES}
     host = host_boundary(cat, k, q, timer) if world == 1 else None
     n_local = end - begin
     B, d = cfg["b"], cfg["d"]
@@ -528,6 +610,8 @@ def main() -> None:
     all_gemm_ms = st["gemm"][0] + st["gemm_filter"][0]   # the extra step
     all_tf = 2.0 * B * n_local * d / (all_gemm_ms * 1e-3) / 1e12 if all_gemm_ms else None
     value = cfg["b"] * args.steps / elapsed
+    traffic, traffic_note = pmc_traffic(args.config, world)
+    pl_ms = 1e3 * elapsed / args.steps
 
     out = None
     if rank == 0:
@@ -560,7 +644,7 @@ def main() -> None:
                 "achieved": round(achieved, 2) if achieved else None,
                 "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_F16_TFLOPS, 4) if achieved else None,
-                "traffic": pmc_traffic(args.config, world),
+                "traffic": traffic,
                 "per_launch": {"launches": dom_n, "avg_ms": round(dom_ms / max(dom_n, 1), 4),
                                "flops": dom_flops / max(dom_n, 1),
                                "flops_formula": "2*B*rows*d per launch (rows = the launch's segment "
@@ -573,23 +657,26 @@ def main() -> None:
             },
             "plan": pl,
             "stage_ms_per_step": {name: round(v[0], 4) for name, v in st.items()},
+            "stage_breakdown": stage_breakdown(st, pl_ms, world),
             "host_boundary": host,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            base, parity = cpu_baseline_and_parity(cfg, emb, q, s, r, args.cpu_budget,
-                                                   args.parity)
-            out["cpu_baseline"] = base
-            out["parity"] = parity
-        else:
+        out["roofline"]["traffic_note"] = traffic_note
+        if args.no_cpu_baseline:
             out["cpu_baseline"] = None
-            if world > 1 and not args.no_cpu_baseline:
-                # N > 1: the merged global top-k of the last timed batch against the host oracle
-                # over the whole catalog, regenerated block by block on rank 0's GPU
-                log("parity: regenerating the global catalog on rank 0 for the host oracle")
-                out["parity"] = oracle_parity(
-                    k, global_blocks(cfg, dev), q.to(torch.float64).cpu().numpy(), s, r,
-                    args.parity or 32, "whole global catalog (every shard), regenerated "
-                    "from its seeds on rank 0 and streamed in row blocks")
+        elif world == 1:
+            out["cpu_baseline"], out["parity"] = cpu_baseline_and_parity(
+                cfg, lambda rows: host_blocks(emb, rows), emb.shape[0], q, s, r,
+                args.cpu_budget, args.parity)
+        else:
+            # N > 1: rank 0 holds only its shard; the CPU baselines and the parity sample (the
+            # merged global top-k of the last timed batch) run over the WHOLE catalog,
+            # regenerated block by block from its seeds on rank 0's GPU
+            log("cpu baseline + parity: regenerating the global catalog on rank 0")
+            out["cpu_baseline"], out["parity"] = cpu_baseline_and_parity(
+                cfg, lambda rows: global_blocks(cfg, dev, rows=rows), cfg["n"], q, s, r,
+                args.cpu_budget, args.parity,
+                "whole global catalog (every shard), regenerated from its seeds on rank 0 and "
+                "streamed in row blocks")
         if args.share_gpu and world > 1:
             out["rehearsal"] = (f"{world} ranks sharing GPU 0 over gloo: the multi-process "
                                 "sharded path end to end, NOT a scaling measurement")

@@ -18,12 +18,19 @@
  *     enqueues work on that stream and returns; nothing synchronises except ebt_timer_query().
  *   - Return value: EBT_OK (0) or a negative EBT_E* code; the message of the last failure on the
  *     calling thread is available from ebt_last_error(). All entry points are reentrant: no
- *     mutable global state apart from the thread-local error string.
+ *     mutable global state apart from the thread-local error string and a per-device cache of
+ *     the compute-unit count (atomic; every writer stores the same value).
  *   - Row ids: catalog rows are addressed by their row number inside the (shard-local) matrix;
  *     results carry GLOBAL row ids = local row + row_offset (a catalog row-sharded over ranks).
  *   - Ordering of every top-k result: score descending, then row ascending. The reference's
  *     pandas sort is an unstable introsort (pandas core/sorting.py:436-441), so its tie order is
  *     unspecified; this is the deterministic order the build defines.
+ *   - Non-finite catalog rows: a row holding a NaN or an infinity has a NaN cosine against every
+ *     query; such a row is never a candidate on any path (the selects, merges, the filter
+ *     epilogue and the large-k sort all drop NaN scores), so it only shows as an empty NaN / -1
+ *     slot when k exceeds the remaining candidates. pandas would list it last with score NaN
+ *     (sort_values(na_position="last")); the reference's catalogs are finite ALS / embedding
+ *     factors, and no reference fixture holds a non-finite row (parity unpinned on this edge).
  */
 #ifndef EBERT_H_
 #define EBERT_H_
@@ -168,7 +175,7 @@ int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dt
                 const double* gnorm64, int64_t row_offset, const float* cand_vals,
                 const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
                 const double* t_floor, double* out_scores, int64_t* out_rows, int32_t* certified,
-                void* stream);
+                void* timer, void* stream);
 
 /* The fused screen's merge step: query b's candidate list (fv/fi[b*kprime + j], a PARTITIONED
  * list: see below; a sorted list, as ebt_select_topk leaves it, is one) and the hits
@@ -183,6 +190,17 @@ int ebt_merge_hits(float* fv, int64_t* fi, int64_t B, int32_t kprime, int32_t k,
                    const uint64_t* cand, int64_t ld_cand, int32_t slots, const uint8_t* counts,
                    int64_t ld_counts, int64_t n_groups, int64_t row_offset,
                    const int64_t* excl_off, const int64_t* excl_rows, int32_t* ovf, void* stream);
+
+/* Exclusion CSR order: the search entry points binary-search each exclusion segment and take
+ * it sorted ascending. ebt_sort_exclusions sorts every segment of a caller's CSR on the device:
+ * segment b = rows_in[off[b] .. off[b+1]) (ABSOLUTE positions, off[0] may be > 0), sorted into
+ * the same positions of rows_out; positions outside every segment are copied unchanged; rows_out
+ * may equal rows_in. nnz = the length of the rows array. Offsets are clamped into [0, nnz] before
+ * use (a malformed CSR is then rejected by the search entry's own check). Workspace: device,
+ * ebt_sort_exclusions_bytes(B, nnz) bytes (0 = invalid sizes: B < 1, nnz >= 2^31). */
+size_t ebt_sort_exclusions_bytes(int64_t B, int64_t nnz);
+int ebt_sort_exclusions(const int64_t* off, const int64_t* rows_in, int64_t* rows_out, int64_t B,
+                        int64_t nnz, void* workspace, size_t ws_bytes, void* stream);
 
 /* Merge R partial top-k lists (scores/rows [R][B][k], each sorted) into the global top-k per
  * query -- the post-all-gather step of a row-sharded catalog. k <= 4096, any R. */
@@ -434,22 +452,33 @@ int ebt_als_solve(const double* YtY, const float* Y, int32_t rank, int64_t n_dst
 
 /* ---- per-stage GPU timing (hipEvents recorded on the launch stream) -----------------------
  * Stages: 0 screening GEMM (score-writing), 1 exclusion mask, 2 chunk select, 3 candidate
- * select (across chunks / head + fused tail), 4 rescore, 5 fused screening GEMM (filtering).
+ * select (across chunks / head + fused tail), 4 rescore, 5 fused screening GEMM (filtering),
+ * and the caller-bracketed stages of a row-sharded step: 6 query prep, 7 merge of the gathered
+ * shard results, 8 stream stalls on collectives, 9 small per-batch kernels (thresholds, floors,
+ * certificate checks).
  * ebt_timer_query synchronises the recorded events and returns the total milliseconds and the
- * number of launches of `stage` since the last reset. Host pointers. */
+ * number of launches of `stage` since the last reset. Host pointers.
+ * ebt_timer_begin / ebt_timer_end bracket a caller's region of `stream` as one record of
+ * `stage` (at most one open region per stage; nothing is recorded for a masked stage). */
 #define EBT_STAGE_GEMM 0
 #define EBT_STAGE_MASK 1
 #define EBT_STAGE_SELECT 2
 #define EBT_STAGE_MERGE_SELECT 3
 #define EBT_STAGE_RESCORE 4
 #define EBT_STAGE_GEMM_FILTER 5
-#define EBT_NUM_STAGES 6
+#define EBT_STAGE_PREP 6
+#define EBT_STAGE_SHARD_MERGE 7
+#define EBT_STAGE_COLLECTIVE 8
+#define EBT_STAGE_SMALL 9
+#define EBT_NUM_STAGES 10
 void* ebt_timer_create(void);
 void ebt_timer_destroy(void* timer);
 int ebt_timer_reset(void* timer);
 /* Record only the stages whose bit (1 << EBT_STAGE_*) is set (default: all). */
 int ebt_timer_set_mask(void* timer, uint32_t stage_mask);
 int ebt_timer_query(void* timer, int stage, double* total_ms, int64_t* launches);
+int ebt_timer_begin(void* timer, int stage, void* stream);
+int ebt_timer_end(void* timer, int stage, void* stream);
 
 #ifdef __cplusplus
 }

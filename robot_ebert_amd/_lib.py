@@ -19,7 +19,8 @@ LIB_PATH = os.environ.get("EBERT_LIB", os.path.join(_HERE, "libebert.so"))
 EBT_F32, EBT_BF16, EBT_F16, EBT_F64 = 0, 1, 2, 3
 DTYPE_CODE = {torch.float32: EBT_F32, torch.bfloat16: EBT_BF16, torch.float16: EBT_F16,
               torch.float64: EBT_F64}
-STAGES = {"gemm": 0, "mask": 1, "select": 2, "merge_select": 3, "rescore": 4, "gemm_filter": 5}
+STAGES = {"gemm": 0, "mask": 1, "select": 2, "merge_select": 3, "rescore": 4, "gemm_filter": 5,
+          "prep": 6, "shard_merge": 7, "collective_wait": 8, "small": 9}
 EBT_FLAG_NO_FUSE = 1
 EBT_FLAG_EXACT = 2
 EBT_FLAG_THETA = 4
@@ -105,7 +106,9 @@ _SIGNATURES = {
     "ebt_select_topk": ([_VP, _VP, _I64, _I64, _I64, _I64, _I32, _I32, _VP, _VP, _I64, _VP],
                         _INT),
     "ebt_rescore": ([_VP, _I64, _I32, _VP, _INT, _I64, _VP, _I64, _VP, _VP, _I32, _I32, _I64, _VP,
-                     _VP, _VP, _VP, _VP, _VP], _INT),
+                     _VP, _VP, _VP, _VP, _VP, _VP], _INT),
+    "ebt_sort_exclusions_bytes": ([_I64, _I64], _SZ),
+    "ebt_sort_exclusions": ([_VP, _VP, _VP, _I64, _I64, _VP, _SZ, _VP], _INT),
     "ebt_merge_topk": ([_VP, _VP, _I32, _I64, _I32, _VP, _VP, _VP], _INT),
     "ebt_screen_exact": ([_VP, _I64, _I32, _VP, _INT, _I64, _VP, _I64, _VP, _I64, _VP], _INT),
     "ebt_cosine_topk_workspace": ([_I64, _I64, _I64, _I32, _I64, _INT], _SZ),
@@ -125,6 +128,8 @@ _SIGNATURES = {
     "ebt_timer_reset": ([_VP], _INT),
     "ebt_timer_set_mask": ([_VP, ctypes.c_uint32], _INT),
     "ebt_timer_query": ([_VP, _INT, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64)], _INT),
+    "ebt_timer_begin": ([_VP, _INT, _VP], _INT),
+    "ebt_timer_end": ([_VP, _INT, _VP], _INT),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -202,6 +207,11 @@ class Timer:
         call("ebt_timer_query", self._h, STAGES[stage], ctypes.byref(tot), ctypes.byref(n))
         return tot.value, n.value
 
+    def region(self, stage: str, device=None):
+        """Context manager: the work enqueued on the current stream inside the block is one
+        record of `stage` (ebt_timer_begin / ebt_timer_end)."""
+        return _Region(self, STAGES[stage], device)
+
     @property
     def handle(self) -> int:
         return self._h
@@ -213,3 +223,22 @@ class Timer:
         except Exception:
             pass
         self._h = None
+
+
+class _Region:
+    def __init__(self, timer: "Timer", stage: int, device) -> None:
+        self.t, self.stage, self.device = timer, stage, device
+
+    def __enter__(self):
+        call("ebt_timer_begin", self.t.handle, self.stage, stream_of(self.device))
+        return self
+
+    def __exit__(self, *exc):
+        call("ebt_timer_end", self.t.handle, self.stage, stream_of(self.device))
+        return False
+
+
+def region(timer: Optional["Timer"], stage: str, device=None):
+    """timer.region(stage) or a no-op when timer is None."""
+    import contextlib
+    return timer.region(stage, device) if timer is not None else contextlib.nullcontext()

@@ -109,6 +109,7 @@ struct Timer {
   std::vector<Rec> recs;
   std::mutex mu;
   uint32_t mask = 0xffffffffu;  // stages recorded (ebt_timer_set_mask)
+  std::vector<std::pair<int, hipEvent_t>> open;  // ebt_timer_begin without its _end yet
 
   hipEvent_t get() {
     if (used == pool.size()) {
@@ -494,7 +495,8 @@ int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dt
                 const double* gnorm64, int64_t row_offset, const float* cand_vals,
                 const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
                 const double* t_floor, double* out_scores, int64_t* out_rows, int32_t* certified,
-                void* stream) {
+                void* timer, void* stream) {
+  StageScope sc(timer, EBT_STAGE_RESCORE, (hipStream_t)stream);
   return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, cand_vals, cand_rows, kprime, k,
                  n_rows, eps, t_floor, out_scores, out_rows, certified, (hipStream_t)stream,
                  nullptr, 0);
@@ -1049,8 +1051,45 @@ int ebt_timer_reset(void* timer) {
   Timer* t = (Timer*)timer;
   std::lock_guard<std::mutex> g(t->mu);
   t->recs.clear();
+  t->open.clear();
   t->used = 0;
   return EBT_OK;
+}
+
+int ebt_timer_begin(void* timer, int stage, void* stream) {
+  if (!timer || stage < 0 || stage >= EBT_NUM_STAGES) return EBT_EINVAL;
+  Timer* t = (Timer*)timer;
+  std::lock_guard<std::mutex> g(t->mu);
+  if (!((t->mask >> stage) & 1u)) return EBT_OK;
+  for (auto& o : t->open)
+    if (o.first == stage) {
+      set_error("ebt_timer_begin: stage %d is already open", stage);
+      return EBT_EINVAL;
+    }
+  hipEvent_t a = t->get();
+  if (!a) return hip_check(hipErrorOutOfMemory, "hipEventCreate");
+  int rc = hip_check(hipEventRecord(a, (hipStream_t)stream), "hipEventRecord");
+  if (rc) return rc;
+  t->open.push_back({stage, a});
+  return EBT_OK;
+}
+
+int ebt_timer_end(void* timer, int stage, void* stream) {
+  if (!timer || stage < 0 || stage >= EBT_NUM_STAGES) return EBT_EINVAL;
+  Timer* t = (Timer*)timer;
+  std::lock_guard<std::mutex> g(t->mu);
+  for (size_t i = 0; i < t->open.size(); ++i) {
+    if (t->open[i].first != stage) continue;
+    hipEvent_t a = t->open[i].second;
+    t->open.erase(t->open.begin() + (long)i);
+    hipEvent_t b = t->get();
+    if (!b) return hip_check(hipErrorOutOfMemory, "hipEventCreate");
+    int rc = hip_check(hipEventRecord(b, (hipStream_t)stream), "hipEventRecord");
+    if (rc) return rc;
+    t->recs.push_back({stage, a, b});
+    return EBT_OK;
+  }
+  return EBT_OK;  // not open: the stage was masked at ebt_timer_begin
 }
 
 int ebt_timer_query(void* timer, int stage, double* total_ms, int64_t* launches) {

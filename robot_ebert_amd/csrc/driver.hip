@@ -619,6 +619,10 @@ int ebt_cosine_topk_finish(ebt_pending* p) {
       const PrepLayout& RP = L.prep_r;
       rc = hip_check(hipMemsetAsync(rprep + RP.qimg, 0, (size_t)m_pad * irow, st), "memset");
       if (!rc) rc = hip_check(hipMemsetAsync(rprep + RP.eps, 0, (size_t)m_pad * 4, st), "memset");
+      if (!rc)  // qscale = 1.0f (bits 0x3f800000), as ebt_query_image leaves padding rows
+        rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)(rprep + RP.qscale), 0x3f800000,
+                                         (size_t)m_pad, st),
+                       "memsetD32");
       if (!rc) rc = move_rows(prep + L.prep.q64, qrow, rprep + RP.q64, qrow, d_idx, m, qrow,
                               false, st);
       if (!rc) rc = move_rows(prep + L.prep.qimg, irow, rprep + RP.qimg, irow, d_idx, m, irow,

@@ -5,7 +5,10 @@
 //
 // Per group of Bg queries (float64 scores of Bg x n as 64-bit order keys, ~1 GiB at most):
 //   exact_keys_kernel  key[b][i] = order key of (q64_b . c_i) / gnorm64_i (the float64 FMA
-//                      tiling of the EXACT screen, rescore.hip); NaN scores sort as -inf
+//                      tiling of the EXACT screen, rescore.hip); a NaN score (a catalog row with
+//                      a NaN / inf element) gets key 0 and is dropped like an excluded row: the
+//                      convention of every other path of the library, whose selects never take
+//                      a NaN (include/ebert.h, "Non-finite catalog rows")
 //   mask_keys_kernel   the query's excluded rows (its CSR segment) -> key 0 (dropped)
 //   per query: hipcub DeviceRadixSort (keys descending, row ids as values; a radix sort is
 //              stable and the ids enter in ascending order, so ties keep row order: the
@@ -27,7 +30,7 @@ constexpr int64_t LARGE_GROUP_MAX = 64;
 size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 __device__ __forceinline__ uint64_t score_key(double v) {
-  if (v != v) v = -__builtin_inf();
+  if (v != v) return 0ull;  // NaN: not a candidate (the key of an excluded row)
   v += 0.0;  // -0 -> +0: one value, as they compare equal
   const uint64_t u = (uint64_t)__double_as_longlong(v);
   return (u >> 63) ? ~u : (u | 0x8000000000000000ull);

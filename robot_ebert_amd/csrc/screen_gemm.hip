@@ -20,6 +20,7 @@
 // Block order: XCD-bijective remap (blocks sharing an XCD get a contiguous logical range), then
 // groups of 8 (128-kernel) / 4 (256-kernel) catalog tiles walked query-tile-major, so a catalog
 // tile is fetched from HBM about once per XCD and re-read from L2 by the query tiles that use it.
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -1007,19 +1008,23 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
 // MI355X ("screening GEMM"): a 4-slot ring with k32 slices, one barrier per phase
 // with two barriers (qp), a persistent one-workgroup-per-CU walk of the same tiles, and a
 // 4-wave 128 x 128-per-wave tile (LDS-DMA issue cost with one wave per SIMD).
-// Compute units of the current device (the persistent grid size), cached per device.
+// Compute units of the current device (the persistent grid size), cached per device. The cache
+// is the library's only process-wide state: relaxed atomics (every writer stores the same value,
+// so concurrent first calls from the serving threads race on nothing).
 static int64_t n_cus() {
-  static int64_t cache[64] = {0};
+  static std::atomic<int64_t> cache[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cache[dev] == 0) {
+  int64_t v = cache[dev].load(std::memory_order_relaxed);
+  if (v == 0) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         cus <= 0)
       cus = 256;
-    cache[dev] = cus;
+    v = cus;
+    cache[dev].store(v, std::memory_order_relaxed);
   }
-  return cache[dev];
+  return v;
 }
 
 template <int EPI>

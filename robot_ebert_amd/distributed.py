@@ -31,7 +31,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from ._lib import EbertError, call, ptr, stream_of
+from ._lib import EbertError, call, ptr, region, stream_of
 from .catalog import Catalog
 from .search import (KPRIME_MAX, _round_up, csr_from_lists, csr_subset, default_kprime,
                      merge_topk, pad_batch, pool_kth, prepare_queries, run_screen,
@@ -218,13 +218,17 @@ def _gather_start(coll, t: torch.Tensor):
     return lambda: g
 
 
-def _gathered_floor(coll, vals: torch.Tensor, eps: torch.Tensor, k: int):
+def _gathered_floor(coll, vals: torch.Tensor, eps: torch.Tensor, k: int, timer=None):
     """union_floor over every shard's (k best approx, eps), in ONE all-gather ([B, k+1] f32);
     returns a future (the gather runs while the caller enqueues other work)."""
     wait = _gather_start(coll, torch.cat([vals, eps[:, None]], 1))
+    dev = vals.device
 
     def floor():
-        return union_floor_gathered(wait(), k)
+        with region(timer, "collective_wait", dev):
+            g = wait()
+        with region(timer, "small", dev):
+            return union_floor_gathered(g, k)
     return floor
 
 
@@ -253,7 +257,13 @@ def _shared_theta(coll, catalog: Catalog, qb, kprime: int, tiles: int, timer=Non
     instead of ~k' j / lambda of its own, and one filter launch covers it. Returns a future of
     (theta [B_pad], expected hits per query on this shard) or None (every rank alike)."""
     wait = _gather_start(coll, local_sample(catalog, qb, tiles, timer))   # [R, B, 4 tiles]
-    return lambda: theta_from_samples(wait(), qb, kprime, tiles, catalog.n_global, catalog.n)
+
+    def theta():
+        with region(timer, "collective_wait", catalog.device):
+            g = wait()
+        with region(timer, "small", catalog.device):
+            return theta_from_samples(g, qb, kprime, tiles, catalog.n_global, catalog.n)
+    return theta
 
 
 def local_sample(catalog: Catalog, qb, tiles: int, timer=None) -> torch.Tensor:
@@ -323,7 +333,7 @@ def score_topk_sharded_local_stages(catalog: Catalog, k: int,
     liked_arg = counts_t = hook = None
     if liked is not None:
         liked_arg, counts_t, hook = _liked_queries(catalog, liked, coll)
-    kw.setdefault("t_floor_hook", lambda v, e: _gathered_floor(coll, v, e, k))
+    kw.setdefault("t_floor_hook", lambda v, e: _gathered_floor(coll, v, e, k, kw.get("timer")))
     B = int(queries.shape[0]) if queries is not None else len(liked)
     tiles = shared_sample_tiles(catalog.n_global, coll.world, pad_batch(B)) \
         if shared_threshold and kw.get("fuse", True) else 0
@@ -353,7 +363,15 @@ def score_topk_sharded_local_finish_start(sub):
     pending, coll, k = sub
     s, r = score_topk_finish(pending)
     ws, wr = _gather_start(coll, s), _gather_start(coll, r)
-    return lambda: merge_topk(ws(), wr(), k)
+    timer = getattr(pending, "timer", None)
+    dev = s.device
+
+    def merge():
+        with region(timer, "collective_wait", dev):
+            gs, gr = ws(), wr()
+        with region(timer, "shard_merge", dev):
+            return merge_topk(gs, gr, k)
+    return merge
 
 
 def run_sharded_steps(make_stages, n: int):

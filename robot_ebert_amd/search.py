@@ -25,7 +25,7 @@ from typing import Optional, Sequence, Tuple, Union
 import torch
 
 from . import _lib
-from ._lib import DTYPE_CODE, EbertError, call, ptr, require_cuda, stream_of
+from ._lib import DTYPE_CODE, EbertError, call, ptr, region, require_cuda, stream_of
 from .catalog import Catalog
 
 KPRIME_MAX = 4096
@@ -85,20 +85,26 @@ def csr_from_lists(lists: Sequence[Sequence[int]], device) -> Tuple[torch.Tensor
 def csr_sorted(off: torch.Tensor, rows: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """A caller's device CSR with every segment sorted ascending (the fused merge drops excluded
     rows by binary search over the segment, so an unsorted segment would silently keep rated
-    rows). One torch.sort of (segment << 32 | row) keys; rows must lie in [0, 2^32)."""
+    rows): ebt_sort_exclusions, the library's own segmented sort. Offsets are absolute positions
+    into `rows` (off[0] may be > 0); positions outside every segment keep their value. Returns
+    (off, sorted copy of rows)."""
+    require_cuda(off, "exclusion offsets")
+    require_cuda(rows, "exclusion rows")
     if off.dtype != torch.int64 or rows.dtype != torch.int64:
         raise EbertError("exclusion CSR must be int64 (offsets, rows)")
+    off, rows = off.contiguous(), rows.contiguous()
     nnz = int(rows.numel())
     B = int(off.numel()) - 1
     if nnz <= 1 or B < 1:
         return off, rows
-    lens = off[1:] - off[:-1]
-    seg = torch.repeat_interleave(torch.arange(B, device=off.device), lens)
-    if seg.numel() != nnz:          # padded rows past off[-1] keep their place
-        seg = torch.cat([seg, torch.full((nnz - seg.numel(),), B, device=off.device,
-                                         dtype=torch.int64)])
-    key, _ = torch.sort((seg << 32) | (rows & 0xFFFFFFFF))
-    return off, key & 0xFFFFFFFF
+    need = _lib.load().ebt_sort_exclusions_bytes(B, nnz)
+    if need == 0:
+        raise EbertError(f"exclusion CSR of {B} segments / {nnz} rows cannot be sorted")
+    ws = torch.empty(need, dtype=torch.uint8, device=rows.device)
+    out = torch.empty_like(rows)
+    call("ebt_sort_exclusions", ptr(off), ptr(rows), ptr(out), B, nnz, ptr(ws), need,
+         stream_of(rows.device))
+    return off, out
 
 
 def csr_subset(off: torch.Tensor, rows: torch.Tensor, idx: torch.Tensor):
@@ -498,8 +504,9 @@ def score_topk_stages(catalog: Catalog, k: int, queries: Optional[torch.Tensor] 
                    else csr_sorted(*exclude))
     if theta_hook is not None and t_floor_hook is None:
         raise EbertError("theta_hook needs t_floor_hook (the threshold is verified against it)")
-    qb = prepare_queries(catalog, queries=queries, liked=liked, liked_counts=liked_counts,
-                         liked_sum_hook=liked_sum_hook)
+    with region(timer, "prep", dev):
+        qb = prepare_queries(catalog, queries=queries, liked=liked, liked_counts=liked_counts,
+                             liked_sum_hook=liked_sum_hook)
     n_cap = _round_up(catalog.n, 4)
     k_eff = min(k, catalog.n)
     if k_eff > KPRIME_MAX:
@@ -683,12 +690,13 @@ def _global_cut_stages(catalog: Catalog, qb: QueryBatch, k: int, k_req: int, kpr
     call("ebt_rescore", ptr(qb.q64), B, catalog.d, ptr(catalog.data), catalog.dtype_code,
          catalog.ld, ptr(catalog.gnorm), catalog.row_offset, ptr(lv), ptr(local.contiguous()),
          kprime, k, catalog.n, ptr(eps), ptr(t_floor), ptr(out_s), ptr(out_r), ptr(cert),
-         stream_of(dev))
+         timer.handle if timer is not None else None, stream_of(dev))
     # an overflowed fused list is rerun unfused (cert -1), unless a row is corrupt (-2); so is a
     # query whose shared threshold may have dropped a row of the global top k: every top-k row
     # has approx >= t_floor - eps, so theta <= t_floor - eps keeps them all
-    call("ebt_certify_cut", ptr(cert), ptr(ovf), ptr(th[0]) if use_theta else None,
-         ptr(t_floor), ptr(eps), B, stream_of(dev))
+    with region(timer, "small", dev):
+        call("ebt_certify_cut", ptr(cert), ptr(ovf), ptr(th[0]) if use_theta else None,
+             ptr(t_floor), ptr(eps), B, stream_of(dev))
     yield out_s, out_r, cert
 
 
@@ -722,5 +730,5 @@ def rescore_rows(catalog: Catalog, qb: QueryBatch, cand_rows: torch.Tensor
     cert = torch.empty(B, dtype=torch.int32, device=dev)
     call("ebt_rescore", ptr(qb.q64), B, catalog.d, ptr(catalog.data), catalog.dtype_code,
          catalog.ld, ptr(catalog.gnorm), catalog.row_offset, ptr(vals), ptr(local), m, m, catalog.n,
-         ptr(eps), None, ptr(out_s), ptr(out_r), ptr(cert), stream_of(dev))
+         ptr(eps), None, ptr(out_s), ptr(out_r), ptr(cert), None, stream_of(dev))
     return out_s, out_r

@@ -51,3 +51,42 @@ def test_bench_world_mismatch_fails():
     assert p.returncode != 0
     assert "WORLD_SIZE=2" in p.stderr
     assert _json_lines(p.stdout) == []
+
+
+def test_bench_skipped_collective_fails_fast():
+    """One rank leaves out a collective: the others fail with the collective timeout (the
+    init_process_group timeout, 5 s here), the launcher stops the job and exits non-zero with
+    a message -- well inside its own wall-clock budget, never hanging."""
+    import time
+    t0 = time.monotonic()
+    p = _run(["--gpus", "2", "--steps", "3", "--warmup", "1", "--dry-run",
+              "--skip-collective-rank", "1", "--collective-timeout", "5",
+              "--launch-timeout", "120"], timeout=150)
+    took = time.monotonic() - t0
+    assert p.returncode != 0, p.stdout
+    assert took < 90, took
+    assert "skipping a collective" in p.stderr
+    assert "stopping the other ranks" in p.stderr or "budget" in p.stderr, p.stderr[-2000:]
+    assert _json_lines(p.stdout) == []
+
+
+def test_bench_launch_budget_stops_hung_ranks():
+    """A rank that hangs past the launcher's wall-clock budget (collective timeout longer than
+    the budget): the launcher SIGTERMs every rank and exits 124."""
+    import time
+    t0 = time.monotonic()
+    p = _run(["--gpus", "2", "--steps", "3", "--warmup", "1", "--dry-run",
+              "--skip-collective-rank", "1", "--collective-timeout", "600",
+              "--launch-timeout", "15"], timeout=150)
+    took = time.monotonic() - t0
+    assert p.returncode == 124, (p.returncode, p.stderr[-2000:])
+    assert took < 60, took
+    assert "budget" in p.stderr
+
+
+def test_bench_group_init_verifies_rank_ids():
+    """The real run's group setup (init_group: timeout + a verified all-gather of the rank ids)
+    is what --dry-run uses; its log line names the verified ids."""
+    p = _run(["--gpus", "2", "--steps", "1", "--warmup", "0", "--dry-run"])
+    assert p.returncode == 0, p.stderr
+    assert "verified (rank-id all-gather [0, 1])" in p.stderr

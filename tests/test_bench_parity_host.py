@@ -54,3 +54,36 @@ def test_oracle_parity_accepts_exact_and_rejects_wrong():
     bad = bench.oracle_parity(CFG["k"], blocks(), q, torch.from_numpy(s),
                               torch.from_numpy(r_repl), CFG["b"], "test")
     assert not bad["rows_bit_exact"]
+
+
+def test_cpu_baseline_over_regenerated_global_catalog():
+    """N > 1: rank 0's cpu_baseline + parity run over the WHOLE catalog regenerated from its
+    seeds (global_blocks), not over its shard: the (i)/(ii) keys are there and the parity of the
+    oracle's own answer passes."""
+    cat = _whole().numpy().astype(np.float64)
+    q = torch.from_numpy(np.random.default_rng(6).standard_normal((CFG["b"], CFG["d"])))
+    s, r = R.cosine_topk(q.numpy(), cat, CFG["k"])
+    base, par = bench.cpu_baseline_and_parity(
+        CFG, lambda rows: bench.global_blocks(CFG, torch.device("cpu"), block=50_000, rows=rows),
+        CFG["n"], q, torch.from_numpy(s), torch.from_numpy(r), budget_s=0.2, n_parity=CFG["b"],
+        what="whole global catalog")
+    for key in ("value", "unit", "cores", "kind", "sample", "batched", "host"):
+        assert key in base, key
+    assert base["value"] > 0 and base["batched"]["value"] > 0 and base["kind"] == "port"
+    assert par["rows_bit_exact"] and par["queries_checked"] == CFG["b"]
+    assert par["oracle"].endswith("whole global catalog")
+
+
+def test_traffic_reason_and_stage_breakdown():
+    """The N > 1 line's roofline.traffic is null WITH a reason when no PMC summary exists for
+    that config/N; the stage breakdown sums the recorded stages and reports the rest."""
+    v, why = bench.pmc_traffic("C3", 8)
+    assert v is None and "PMC" in why
+    v1, note = bench.pmc_traffic("C3", 1)
+    assert v1 is not None and v1 > 0 and note.startswith("profiles/pmc_C3_n1.json")
+    st = {"gemm_filter": (1.0, 3), "rescore": (0.25, 1), "collective_wait": (0.05, 3)}
+    b = bench.stage_breakdown(st, 1.5, 8)
+    assert b["sum_ms"] == 1.3 and abs(b["rest_ms"] - 0.2) < 1e-9
+    from robot_ebert_amd._lib import STAGES
+    for name in ("rescore", "shard_merge", "collective_wait", "prep", "small"):
+        assert name in STAGES

@@ -844,7 +844,7 @@ def test_rescore_two_stage_cut(cuda_device, eps_v):
     cert = torch.empty(B, dtype=torch.int32, device=dev)
     L.call("ebt_rescore", L.ptr(qt), B, d, L.ptr(ct), L.DTYPE_CODE[torch.float64], d, L.ptr(gt),
            0, L.ptr(cvt), L.ptr(crt), kp, k, n, L.ptr(epst), None, L.ptr(out_s), L.ptr(out_r),
-           L.ptr(cert), L.stream_of(dev))
+           L.ptr(cert), None, L.stream_of(dev))
     torch.cuda.synchronize()
     s, r, c = out_s.cpu().numpy(), out_r.cpu().numpy(), cert.cpu().numpy()
     for b in range(B):
@@ -888,6 +888,104 @@ def test_unsorted_device_exclusions(cuda_device, dt):
     img = torch.ops.ebert.screen_image(cat.data, g)
     s2, r2 = torch.ops.ebert.cosine_topk(q, cat.data, g, inv, img, k, eo, er, 0)
     assert_topk_equal(s2, r2, s_ref, r_ref)
+
+
+def test_exclusion_csr_with_offset_start(cuda_device):
+    """a device CSR whose offsets start past 0 (a sub-batch slicing the offsets of a
+    larger CSR), with unsorted segments and foreign rows before off[0] and after off[-1]: the
+    library's segmented sort (ebt_sort_exclusions) sorts each segment in place by its ABSOLUTE
+    positions and leaves the rest alone, so every query excludes exactly its own rows."""
+    ebt, L = _ebt()
+    from robot_ebert_amd.search import csr_sorted
+    n, d, B, k = 40_000, 128, 256, 50
+    c = gaussian(35, n, d, "f32")
+    qv = gaussian(36, B, d, "f32")
+    s0, r0 = R.cosine_topk(qv, c, 120)
+    rng = np.random.default_rng(37)
+    excl = [rng.permutation(np.unique(np.concatenate([r0[b, rng.choice(120, 30, replace=False)],
+                                                      rng.choice(n, 20, replace=False)])))
+            for b in range(B)]
+    excl[5] = np.array([], dtype=np.int64)              # an empty segment
+    junk_head = r0[:7, 0]                               # top rows of other queries
+    junk_tail = r0[7:12, 0]
+    flat = np.concatenate([junk_head] + excl + [junk_tail]).astype(np.int64)
+    off = np.concatenate([[0], np.cumsum([len(e) for e in excl])]) + len(junk_head)
+    eo = torch.tensor(off, dtype=torch.int64, device=cuda_device)
+    er = torch.tensor(flat, dtype=torch.int64, device=cuda_device)
+    so, sr = csr_sorted(eo, er)
+    got = sr.cpu().numpy()
+    assert np.array_equal(got[:len(junk_head)], junk_head)
+    assert np.array_equal(got[off[-1]:], junk_tail)
+    for b in range(B):
+        assert np.array_equal(got[off[b]:off[b + 1]], np.sort(excl[b]))
+    assert torch.equal(er.cpu(), torch.tensor(flat))    # the caller's CSR is not modified
+    cat = ebt.Catalog(_t(c, "f32", cuda_device))
+    q = _t(qv, "f32", cuda_device)
+    s_ref, r_ref = R.cosine_topk(qv, c, k, excl)
+    s, r = ebt.score_topk(cat, k, queries=q, exclude=(eo, er))
+    assert_topk_equal(s, r, s_ref, r_ref)
+
+
+def test_sort_exclusions_entry(cuda_device):
+    """ebt_sort_exclusions through bare ctypes: in place (rows_out == rows_in), long segments
+    (beyond one workgroup), malformed offsets clamped (never read out of bounds)."""
+    ebt, L = _ebt()
+    rng = np.random.default_rng(38)
+    lens = [0, 1, 7, 5000, 300, 0, 70_000, 2]
+    rows = [rng.integers(-5, 1 << 40, size=m) for m in lens]
+    off = np.concatenate([[0], np.cumsum(lens)])
+    flat = np.concatenate(rows).astype(np.int64)
+    eo = torch.tensor(off, dtype=torch.int64, device=cuda_device)
+    er = torch.tensor(flat, dtype=torch.int64, device=cuda_device)
+    B, nnz = len(lens), len(flat)
+    need = L.load().ebt_sort_exclusions_bytes(B, nnz)
+    assert need > 0
+    ws = torch.empty(need, dtype=torch.uint8, device=cuda_device)
+    L.call("ebt_sort_exclusions", L.ptr(eo), L.ptr(er), L.ptr(er), B, nnz, L.ptr(ws), need,
+           L.stream_of(cuda_device))
+    got = er.cpu().numpy()
+    for b in range(B):
+        assert np.array_equal(got[off[b]:off[b + 1]], np.sort(rows[b]))
+    # offsets past nnz / decreasing: clamped, the call succeeds and stays in bounds
+    bad = torch.tensor([0, 10, 5, nnz + 100], dtype=torch.int64, device=cuda_device)
+    er2 = torch.tensor(flat, dtype=torch.int64, device=cuda_device)
+    need3 = L.load().ebt_sort_exclusions_bytes(3, nnz)
+    ws3 = torch.empty(need3, dtype=torch.uint8, device=cuda_device)
+    L.call("ebt_sort_exclusions", L.ptr(bad), L.ptr(er2), L.ptr(er2), 3, nnz, L.ptr(ws3), need3,
+           L.stream_of(cuda_device))
+    g2 = er2.cpu().numpy()
+    assert np.array_equal(g2[:10], np.sort(flat[:10]))
+    assert np.array_equal(g2[10:], np.sort(flat[10:]))   # [5, 10) is empty after the clamp
+    with pytest.raises(L.EbertError):
+        L.call("ebt_sort_exclusions", L.ptr(eo), L.ptr(er), L.ptr(er), B, nnz, L.ptr(ws), 16,
+               L.stream_of(cuda_device))
+
+
+@pytest.mark.parametrize("k", [20, 5999])
+def test_non_finite_catalog_rows_never_candidates(cuda_device, k):
+    """include/ebert.h "Non-finite catalog rows": a row with a NaN or an inf element scores NaN
+    against every query and is never returned, on the screen path (k = 20) and the large-k
+    full-sort path (k = 5999 > 4096, two slots left empty) alike; the rest keep the oracle order."""
+    ebt, L = _ebt()
+    n, d, B = 6000, 64, 4
+    rng = np.random.default_rng(39)
+    c = rng.standard_normal((n, d))
+    q = rng.standard_normal((B, d))
+    bad = [3, 1000, 4321]
+    c[3, 5] = np.nan
+    c[1000, 0] = np.inf
+    c[4321] = q[0] * 10          # would be query 0's best row
+    c[4321, 7] = np.nan
+    cat = ebt.Catalog(torch.tensor(c, dtype=torch.float64, device=cuda_device))
+    s, r = ebt.score_topk(cat, k, queries=torch.tensor(q, device=cuda_device))
+    sn, rn = s.cpu().numpy(), r.cpu().numpy()
+    good = np.setdiff1d(np.arange(n), bad)
+    s_ref, r_ref = R.cosine_topk(q, c[good], min(k, len(good)))
+    m = min(k, len(good))
+    assert np.array_equal(rn[:, :m], good[r_ref])
+    assert np.max(np.abs(sn[:, :m] - s_ref)) <= 1e-12
+    assert not np.isin(rn, bad).any()
+    assert np.all(rn[:, m:] == -1) and np.all(np.isnan(sn[:, m:]))
 
 
 @pytest.mark.parametrize("k", [10, 10000])

@@ -119,7 +119,7 @@ def main():
     def rs():
         L.call("ebt_rescore", L.ptr(qb.q64), B, d, L.ptr(emb), L.EBT_F32, d, L.ptr(cat.gnorm), 0,
                L.ptr(lv), L.ptr(lr), kp, k, n, L.ptr(eps), None, L.ptr(out_s), L.ptr(out_r),
-               L.ptr(cert), st)
+               L.ptr(cert), None, st)
     ms = timeit(rs, args.iters)
     # replay the two-stage cut: pass A gathers the list's first k rows; pass B the rest with
     # approx >= max(approx[k-1] - 2 eps, s_min - eps)
