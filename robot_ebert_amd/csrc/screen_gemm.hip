@@ -491,6 +491,14 @@ __device__ __forceinline__ QpArgsK qp_args() {
   return p;
 }
 
+#ifdef EBT_CLOCK_STAMP
+// Diagnostic build only (MI355X_MICROARCH.md "DVFS give-back" item 6): lane 0 of each workgroup
+// of a filter-mode launch records the shader-clock and the 100 MHz real-time counters after the
+// prologue and at exit into g_stamps[4 * blockIdx.x ..] (vector stores; nothing else reads them).
+// The in-kernel clock is d(clock) / d(real time) x 100 MHz. The shipped library has none of it.
+__device__ unsigned long long* g_stamps;
+#endif
+
 template <bool BF16, int EPI, bool ODD>
 __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs args) {
   (void)args;  // read through qp_args()
@@ -668,6 +676,13 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
   }
   wait_vm<8>();  // A0(0), B0(0), B1(0)
   qp_barrier();
+#ifdef EBT_CLOCK_STAMP
+  unsigned long long st_t0 = 0, st_r0 = 0;
+  if (EPI == EPI_FILTER && tid == 0) {
+    st_t0 = __builtin_amdgcn_s_memtime();
+    st_r0 = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 
   // One K-tile of four phases: P = buffer of this K-tile (compile time); (RC1, RQ1, K1): the tile
   // and local index of K-tile t+1 (its A1 is issued in Q1), (RC2, RQ2, K2): of K-tile t+2.
@@ -1000,7 +1015,25 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
 #undef QP2_KTILE
   // the last tile restaged its own first K-tiles: drain before the LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef EBT_CLOCK_STAMP
+  if (EPI == EPI_FILTER && tid == 0 && g_stamps) {
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* o = g_stamps + 4 * (int64_t)bid;
+    o[0] = st_t0;
+    o[1] = st_r0;
+    o[2] = t1;
+    o[3] = r1;
+  }
+#endif
 }
+
+#ifdef EBT_CLOCK_STAMP
+extern "C" int ebt_debug_clock_stamps(unsigned long long* buf) {
+  return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf)),
+                   "hipMemcpyToSymbol");
+}
+#endif
 
 
 // Kernel choice: batches padded to a multiple of 256 queries take the 256 x 256 quadrant-phase

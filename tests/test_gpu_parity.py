@@ -946,16 +946,22 @@ def test_sort_exclusions_entry(cuda_device):
     got = er.cpu().numpy()
     for b in range(B):
         assert np.array_equal(got[off[b]:off[b + 1]], np.sort(rows[b]))
-    # offsets past nnz / decreasing: clamped, the call succeeds and stays in bounds
+    # offsets past nnz / decreasing: clamped into [0, nnz], the call succeeds and stays in
+    # bounds (what the overlapping clamped segments hold afterwards is unspecified); the search
+    # entry then rejects the malformed CSR itself
     bad = torch.tensor([0, 10, 5, nnz + 100], dtype=torch.int64, device=cuda_device)
     er2 = torch.tensor(flat, dtype=torch.int64, device=cuda_device)
     need3 = L.load().ebt_sort_exclusions_bytes(3, nnz)
     ws3 = torch.empty(need3, dtype=torch.uint8, device=cuda_device)
     L.call("ebt_sort_exclusions", L.ptr(bad), L.ptr(er2), L.ptr(er2), 3, nnz, L.ptr(ws3), need3,
            L.stream_of(cuda_device))
-    g2 = er2.cpu().numpy()
-    assert np.array_equal(g2[:10], np.sort(flat[:10]))
-    assert np.array_equal(g2[10:], np.sort(flat[10:]))   # [5, 10) is empty after the clamp
+    torch.cuda.synchronize(cuda_device)
+    # (in bounds, but segment 1 runs backwards: every kernel reads an empty range there)
+    bad2 = torch.tensor([0, 10, 5, nnz], dtype=torch.int64, device=cuda_device)
+    cat = ebt.Catalog(torch.randn((5000, 64), device=cuda_device))
+    with pytest.raises(L.EbertError):
+        ebt.score_topk(cat, 10, queries=torch.randn((3, 64), device=cuda_device),
+                       exclude=(bad2, torch.zeros(nnz, dtype=torch.int64, device=cuda_device)))
     with pytest.raises(L.EbertError):
         L.call("ebt_sort_exclusions", L.ptr(eo), L.ptr(er), L.ptr(er), B, nnz, L.ptr(ws), 16,
                L.stream_of(cuda_device))

@@ -9,7 +9,7 @@ B=$R/_abl/build_$NAME
 mkdir -p $B
 CXX="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $FLAGS"
 pids=()
-for f in api screen_gemm select_topk prep rescore; do
+for f in $(cd $S && ls *.hip | sed "s/\.hip$//"); do
   $CXX -c $S/$f.hip -o $B/$f.o & pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p; done

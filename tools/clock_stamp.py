@@ -1,0 +1,111 @@
+"""In-kernel clock of the screening GEMM (MI355X_MICROARCH.md "DVFS give-back" item 6).
+
+    python tools/clock_stamp.py [--n 333334] [--b 4096] [--d 1536] [--secs 2.5]
+
+Loads the diagnostic build _abl/libebert_stamp.so (tools/abl_build.sh stamp -DEBT_CLOCK_STAMP):
+lane 0 of every workgroup of a filter-mode launch stamps the shader clock and the 100 MHz
+real-time counter after its prologue and at exit. After >= `secs` seconds of back-to-back
+launches of one C3 filter segment (4096 queries x n rows x 1536, f16 operands: the normalised
+rows of C3's screening image) it times 10 launches with hipEvents, then stamps one more: the
+in-kernel clock of a workgroup = d(clock) / d(real time) x 100 MHz; median / p10 / p90 over the
+workgroups. Modes: random operands at the C3 threshold (3 sigma of the cosine, ~0.13 % hits),
+random operands with no hits (threshold +inf: the main loop + the column test), and all-zero
+operands with no hits (the same instructions, the least switching energy). One JSON line per
+mode; the TFLOP/s a launch would reach at 2.4 GHz with the measured cycles is `tflops_at_2p4`.
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VP, I32, I64, INT = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=333_334)
+    ap.add_argument("--b", type=int, default=4096)
+    ap.add_argument("--d", type=int, default=1536)
+    ap.add_argument("--secs", type=float, default=2.5)
+    ap.add_argument("--lib", default=os.path.join(ROOT, "_abl", "libebert_stamp.so"))
+    a = ap.parse_args()
+    lib = ctypes.CDLL(a.lib)
+    f = lib.ebt_screen_filter
+    f.argtypes = [VP, I64, VP, I64, I32, I32, INT, VP, VP, VP, VP, I64, I32, VP, I64, VP, I64, VP]
+    f.restype = INT
+    lib.ebt_debug_clock_stamps.argtypes = [VP]
+    lib.ebt_debug_clock_stamps.restype = INT
+    lib.ebt_last_error.restype = ctypes.c_char_p
+    dev = torch.device("cuda:0")
+    B, N, d = a.b, a.n, a.d
+    g = torch.Generator(device=dev).manual_seed(0)
+    q = torch.randn((B, d), generator=g, device=dev)
+    q = (q / q.norm(dim=1, keepdim=True)).half()
+    c = torch.randn((N, d), generator=g, device=dev)
+    c = (c / c.norm(dim=1, keepdim=True)).half()
+    qs = torch.ones(B, device=dev)
+    G, slots = 256, 32
+    groups = (N + G - 1) // G
+    cand = torch.empty((B, groups * slots), dtype=torch.int64, device=dev)
+    counts = torch.empty((B, groups), dtype=torch.uint8, device=dev)
+    ovf = torch.zeros(B, dtype=torch.int32, device=dev)
+    stamps = torch.zeros(4 * 4096, dtype=torch.int64, device=dev)
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    zq, zc = torch.zeros_like(q), torch.zeros_like(c)
+    modes = [("random_c3_threshold", q, c, 3.0 / d ** 0.5),
+             ("random_no_hits", q, c, float("inf")),
+             ("zero_no_hits", zq, zc, float("inf"))]
+    fl = 2.0 * B * N * d
+    for name, qq, cc, t in modes:
+        thr = torch.full((B,), t, device=dev)
+
+        def launch():
+            rc = f(P(qq), B, P(cc), N, d, d, 2, P(qs), None, P(thr), P(cand), groups * slots,
+                   slots, P(counts), groups, P(ovf), 0, st)
+            if rc:
+                raise RuntimeError(lib.ebt_last_error().decode())
+        lib.ebt_debug_clock_stamps(None)
+        t0 = time.perf_counter()
+        n_warm = 0
+        while time.perf_counter() - t0 < a.secs:
+            for _ in range(10):
+                launch()
+            n_warm += 10
+            torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(10):
+            launch()
+        e.record()
+        stamps.zero_()
+        lib.ebt_debug_clock_stamps(P(stamps))
+        launch()
+        torch.cuda.synchronize()
+        lib.ebt_debug_clock_stamps(None)
+        ms = s.elapsed_time(e) / 10
+        v = stamps.view(-1, 4).cpu()
+        v = v[v[:, 3] > 0]
+        clk = [(int(r[2]) - int(r[0])) / max(1, int(r[3]) - int(r[1])) * 0.1 for r in v]
+        span = [(int(r[3]) - int(r[1])) / 1e5 for r in v]   # ms
+        clk.sort()
+        med = statistics.median(clk)
+        tf = fl / ms / 1e9
+        hits = float(counts.float().sum(1).mean()) if t != float("inf") else 0.0
+        print(json.dumps({
+            "mode": name, "shape": [B, N, d], "warm_launches": n_warm,
+            "launch_ms": round(ms, 4), "tflops": round(tf, 1), "frac_of_2500": round(tf / 2500, 4),
+            "clock_ghz_median": round(med, 3), "clock_ghz_p10": round(clk[len(clk) // 10], 3),
+            "clock_ghz_p90": round(clk[9 * len(clk) // 10], 3), "workgroups": len(clk),
+            "stamped_span_ms_median": round(statistics.median(span), 4),
+            "tflops_at_2p4": round(tf * 2.4 / med, 1), "hits_per_query": round(hits, 1)}),
+            flush=True)
+
+
+if __name__ == "__main__":
+    main()
