@@ -365,6 +365,49 @@ int ebt_cosine_topk_submit(const ebt_catalog* cat, const void* q, int q_dtype, i
                            void* timer, void* stream);
 int ebt_cosine_topk_finish(ebt_pending* pending);
 
+/* ---- row-sharded catalog, self-contained: one call per batch on every rank ---------------
+ * The per-shard protocol of robot_ebert_amd/distributed.py (score_topk_sharded_local_stages)
+ * inside the library, for a host without Python: every rank holds one shard (an ebt_catalog
+ * whose row_offset is the shard's first GLOBAL row) and calls ebt_cosine_topk_sharded with the
+ * same queries, k and exclusions; every rank returns the same GLOBAL top-k, equal to
+ * ebt_cosine_topk over the whole catalog (rows bit-exact, float64 scores). Per batch:
+ *   query prep (liked rows: each shard sums its own, one all-gather of the [B][d] float64
+ *   partial sums completes the means); when the shards are small (<= 200K rows, >= 2 ranks, the
+ *   fused screen) a catalog-wide screening threshold from every shard's sample maxima (one
+ *   all-gather); the shard's screen; the catalog-wide floor of the k-th exact score (one
+ *   all-gather of [B][k+1] float32) so each shard rescores only rows that can enter the global
+ *   top k; the float64 rescore + certificate; the local retries (no collective: every rank
+ *   issues the same all-gathers in the same order whatever its retries); two all-gathers of the
+ *   shard results ([B][k] float64 scores, int64 rows) and the merge (ebt_merge_topk).
+ * The caller supplies the collective, an all-gather over its communicator:
+ *   all_gather(ctx, send, recv, bytes, stream): recv (device, world * bytes) receives every
+ *   rank's `bytes` from send (device) in rank order. It is called after the work producing
+ *   `send` has been enqueued on `stream`, and the library enqueues work reading `recv` on
+ *   `stream` right after it returns: a stream-ordered collective (RCCL: ncclAllGather(send,
+ *   recv, bytes, ncclInt8, comm, stream)) or a blocking one both work.
+ *   It returns 0 on success; anything else fails the call with EBT_EHIP (the other ranks are
+ *   then left in their next all_gather: the caller's collective timeout must end them).
+ * Limits: k <= 4096 (the merge); B, k, the queries and the exclusions equal on every rank
+ * (argument errors are then detected alike everywhere before the first collective). The call
+ * returns when the results are final (the stream is synchronised once per retry round and at
+ * the end). Workspace: ebt_sharded_workspace_bytes (device). */
+typedef int (*ebt_allgather_fn)(void* ctx, const void* send, void* recv, size_t bytes,
+                                void* stream);
+typedef struct ebt_comm {
+  int32_t rank, world;
+  int64_t n_global;           /* rows of the whole catalog: every shard's row_offset + n <= it */
+  ebt_allgather_fn all_gather;
+  void* ctx;
+} ebt_comm;
+size_t ebt_sharded_workspace_bytes(const ebt_catalog* cat, const ebt_comm* comm, int64_t B,
+                                   int32_t k, const ebt_options* opt);
+int ebt_cosine_topk_sharded(const ebt_catalog* cat, const ebt_comm* comm, const void* q,
+                            int q_dtype, int64_t B, int64_t ldq, const int64_t* liked_off,
+                            const int64_t* liked_rows, int32_t k, const int64_t* excl_off,
+                            const int64_t* excl_rows, const ebt_options* opt, void* workspace,
+                            size_t ws_bytes, double* out_scores, int64_t* out_rows, void* timer,
+                            void* stream);
+
 /* ---- two-phase top-k over a row-sharded catalog (robot_ebert_amd/distributed.py) ---------
  * Phase 1, every rank: ebt_cosine_screen = ebt_cosine_topk_prepared without the rescore: the shard's k'
  * best approx candidates, list_vals (f32) / list_rows (GLOBAL, -1 empty) [B][kprime]

@@ -56,8 +56,18 @@ class EbtPending(ctypes.Structure):
                 ("event", _VP), ("timer", _VP), ("stream", _VP)]
 
 
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, _VP, _VP, _VP, _SZ, _VP)
+
+
+class EbtComm(ctypes.Structure):
+    """include/ebert.h `ebt_comm`: the caller's all-gather for ebt_cosine_topk_sharded."""
+    _fields_ = [("rank", _I32), ("world", _I32), ("n_global", _I64),
+                ("all_gather", ALLGATHER_FN), ("ctx", _VP)]
+
+
 _PCAT, _POPT, _PPEND = (ctypes.POINTER(EbtCatalog), ctypes.POINTER(EbtOptions),
                         ctypes.POINTER(EbtPending))
+_PCOMM = ctypes.POINTER(EbtComm)
 
 _SIGNATURES = {
     "ebt_catalog_state_bytes": ([_VP, _INT, _I64, _I32, _I64], _SZ),
@@ -68,6 +78,9 @@ _SIGNATURES = {
     "ebt_cosine_topk_submit": ([_PCAT, _VP, _INT, _I64, _I64, _VP, _VP, _I32, _VP, _VP, _POPT,
                                 _VP, _SZ, _VP, _VP, _VP, _PPEND, _VP, _VP], _INT),
     "ebt_cosine_topk_finish": ([_PPEND], _INT),
+    "ebt_sharded_workspace_bytes": ([_PCAT, _PCOMM, _I64, _I32, _POPT], _SZ),
+    "ebt_cosine_topk_sharded": ([_PCAT, _PCOMM, _VP, _INT, _I64, _I64, _VP, _VP, _I32, _VP, _VP,
+                                 _POPT, _VP, _SZ, _VP, _VP, _VP, _VP], _INT),
     "ebt_version": ([], _INT),
     "ebt_last_error": ([], ctypes.c_char_p),
     "ebt_row_norms": ([_VP, _INT, _I64, _I32, _I64, _VP, _VP, _VP], _INT),

@@ -38,7 +38,8 @@ int screen_image(const void*, int, int64_t, int32_t, int64_t, const double*, int
                  int32_t, hipStream_t);
 int query_dense(const void*, int, int64_t, int32_t, int64_t, double*, hipStream_t);
 int query_liked_sum(const void*, int, int32_t, int64_t, const double*, int64_t, const int64_t*,
-                    const int64_t*, double*, hipStream_t, int64_t row_offset = 0);
+                    const int64_t*, double*, hipStream_t, int64_t row_offset = 0,
+                    int64_t n_local = 0);
 int scale_rows_f64(double*, int64_t, int32_t, const double*, hipStream_t);
 int query_image(const double*, int64_t, int64_t, int32_t, int, const void*, int64_t, int, float,
                 void*, int32_t, float*, float*, hipStream_t);

@@ -23,7 +23,7 @@
 namespace ebt {
 
 int query_liked_sum(const void*, int, int32_t, int64_t, const double*, int64_t, const int64_t*,
-                    const int64_t*, double*, hipStream_t, int64_t row_offset);
+                    const int64_t*, double*, hipStream_t, int64_t row_offset, int64_t n_local);
 size_t large_topk_bytes(int64_t B, int64_t n, int64_t* Bg_out);
 int large_topk(const double*, int64_t, int32_t, const void*, int, int64_t, const double*, int64_t,
                int64_t, const int64_t*, const int64_t*, int32_t, double*, int64_t*, void*, size_t,
@@ -306,7 +306,7 @@ int prep_liked(const ebt_catalog& c, const int64_t* off, const int64_t* rows, in
   if (rc) return rc;
   double* q64 = (double*)(base + P.q64);
   rc = query_liked_sum(c.data, c.dtype, c.d, c.ld, c.gnorm64, B, off, rows, q64, st,
-                       c.row_offset);
+                       c.row_offset, 0);
   if (!rc) rc = ebt_scale_rows_f64(q64, B, c.d, d_scale, st);
   if (rc) return rc;
   return ebt_query_image(q64, B, pad_batch(B), c.d, c.img_dtype, nullptr, 0, 0, c.u_cat,
@@ -692,6 +692,445 @@ int ebt_cosine_topk(const ebt_catalog* cat, const void* q, int q_dtype, int64_t 
   if (rc) return rc;
   rc = ebt_cosine_topk_finish(&p);
   if (!rc) rc = hip_check(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
+  return rc;
+}
+
+}  // extern "C"
+
+// =========================================================== the row-sharded self-contained entry
+// ebt_cosine_topk_sharded (include/ebert.h): distributed.py's per-shard protocol
+// (score_topk_sharded_local_stages) in C++ over a caller-supplied all-gather. Reference:
+// /root/reference/src/backend/app/lib.py:51-55 restated on every shard; the merge of the shards'
+// exact top-k is the only thing the reference (one CPU process) has no counterpart for.
+namespace ebt {
+namespace {
+
+constexpr int SH_MERGE_WAVE_KMAX = 512;          // search.py MERGE_WAVE_KMAX
+constexpr int64_t SH_SHARED_MAX_SHARD_ROWS = 200000;  // distributed.py SHARED_MAX_SHARD_ROWS
+constexpr int64_t SH_SAMPLE_TILES_MAX = 64;
+constexpr int SH_K_MAX = 4096;                   // ebt_merge_topk
+
+// search.py spec_rank: the smallest j with P(Poisson(lam) >= j) <= 1e-6
+int sh_spec_rank(double lam) {
+  double pmf = exp(-lam), cdf = 0.0;
+  int j = 0;
+  while (j < 100000 && 1.0 - cdf > 1e-6) {
+    cdf += pmf;
+    pmf *= lam / (j + 1);
+    ++j;
+  }
+  return j > 1 ? j : 1;
+}
+
+// distributed.py shared_sample_tiles: 256-row sample tiles per shard for the catalog-wide
+// screening threshold (0 = every shard screens at its own); depends only on (n_global, world,
+// B_pad), so every rank decides alike
+int64_t sh_tiles(int64_t n_global, int world, int64_t B_pad) {
+  const int64_t shard = ceil_div(n_global, world);
+  if (world < 2 || B_pad % 256 != 0 || shard > SH_SHARED_MAX_SHARD_ROWS) return 0;
+  const int64_t full = shard / 256;
+  int64_t cap = ceil_div(SH_SAMPLE_TILES_MAX, world);
+  cap = cap > 4 ? cap : 4;
+  int64_t P = SH_SAMPLE_TILES_MAX < full / 24 ? SH_SAMPLE_TILES_MAX : full / 24;
+  P = P < cap ? P : cap;
+  const int64_t per = 256 / (B_pad / 256) > 1 ? 256 / (B_pad / 256) : 1;
+  if (P / per * per >= 8) P = P / per * per;
+  return (P >= 1 && world * P >= 8) ? P : 0;
+}
+
+struct ShardLayout {
+  DriverLayout D;
+  int64_t tiles, G, RG;
+  size_t screen_bytes;
+  size_t off_spass, off_pool, off_gsamp, off_perm, off_theta, off_lv, off_lr, off_lloc, off_ovf,
+      off_eps, off_fsend, off_frecv, off_tfloor, off_ls, off_lrr, off_gs, off_gr, off_scale,
+      off_qrecv, bytes;
+};
+
+bool shard_layout(const ebt_catalog& c, const ebt_comm& cm, int64_t B, int32_t k,
+                  const ebt_options& opt, ShardLayout* S) {
+  if (k < 1 || k > SH_K_MAX || cm.world < 1 || cm.rank < 0 || cm.rank >= cm.world ||
+      cm.n_global < c.row_offset + c.n || !cm.all_gather)
+    return false;
+  ShardLayout& L = *S;
+  L = ShardLayout{};
+  if (!driver_layout(c, B, k, opt, &L.D) || L.D.large) return false;
+  const DriverLayout& D = L.D;
+  const int64_t R = cm.world, kp = D.kprime;
+  // the shared threshold only serves the wave-merge screen (k' <= 512); decided from
+  // rank-invariant sizes (k against the WHOLE catalog), since its all-gather is a collective
+  const int64_t kg = k < cm.n_global ? k : cm.n_global;
+  int64_t kpg = opt.kprime ? round_up(opt.kprime, 4)
+                           : round_up(c.native ? kg + (kg / 4 > 16 ? kg / 4 : 16)
+                                               : (2 * kg > kg + 32 ? 2 * kg : kg + 32), 8);
+  L.tiles = (opt.flags & EBT_FLAG_NO_FUSE) || kpg > SH_MERGE_WAVE_KMAX
+                ? 0
+                : sh_tiles(cm.n_global, cm.world, D.B_pad);
+  L.G = 4 * L.tiles;
+  L.RG = R * L.G;
+  if (L.RG > 2048) L.tiles = L.G = L.RG = 0;  // ebt_pool_kth's limit (not reached: <= 8 x 32)
+  size_t scr = ebt_cosine_topk_workspace(B, D.B_pad, c.n, D.kprime, D.chunk, D.flags);
+  if (L.tiles) {
+    const size_t t = ebt_cosine_topk_workspace(B, D.B_pad, c.n, D.kprime, D.chunk, EBT_FLAG_THETA);
+    scr = t > scr ? t : scr;
+  }
+  if (scr == 0) return false;
+  L.screen_bytes = scr;
+  size_t o = al(D.bytes);
+  L.off_spass = D.off_pass;
+  if (scr > D.pass_bytes) {  // the first pass's screen needs more than the retries' region
+    L.off_spass = o;
+    o = al(o + scr);
+  }
+  L.off_pool = o;
+  o = al(o + (size_t)D.B_pad * L.G * 4);
+  L.off_gsamp = o;
+  o = al(o + (size_t)R * B * L.G * 4);
+  L.off_perm = o;
+  o = al(o + (size_t)B * L.RG * 4);
+  L.off_theta = o;
+  o = al(o + (size_t)D.B_pad * 4);
+  L.off_lv = o;
+  o = al(o + (size_t)B * kp * 4);
+  L.off_lr = o;
+  o = al(o + (size_t)B * kp * 8);
+  L.off_lloc = o;
+  o = al(o + (size_t)B * kp * 8);
+  L.off_ovf = o;
+  o = al(o + (size_t)B * 4);
+  L.off_eps = o;
+  o = al(o + (size_t)B * 4);
+  L.off_fsend = o;
+  o = al(o + (size_t)B * (k + 1) * 4);
+  L.off_frecv = o;
+  o = al(o + (size_t)R * B * (k + 1) * 4);
+  L.off_tfloor = o;
+  o = al(o + (size_t)B * 8);
+  L.off_ls = o;
+  o = al(o + (size_t)B * k * 8);
+  L.off_lrr = o;
+  o = al(o + (size_t)B * k * 8);
+  L.off_gs = o;
+  o = al(o + (size_t)R * B * k * 8);
+  L.off_gr = o;
+  o = al(o + (size_t)R * B * k * 8);
+  L.off_scale = o;
+  o = al(o + (size_t)B * 8);
+  L.off_qrecv = o;
+  o = al(o + (size_t)R * B * c.d * 8);  // the liked path's gathered partial sums
+  L.bytes = o;
+  return true;
+}
+
+// fsend[b][0 .. k_req] = the shard's k_eff best approx scores, -inf up to k_req, then eps[b]
+__global__ void floor_pack_kernel(const float* __restrict__ lv, int kp, int k_eff, int k_req,
+                                  const float* __restrict__ eps, int64_t B,
+                                  float* __restrict__ out) {
+  const int64_t total = B * (k_req + 1);
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = t / (k_req + 1);
+    const int j = (int)(t - b * (k_req + 1));
+    out[t] = j == k_req ? eps[b] : (j < k_eff ? lv[b * kp + j] : -__builtin_inff());
+  }
+}
+
+// GLOBAL candidate rows -> rows of this shard (-1 stays empty)
+__global__ void local_rows_kernel(const int64_t* __restrict__ g, int64_t n, int64_t off,
+                                  int64_t* __restrict__ out) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * blockDim.x)
+    out[t] = g[t] >= 0 ? g[t] - off : -1;
+}
+
+// gathered sample maxima [R][B][G] -> [B][R * G] (ebt_pool_kth's rows)
+__global__ void permute_samples_kernel(const float* __restrict__ g, int R, int64_t B, int G,
+                                       float* __restrict__ out) {
+  const int64_t total = (int64_t)R * B * G;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / (B * G), rem = t - r * B * G, b = rem / G, j = rem - b * G;
+    out[b * R * G + r * G + j] = g[t];
+  }
+}
+
+// out[t] = sum over ranks r (in rank order) of in[r * total + t]: the all-reduce of the liked
+// queries' partial sums, identical on every rank
+__global__ void sum_ranks_kernel(const double* __restrict__ in, int R, int64_t total,
+                                 double* __restrict__ out) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int r = 0; r < R; ++r) s += in[(int64_t)r * total + t];
+    out[t] = s;
+  }
+}
+
+unsigned grid_for(int64_t total) {
+  int64_t b = ceil_div(total, 256);
+  return (unsigned)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
+}
+
+int sh_gather(const ebt_comm& cm, const void* send, void* recv, size_t bytes, void* timer,
+              hipStream_t st) {
+  if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_COLLECTIVE, st);
+  const int rc = cm.all_gather(cm.ctx, send, recv, bytes, (void*)st);
+  if (timer) (void)ebt_timer_end(timer, EBT_STAGE_COLLECTIVE, st);
+  if (rc) {
+    set_error("ebt_cosine_topk_sharded: the caller's all_gather returned %d", rc);
+    return EBT_EHIP;
+  }
+  return EBT_OK;
+}
+
+// liked rows of a row-sharded catalog: GLOBAL rows, each shard sums its own, the partial sums
+// are all-gathered and added in rank order, then / L_b (lib.py:51-52)
+int prep_liked_sharded(const ebt_catalog& c, const ebt_comm& cm, const int64_t* off,
+                       const int64_t* rows, int64_t B, const PrepLayout& P, char* base,
+                       double* d_scale, double* qrecv, void* timer, hipStream_t st) {
+  std::vector<int64_t> h_off(B + 1);
+  int rc = hip_check(hipMemcpyAsync(h_off.data(), off, (B + 1) * 8, hipMemcpyDeviceToHost, st),
+                     "hipMemcpyAsync");
+  if (!rc) rc = hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+  if (rc) return rc;
+  std::vector<double> scale(B);
+  for (int64_t b = 0; b < B; ++b) {
+    const int64_t cnt = h_off[b + 1] - h_off[b];
+    if (cnt <= 0) {
+      set_error("Found array with 0 sample(s) (shape=(0, %d)) while a minimum of 1 is required "
+                "by check_pairwise_arrays.", c.d);
+      return EBT_EINVAL;
+    }
+    scale[b] = 1.0 / (double)cnt;
+  }
+  const int64_t nnz = h_off[B] - h_off[0];
+  if (nnz > 0) {
+    std::vector<int64_t> h_rows(nnz);
+    rc = hip_check(hipMemcpy(h_rows.data(), rows + h_off[0], nnz * 8, hipMemcpyDeviceToHost),
+                   "hipMemcpy");
+    if (rc) return rc;
+    for (int64_t r : h_rows)
+      if (r < 0 || r >= cm.n_global) {
+        set_error("liked row %lld is not in the catalog rows [0, %lld)", (long long)r,
+                  (long long)cm.n_global);
+        return EBT_EINVAL;
+      }
+  }
+  rc = hip_check(hipMemcpy(d_scale, scale.data(), B * 8, hipMemcpyHostToDevice), "hipMemcpy");
+  if (rc) return rc;
+  double* q64 = (double*)(base + P.q64);
+  rc = query_liked_sum(c.data, c.dtype, c.d, c.ld, c.gnorm64, B, off, rows, q64, st,
+                       c.row_offset, c.n);
+  if (!rc) rc = sh_gather(cm, q64, qrecv, (size_t)B * c.d * 8, timer, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(sum_ranks_kernel, dim3(grid_for(B * c.d)), dim3(256), 0, st, qrecv,
+                     (int)cm.world, B * c.d, q64);
+  rc = launch_check("sum_ranks_kernel");
+  if (!rc) rc = ebt_scale_rows_f64(q64, B, c.d, d_scale, st);
+  if (rc) return rc;
+  return ebt_query_image(q64, B, pad_batch(B), c.d, c.img_dtype, nullptr, 0, 0, c.u_cat,
+                         base + P.qimg, c.ld_img, (float*)(base + P.qscale),
+                         (float*)(base + P.eps), st);
+}
+
+}  // namespace
+}  // namespace ebt
+
+extern "C" {
+
+size_t ebt_sharded_workspace_bytes(const ebt_catalog* cat, const ebt_comm* comm, int64_t B,
+                                   int32_t k, const ebt_options* opt) {
+  if (!valid_catalog(cat) || !comm) return 0;
+  ShardLayout S;
+  if (!shard_layout(*cat, *comm, B, k, opt ? *opt : ebt_options{}, &S)) return 0;
+  return S.bytes;
+}
+
+int ebt_cosine_topk_sharded(const ebt_catalog* cat, const ebt_comm* comm, const void* q,
+                            int q_dtype, int64_t B, int64_t ldq, const int64_t* liked_off,
+                            const int64_t* liked_rows, int32_t k, const int64_t* excl_off,
+                            const int64_t* excl_rows, const ebt_options* opt, void* workspace,
+                            size_t ws_bytes, double* out_scores, int64_t* out_rows, void* timer,
+                            void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!valid_catalog(cat) || !comm || !workspace || !out_scores || !out_rows || B < 1 ||
+      k < 1 || ((q == nullptr) == (liked_off == nullptr)) || (liked_off && !liked_rows) ||
+      ((excl_off == nullptr) != (excl_rows == nullptr)) ||
+      (q && (q_dtype < 0 || q_dtype > 3 || ldq < cat->d))) {
+    set_error("ebt_cosine_topk_sharded: bad arguments (B=%lld k=%d; pass exactly one of q / "
+              "liked)", (long long)B, k);
+    return EBT_EINVAL;
+  }
+  const ebt_options o = opt ? *opt : ebt_options{};
+  ShardLayout S;
+  if (!shard_layout(*cat, *comm, B, k, o, &S)) {
+    set_error("ebt_cosine_topk_sharded: unsupported sizes, options or communicator (B=%lld "
+              "k=%d <= %d, n=%lld, row_offset=%lld, n_global=%lld, rank %d of %d)",
+              (long long)B, k, SH_K_MAX, (long long)cat->n, (long long)cat->row_offset,
+              (long long)comm->n_global, comm->rank, comm->world);
+    return EBT_EINVAL;
+  }
+  if (ws_bytes < S.bytes) {
+    set_error("ebt_cosine_topk_sharded: workspace %zu < %zu bytes "
+              "(ebt_sharded_workspace_bytes)", ws_bytes, S.bytes);
+    return EBT_ENOMEM;
+  }
+  const ebt_catalog& c = *cat;
+  const ebt_comm& cm = *comm;
+  const DriverLayout& L = S.D;
+  const int R = cm.world;
+  char* ws = (char*)workspace;
+  char* prep = ws + L.off_prep;
+  const double* q64 = (const double*)(prep + L.prep.q64);
+  const void* qimg = prep + L.prep.qimg;
+  const float* qscale = (const float*)(prep + L.prep.qscale);
+  const float* qeps = (const float*)(prep + L.prep.eps);
+  int rc = EBT_OK;
+  // 1. the queries (lib.py:51-52)
+  if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_PREP, st);
+  rc = q ? prep_dense(c, q, q_dtype, B, ldq, L.prep, prep, st)
+         : prep_liked_sharded(c, cm, liked_off, liked_rows, B, L.prep, prep,
+                              (double*)(ws + S.off_scale), (double*)(ws + S.off_qrecv), timer, st);
+  if (timer) (void)ebt_timer_end(timer, EBT_STAGE_PREP, st);
+  if (rc) return rc;
+  // 2. the catalog-wide screening threshold from every shard's sample maxima
+  float* theta = nullptr;
+  double hits = 0.0;
+  if (S.tiles) {
+    float* pool = (float*)(ws + S.off_pool);
+    float* gsamp = (float*)(ws + S.off_gsamp);
+    rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)pool, (int)0xff800000u,
+                                     (size_t)L.B_pad * S.G, st), "hipMemsetD32Async");
+    if (rc) return rc;
+    const int64_t own = S.tiles < c.n / 256 ? S.tiles : c.n / 256;
+    if (own >= 1) {
+      int64_t stride = (c.n / 256) / own;
+      if (stride > 1 && stride % 2 == 0) stride -= 1;
+      rc = ebt_cosine_sample(qimg, qscale, L.B_pad, c.image, c.cscale, c.img_dtype, c.ld_img,
+                             c.n, c.d_pad, own, stride, pool, S.G, timer, st);
+      if (rc) return rc;
+    }
+    rc = sh_gather(cm, pool, gsamp, (size_t)B * S.G * 4, timer, st);
+    if (rc) return rc;
+    const double m_total = 256.0 * (double)S.tiles * R;
+    const int j = sh_spec_rank((double)L.kprime * m_total / (double)cm.n_global);
+    if (j <= S.RG / 2) {
+      float* perm = (float*)(ws + S.off_perm);
+      theta = (float*)(ws + S.off_theta);
+      if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
+      hipLaunchKernelGGL(permute_samples_kernel, dim3(grid_for((int64_t)R * B * S.G)), dim3(256),
+                         0, st, gsamp, R, B, (int)S.G, perm);
+      rc = launch_check("permute_samples_kernel");
+      if (!rc) rc = ebt_pool_kth(perm, S.RG, B, L.B_pad, (int32_t)S.RG, j, theta, st);
+      if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
+      if (rc) return rc;
+      hits = ((double)j + (double)j * j / (2.0 * (double)S.RG)) * (double)c.n / m_total;
+    }
+  }
+  const bool use_theta = theta && L.flags == 0 && L.kprime <= SH_MERGE_WAVE_KMAX;
+  // 3. the shard's screen: its k' best approx candidates (GLOBAL rows)
+  float* lv = (float*)(ws + S.off_lv);
+  int64_t* lr = (int64_t*)(ws + S.off_lr);
+  int32_t* ovf = (int32_t*)(ws + S.off_ovf);
+  float* eps = (float*)(ws + S.off_eps);
+  if (use_theta)
+    rc = ebt_cosine_screen_at(q64, qimg, qscale, qeps, B, L.B_pad, c.data, c.dtype, c.ld,
+                              c.gnorm64, c.image, c.cscale, c.img_dtype, c.ld_img, c.n, c.d,
+                              c.d_pad, c.row_offset, excl_off, excl_rows, L.k_eff, L.kprime,
+                              L.chunk, 0, ws + S.off_spass, S.screen_bytes, lv, lr, ovf, eps,
+                              theta, hits, timer, st);
+  else
+    rc = ebt_cosine_screen(q64, qimg, qscale, qeps, B, L.B_pad, c.data, c.dtype, c.ld, c.gnorm64,
+                           c.image, c.cscale, c.img_dtype, c.ld_img, c.n, c.d, c.d_pad,
+                           c.row_offset, excl_off, excl_rows, L.k_eff, L.kprime, L.chunk,
+                           L.flags, ws + S.off_spass, S.screen_bytes, lv, lr, ovf, eps, timer,
+                           st);
+  if (rc) return rc;
+  // 4. the catalog-wide floor: the k-th largest (approx - eps) over every shard
+  float* fsend = (float*)(ws + S.off_fsend);
+  float* frecv = (float*)(ws + S.off_frecv);
+  double* tfloor = (double*)(ws + S.off_tfloor);
+  hipLaunchKernelGGL(floor_pack_kernel, dim3(grid_for(B * (k + 1))), dim3(256), 0, st, lv,
+                     L.kprime, L.k_eff, k, eps, B, fsend);
+  rc = launch_check("floor_pack_kernel");
+  if (!rc) rc = sh_gather(cm, fsend, frecv, (size_t)B * (k + 1) * 4, timer, st);
+  if (rc) return rc;
+  if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
+  rc = ebt_union_floor(frecv, R, B, k + 1, k, tfloor, st);
+  if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
+  if (rc) return rc;
+  // 5. the rescore of the rows that can enter the global top k, the certificate
+  int64_t* lloc = (int64_t*)(ws + S.off_lloc);
+  double* ls = (double*)(ws + S.off_ls);
+  int64_t* lrr = (int64_t*)(ws + S.off_lrr);
+  const bool padded = L.k_eff < k;
+  double* rs = padded ? (double*)(ws + L.off_res_s) : ls;
+  int64_t* rr = padded ? (int64_t*)(ws + L.off_res_r) : lrr;
+  int32_t* cert = (int32_t*)(ws + L.off_cert);
+  hipLaunchKernelGGL(local_rows_kernel, dim3(grid_for(B * L.kprime)), dim3(256), 0, st, lr,
+                     B * L.kprime, c.row_offset, lloc);
+  rc = launch_check("local_rows_kernel");
+  if (!rc)
+    rc = ebt_rescore(q64, B, c.d, c.data, c.dtype, c.ld, c.gnorm64, c.row_offset, lv, lloc,
+                     L.kprime, L.k_eff, c.n, eps, tfloor, rs, rr, cert, timer, st);
+  if (rc) return rc;
+  if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
+  rc = ebt_certify_cut(cert, ovf, use_theta ? theta : nullptr, tfloor, eps, B, st);
+  if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
+  if (rc) return rc;
+  if (excl_off) {
+    rc = hip_check(hipMemsetAsync(cert + B, 0, 4, st), "hipMemsetAsync");
+    if (rc) return rc;
+    hipLaunchKernelGGL(csr_sorted_kernel, dim3((unsigned)B), dim3(256), 0, st, excl_off,
+                       excl_rows, cert + B);
+    rc = launch_check("csr_sorted_kernel");
+    if (rc) return rc;
+  }
+  // the local retries (ebt_cosine_topk_finish: unfused reruns, k' x 4, the float64 screen) on
+  // this shard alone: a retried query gets the shard's exact top k, which the merge accepts
+  std::vector<int32_t> cert_host((size_t)B + 1);
+  rc = hip_check(hipMemcpyAsync(cert_host.data(), cert, (size_t)(B + 1) * 4,
+                                hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+  if (rc) return rc;
+  hipEvent_t ev;
+  rc = hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+  if (rc) return rc;
+  rc = hip_check(hipEventRecord(ev, st), "hipEventRecord");
+  if (rc) {
+    (void)hipEventDestroy(ev);
+    return rc;
+  }
+  ebt_pending P{};
+  P.cat = cat;
+  P.opt = o;
+  P.B = B;
+  P.B_pad = L.B_pad;
+  P.chunk = L.chunk;
+  P.k = k;
+  P.k_eff = L.k_eff;
+  P.kprime = L.kprime;
+  P.excl_off = excl_off;
+  P.excl_rows = excl_rows;
+  P.ws = ws;
+  P.ws_bytes = ws_bytes;
+  P.out_scores = ls;
+  P.out_rows = lrr;
+  P.cert_host = cert_host.data();
+  P.event = ev;
+  P.timer = timer;
+  P.stream = stream;
+  rc = ebt_cosine_topk_finish(&P);
+  if (rc) return rc;
+  // 6. every shard's exact top k, gathered and merged (the global answer on every rank)
+  double* gs = (double*)(ws + S.off_gs);
+  int64_t* gr = (int64_t*)(ws + S.off_gr);
+  rc = sh_gather(cm, ls, gs, (size_t)B * k * 8, timer, st);
+  if (!rc) rc = sh_gather(cm, lrr, gr, (size_t)B * k * 8, timer, st);
+  if (rc) return rc;
+  if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SHARD_MERGE, st);
+  rc = ebt_merge_topk(gs, gr, R, B, k, out_scores, out_rows, st);
+  if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SHARD_MERGE, st);
+  if (!rc) rc = hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
   return rc;
 }
 

@@ -193,13 +193,15 @@ int query_dense(const void* q, int dtype, int64_t B, int32_t d, int64_t ldq, dou
   return launch_check("query_dense_kernel");
 }
 
+// n_local > 0: rows outside [row_offset, row_offset + n_local) are skipped (a row-sharded
+// catalog: each shard sums its own liked rows; the caller adds the shards' partial sums)
 template <int DT>
 __global__ __launch_bounds__(256) void query_liked_kernel(const void* __restrict__ cat, int d,
                                                            int64_t ld,
                                                            const double* __restrict__ gnorm,
                                                            const int64_t* __restrict__ off,
                                                            const int64_t* __restrict__ rows,
-                                                           int64_t row_offset,
+                                                           int64_t row_offset, int64_t n_local,
                                                            double* __restrict__ q64) {
   const int64_t b = blockIdx.x;
   const int64_t l0 = off[b], l1 = off[b + 1];
@@ -207,6 +209,7 @@ __global__ __launch_bounds__(256) void query_liked_kernel(const void* __restrict
     double acc = 0.0;
     for (int64_t l = l0; l < l1; ++l) {
       const int64_t r = rows[l] - row_offset;
+      if (n_local > 0 && (r < 0 || r >= n_local)) continue;
       acc += load_as_f64<DT>(cat, r * ld + j) / gnorm[r];
     }
     q64[b * d + j] = acc;
@@ -217,7 +220,7 @@ __global__ __launch_bounds__(256) void query_liked_kernel(const void* __restrict
 // guarantees every row lies inside the catalog)
 int query_liked_sum(const void* cat, int dtype, int32_t d, int64_t ld, const double* gnorm,
                     int64_t B, const int64_t* off, const int64_t* rows, double* q64,
-                    hipStream_t st, int64_t row_offset) {
+                    hipStream_t st, int64_t row_offset, int64_t n_local) {
   if (!cat || !gnorm || !off || !q64 || B < 0 || d <= 0 || ld < d || dtype < 0 || dtype > 3) {
     set_error("ebt_query_liked_sum: bad arguments");
     return EBT_EINVAL;
@@ -225,10 +228,10 @@ int query_liked_sum(const void* cat, int dtype, int32_t d, int64_t ld, const dou
   if (B == 0) return EBT_OK;
   dim3 grid((unsigned)B), block(256);
   switch (dtype) {
-    case EBT_F32: hipLaunchKernelGGL(query_liked_kernel<EBT_F32>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, row_offset, q64); break;
-    case EBT_BF16: hipLaunchKernelGGL(query_liked_kernel<EBT_BF16>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, row_offset, q64); break;
-    case EBT_F16: hipLaunchKernelGGL(query_liked_kernel<EBT_F16>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, row_offset, q64); break;
-    default: hipLaunchKernelGGL(query_liked_kernel<EBT_F64>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, row_offset, q64); break;
+    case EBT_F32: hipLaunchKernelGGL(query_liked_kernel<EBT_F32>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, row_offset, n_local, q64); break;
+    case EBT_BF16: hipLaunchKernelGGL(query_liked_kernel<EBT_BF16>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, row_offset, n_local, q64); break;
+    case EBT_F16: hipLaunchKernelGGL(query_liked_kernel<EBT_F16>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, row_offset, n_local, q64); break;
+    default: hipLaunchKernelGGL(query_liked_kernel<EBT_F64>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, row_offset, n_local, q64); break;
   }
   return launch_check("query_liked_kernel");
 }

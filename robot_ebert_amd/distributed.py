@@ -33,8 +33,8 @@ import torch.distributed as dist
 from . import _lib
 from ._lib import EbertError, call, ptr, region, stream_of
 from .catalog import Catalog
-from .search import (KPRIME_MAX, _round_up, csr_from_lists, csr_subset, default_kprime,
-                     merge_topk, pad_batch, pool_kth, prepare_queries, run_screen,
+from .search import (KPRIME_MAX, MERGE_WAVE_KMAX, _round_up, csr_from_lists, csr_subset,
+                     default_kprime, merge_topk, pad_batch, pool_kth, prepare_queries, run_screen,
                      sample_maxima, score_topk, score_topk_finish, score_topk_stages,
                      score_topk_submit, spec_rank, union_floor_gathered)
 
@@ -335,8 +335,11 @@ def score_topk_sharded_local_stages(catalog: Catalog, k: int,
         liked_arg, counts_t, hook = _liked_queries(catalog, liked, coll)
     kw.setdefault("t_floor_hook", lambda v, e: _gathered_floor(coll, v, e, k, kw.get("timer")))
     B = int(queries.shape[0]) if queries is not None else len(liked)
+    # the shared threshold only serves the wave-merge screen (k' <= MERGE_WAVE_KMAX); decided
+    # from rank-invariant sizes (k against the whole catalog): its all-gather is a collective
+    kp_glob = kw.get("kprime") or default_kprime(catalog, min(k, catalog.n_global))
     tiles = shared_sample_tiles(catalog.n_global, coll.world, pad_batch(B)) \
-        if shared_threshold and kw.get("fuse", True) else 0
+        if shared_threshold and kw.get("fuse", True) and kp_glob <= MERGE_WAVE_KMAX else 0
     if tiles:
         timer = kw.get("timer")
         kw.setdefault("theta_hook", lambda qb, kp: _shared_theta(coll, catalog, qb, kp, tiles,

@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--d", type=int, default=1536)
     ap.add_argument("--secs", type=float, default=2.5)
     ap.add_argument("--lib", default=os.path.join(ROOT, "_abl", "libebert_stamp.so"))
+    ap.add_argument("--precision", action="store_true",
+                    help="instead: no-hit launches on operands of reduced mantissa width "
+                         "(energy per MFMA vs operand bits; bf16 and f16 images)")
     a = ap.parse_args()
     lib = ctypes.CDLL(a.lib)
     f = lib.ebt_screen_filter
@@ -58,15 +61,34 @@ def main():
     st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     zq, zc = torch.zeros_like(q), torch.zeros_like(c)
-    modes = [("random_c3_threshold", q, c, 3.0 / d ** 0.5),
-             ("random_no_hits", q, c, float("inf")),
-             ("zero_no_hits", zq, zc, float("inf"))]
+    modes = [("random_c3_threshold", q, c, 3.0 / d ** 0.5, 2),
+             ("random_no_hits", q, c, float("inf"), 2),
+             ("zero_no_hits", zq, zc, float("inf"), 2)]
+    if a.precision:
+        def trunc(x, bits, bf16=False):
+            """the same values with only `bits` explicit mantissa bits (truncated)"""
+            y = x.to(torch.bfloat16) if bf16 else x
+            keep = 7 if bf16 else 10
+            mask = ~((1 << (keep - bits)) - 1) & 0xFFFF
+            v = y.view(torch.int16).to(torch.int32) & mask
+            return v.to(torch.int16).view(y.dtype)
+        inf = float("inf")
+        qb, cb = q.to(torch.bfloat16), c.to(torch.bfloat16)
+        modes = [("f16_m10", q, c, inf, 2), ("bf16_m7", qb, cb, inf, 1),
+                 ("f16_m7", trunc(q, 7), trunc(c, 7), inf, 2),
+                 ("f16_m5", trunc(q, 5), trunc(c, 5), inf, 2),
+                 ("f16_m3", trunc(q, 3), trunc(c, 3), inf, 2),
+                 ("f16_cat_m7_query_m10", q, trunc(c, 7), inf, 2),
+                 ("f16_cat_m10_query_m7", trunc(q, 7), c, inf, 2),
+                 ("f16_cat_m5_query_m10", q, trunc(c, 5), inf, 2),
+                 ("bf16_m4", trunc(q, 4, True), trunc(c, 4, True), inf, 1),
+                 ("f16_m10_again", q, c, inf, 2)]
     fl = 2.0 * B * N * d
-    for name, qq, cc, t in modes:
+    for name, qq, cc, t, img_dt in modes:
         thr = torch.full((B,), t, device=dev)
 
         def launch():
-            rc = f(P(qq), B, P(cc), N, d, d, 2, P(qs), None, P(thr), P(cand), groups * slots,
+            rc = f(P(qq), B, P(cc), N, d, d, img_dt, P(qs), None, P(thr), P(cand), groups * slots,
                    slots, P(counts), groups, P(ovf), 0, st)
             if rc:
                 raise RuntimeError(lib.ebt_last_error().decode())
