@@ -212,7 +212,13 @@ static bool spec_params(int64_t B_pad, int64_t n_rows, int32_t kprime, int64_t* 
   // (C2: 64 tiles instead of 16 -> ~300 instead of ~565 hits per query, one filter launch)
   const int64_t fill = 256 / (B_pad / 256 > 0 ? B_pad / 256 : 1);
   if (P < fill && fill <= full / 6) P = fill;
-  P = P > 64 ? 64 : P;
+  // at most 64 tiles, or 1/200 of the rows of a large catalog (up to 512 tiles: 2048 pooled
+  // maxima, ebt_pool_kth's limit). A sample of m rows puts the k'-th best score near sample rank
+  // lambda = k' m / n, and the threshold at the j-th (j ~ lambda + 5 sqrt(lambda) + 6), so the
+  // hits per query ~ j n / m fall roughly as 1 / m while lambda is small: C5 (50M rows, k' = 1256)
+  // 64 -> 512 tiles takes ~21.6K hits per query to ~5.4K for 0.3 % more GEMM rows
+  const int64_t pmax = full / 200 > 64 ? (full / 200 < 512 ? full / 200 : 512) : 64;
+  P = P > pmax ? pmax : P;
   // whole rounds of workgroups: P x (query tiles) a multiple of 256 when that keeps >= 8 tiles
   const int64_t per = 256 / (B_pad / 256) > 0 ? 256 / (B_pad / 256) : 1;
   if (P / per * per >= 8) P = P / per * per;

@@ -92,7 +92,33 @@ int row_norms(const void* x, int dtype, int64_t n, int32_t d, int64_t ld, double
 }
 
 // ------------------------------------------------------------------------- screen image ----
-template <int DT, int IMG>
+// One wave per row (grid-stride over rows): the row's scale 1/gnorm is computed once per lane,
+// lanes take consecutive 16-byte output chunks (coalesced loads and stores), and with VEC the 8
+// source elements of a chunk come in 16-byte vector loads (one for 16-bit sources, two for f32,
+// four for f64). Same arithmetic as the element form: round_to(img, x * (1/gnorm)) in float64.
+template <int DT>
+__device__ __forceinline__ void load8_f64(const void* __restrict__ x, int64_t off, double (&v)[8]) {
+  if constexpr (DT == EBT_F32) {
+    const float4 a = *(const float4*)((const float*)x + off);
+    const float4 b = *(const float4*)((const float*)x + off + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else if constexpr (DT == EBT_F64) {
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      const double2 a = *(const double2*)((const double*)x + off + e);
+      v[e] = a.x;
+      v[e + 1] = a.y;
+    }
+  } else {
+    const u16x8_t h = *(const u16x8_t*)((const uint16_t*)x + off);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      v[e] = DT == EBT_BF16 ? bf16_bits_to_f64(h[e]) : f16_bits_to_f64(h[e]);
+  }
+}
+
+template <int DT, int IMG, bool VEC>
 __global__ __launch_bounds__(256) void screen_image_kernel(const void* __restrict__ x, int64_t n,
                                                             int d, int64_t ld,
                                                             const double* __restrict__ gnorm,
@@ -100,20 +126,28 @@ __global__ __launch_bounds__(256) void screen_image_kernel(const void* __restric
                                                             uint16_t* __restrict__ img,
                                                             int ld_img) {
   const int cpr = ld_img / 8;  // 16-byte chunks per image row
-  const int64_t total = n * cpr;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t row = t / cpr;
-    const int c = (int)(t - row * cpr);
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); row < n;
+       row += waves) {
     const double s = normalize ? 1.0 / gnorm[row] : 1.0;
-    u16x8_t o;
+    for (int c = lane; c < cpr; c += 64) {
+      u16x8_t o;
+      if (VEC && c * 8 + 8 <= d) {
+        double v[8];
+        load8_f64<DT>(x, row * ld + c * 8, v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int j = c * 8 + e;
-      const double v = j < d ? load_as_f64<DT>(x, row * ld + j) * s : 0.0;
-      o[e] = f64_to_img<IMG>(v);
+        for (int e = 0; e < 8; ++e) o[e] = f64_to_img<IMG>(v[e] * s);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int jj = c * 8 + e;
+          const double v = jj < d ? load_as_f64<DT>(x, row * ld + jj) * s : 0.0;
+          o[e] = f64_to_img<IMG>(v);
+        }
+      }
+      *(u16x8_t*)(img + row * ld_img + c * 8) = o;
     }
-    *(u16x8_t*)(img + row * ld_img + c * 8) = o;
   }
 }
 
@@ -127,17 +161,24 @@ int screen_image(const void* x, int dtype, int64_t n, int32_t d, int64_t ld,
     return EBT_EINVAL;
   }
   if (n == 0) return EBT_OK;
-  const int64_t total = n * (ld_img / 8);
-  int64_t blocks = ceil_div(total, 256);
-  if (blocks > 65536) blocks = 65536;
+  int64_t blocks = ceil_div(n, 4);  // one wave per row, 4 waves per block
+  if (blocks > 8192) blocks = 8192;
   dim3 grid((unsigned)blocks), block(256);
-#define EBT_SI(DT)                                                                             \
-  if (img_dtype == EBT_F16)                                                                    \
-    hipLaunchKernelGGL((screen_image_kernel<DT, EBT_F16>), grid, block, 0, st, x, n, d, ld,    \
+  const int es = dtype == EBT_F64 ? 8 : (dtype == EBT_F32 ? 4 : 2);
+  const bool vec = ((uintptr_t)x & 15) == 0 && (ld * es) % 16 == 0;
+#define EBT_SI_V(DT, IMG)                                                                      \
+  if (vec)                                                                                     \
+    hipLaunchKernelGGL((screen_image_kernel<DT, IMG, true>), grid, block, 0, st, x, n, d, ld,  \
                        gnorm, normalize, (uint16_t*)img, ld_img);                              \
   else                                                                                         \
-    hipLaunchKernelGGL((screen_image_kernel<DT, EBT_BF16>), grid, block, 0, st, x, n, d, ld,   \
+    hipLaunchKernelGGL((screen_image_kernel<DT, IMG, false>), grid, block, 0, st, x, n, d, ld, \
                        gnorm, normalize, (uint16_t*)img, ld_img);
+#define EBT_SI(DT)                                                                             \
+  if (img_dtype == EBT_F16) {                                                                  \
+    EBT_SI_V(DT, EBT_F16)                                                                      \
+  } else {                                                                                     \
+    EBT_SI_V(DT, EBT_BF16)                                                                     \
+  }
   switch (dtype) {
     case EBT_F32: EBT_SI(EBT_F32) break;
     case EBT_BF16: EBT_SI(EBT_BF16) break;
@@ -145,6 +186,7 @@ int screen_image(const void* x, int dtype, int64_t n, int32_t d, int64_t ld,
     default: EBT_SI(EBT_F64) break;
   }
 #undef EBT_SI
+#undef EBT_SI_V
   return launch_check("screen_image_kernel");
 }
 

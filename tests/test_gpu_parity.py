@@ -890,6 +890,34 @@ def test_unsorted_device_exclusions(cuda_device, dt):
     assert_topk_equal(s2, r2, s_ref, r_ref)
 
 
+@pytest.mark.parametrize("dt,d,ld,img", [("f32", 1536, 1536, 2), ("f32", 77, 80, 2),
+                                          ("f64", 200, 200, 1), ("bf16", 72, 72, 2),
+                                          ("f16", 130, 136, 1), ("f32", 77, 77, 1)])
+def test_screen_image_bitwise(cuda_device, dt, d, ld, img):
+    """ebt_screen_image (one wave per row, 16-byte vector loads where the rows allow it, the
+    element form for a ragged last chunk or an unaligned stride): bitwise equal to
+    round_to(img, x * (1/gnorm)) in float64 -> float32 -> f16/bf16, zero columns past d."""
+    ebt, L = _ebt()
+    n = 1000
+    x = torch.randn((n, ld), generator=torch.Generator().manual_seed(d), dtype=torch.float64)
+    x[3] = 0.0                                          # the zero-norm guard
+    xt = x.to(TORCH_DT[dt]).to(cuda_device)
+    g = torch.empty(n, dtype=torch.float64, device=cuda_device)
+    L.call("ebt_row_norms", L.ptr(xt), L.DTYPE_CODE[xt.dtype], n, d, ld, L.ptr(g), None,
+           L.stream_of(cuda_device))
+    ld_img = (d + 63) // 64 * 64
+    out = torch.full((n, ld_img), 7, dtype=torch.int16, device=cuda_device)
+    for normalize in (1, 0):
+        L.call("ebt_screen_image", L.ptr(xt), L.DTYPE_CODE[xt.dtype], n, d, ld, L.ptr(g),
+               normalize, img, L.ptr(out), ld_img, L.stream_of(cuda_device))
+        xd = xt[:, :d].double()
+        s = (1.0 / g) if normalize else torch.ones_like(g)
+        want = (xd * s[:, None]).float().to(torch.float16 if img == 2 else torch.bfloat16)
+        got = out[:, :d].view(torch.float16 if img == 2 else torch.bfloat16)
+        assert torch.equal(got.view(torch.int16), want.view(torch.int16))
+        assert bool((out[:, d:] == 0).all())
+
+
 def test_exclusion_csr_with_offset_start(cuda_device):
     """a device CSR whose offsets start past 0 (a sub-batch slicing the offsets of a
     larger CSR), with unsorted segments and foreign rows before off[0] and after off[-1]: the

@@ -3,7 +3,7 @@ rank, each with its own shard of the C3 catalog, exchanging through in-process c
 communication cost). The GPU runs the ranks' work back to back, so per-rank time ~ the step
 time / N. Compares the two-phase path with the per-shard-rescore path.
 
-    python tools/shard_sim.py [--ranks 2 4 8] [--steps 3]
+    python tools/shard_sim.py [--config C3] [--ranks 2 4 8] [--steps 3] [--one-rank]
 """
 import argparse
 import json
@@ -47,7 +47,7 @@ def one_rank(args):
     floor (approx[k-1] - eps) is computed first, then rank 0 runs alone with the all-reduce
     replaced by the stored max."""
     from robot_ebert_amd import _lib, search
-    cfg = bench.CONFIGS["C3"]
+    cfg = bench.CONFIGS[args.config]
     dev = torch.device("cuda:0")
     q = bench.make_queries(cfg, dev)
     k = cfg["k"]
@@ -124,7 +124,8 @@ def one_rank(args):
                 else:
                     same = bool(torch.equal(r_, ref[1]) and torch.allclose(s_, ref[0], rtol=0, atol=0,
                                                                            equal_nan=True))
-            print(json.dumps({"ranks": R, "path": "one_rank_" + name, "ms_per_step": round(ms, 3),
+            print(json.dumps({"config": args.config, "ranks": R, "path": "one_rank_" + name,
+                              "ms_per_step": round(ms, 3),
                               "same_as_shared": same,
                               "stages_ms": {kk: round(tm.query(kk)[0], 3) for kk in _lib.STAGES}}),
                   flush=True)
@@ -134,6 +135,7 @@ def one_rank(args):
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3", choices=sorted(bench.CONFIGS))
     ap.add_argument("--ranks", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--one-rank", action="store_true",
@@ -144,7 +146,7 @@ def main():
     args = ap.parse_args()
     if args.one_rank:
         return one_rank(args)
-    cfg = bench.CONFIGS["C3"]
+    cfg = bench.CONFIGS[args.config]
     dev = torch.device("cuda:0")
     q = bench.make_queries(cfg, dev)
     import threading
