@@ -424,22 +424,17 @@ static int merge_entries(int kprime) {
   return P;
 }
 
-__global__ __launch_bounds__(STHREADS) void merge_segment_kernel(
-    float* __restrict__ fv, int64_t* __restrict__ fi, int kprime,
+// One query's merge (the whole workgroup). tier 1 (P_max = a small LDS buffer, several
+// workgroups per CU) defers a query whose union does not fit (ovf bit MERGE_DEFER, nothing
+// written); tier 2 (the full buffer) merges a deferred one.
+__device__ __forceinline__ void merge_segment_one(
+    int64_t b, float* __restrict__ fv, int64_t* __restrict__ fi, int kprime,
     const uint64_t* __restrict__ cand, int64_t ld_cand, int slots,
     const uint8_t* __restrict__ counts, int64_t ld_counts, int n_groups, int P_max,
-    int64_t row_offset,
-    const int64_t* __restrict__ eo, const int64_t* __restrict__ er, int* __restrict__ ovf,
-    int tier) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t mkeep[];
-  __shared__ int wsum[STHREADS / 64];
-  __shared__ int flag;
+    int64_t row_offset, const int64_t* __restrict__ eo, const int64_t* __restrict__ er,
+    int* __restrict__ ovf, int tier, uint64_t* mkeep, int* wsum, int& flag) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t b = blockIdx.x;
-  // tier 1 (P_max = a small LDS buffer, several workgroups per CU) defers a query whose union
-  // does not fit (ovf bit MERGE_DEFER, nothing written); tier 2 (the full buffer) merges only those
   const int ovf_in = tier ? ovf[b] : 0;
-  if (tier == 2 && !(ovf_in & MERGE_DEFER)) return;
   const uint8_t* cr = counts + b * ld_counts;
   const uint64_t* cb = cand + b * ld_cand;
   if (tid == 0) flag = 0;
@@ -516,6 +511,33 @@ __global__ __launch_bounds__(STHREADS) void merge_segment_kernel(
   if (tid == 0 && (flag || tier == 2)) ovf[b] = (ovf_in & ~MERGE_DEFER) | (flag ? 1 : 0);
 }
 
+// tier 0 / 1: one workgroup per query. tier 2: a grid of at most one workgroup per CU (the
+// full LDS buffer) walks the queries and merges only those tier 1 deferred -- a handful per
+// batch -- instead of launching B full-LDS workgroups that mostly exit at once (64 dispatch
+// rounds of them at 16384 queries per merge).
+__global__ __launch_bounds__(STHREADS) void merge_segment_kernel(
+    float* __restrict__ fv, int64_t* __restrict__ fi, int kprime,
+    const uint64_t* __restrict__ cand, int64_t ld_cand, int slots,
+    const uint8_t* __restrict__ counts, int64_t ld_counts, int n_groups, int P_max,
+    int64_t row_offset,
+    const int64_t* __restrict__ eo, const int64_t* __restrict__ er, int* __restrict__ ovf,
+    int tier, int64_t B) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t mkeep[];
+  __shared__ int wsum[STHREADS / 64];
+  __shared__ int flag;
+  if (tier != 2) {
+    merge_segment_one(blockIdx.x, fv, fi, kprime, cand, ld_cand, slots, counts, ld_counts,
+                      n_groups, P_max, row_offset, eo, er, ovf, tier, mkeep, wsum, flag);
+    return;
+  }
+  for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    if (!(ovf[b] & MERGE_DEFER)) continue;  // uniform
+    merge_segment_one(b, fv, fi, kprime, cand, ld_cand, slots, counts, ld_counts, n_groups,
+                      P_max, row_offset, eo, er, ovf, tier, mkeep, wsum, flag);
+    __syncthreads();  // LDS and the block's shared words are reused by the next query
+  }
+}
+
 int merge_segment(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t* cand,
                   int64_t ld_cand, int slots, const uint8_t* counts, int64_t ld_counts,
                   int64_t n_groups,
@@ -546,13 +568,23 @@ int merge_segment(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t*
   if (P_small < P_max) {
     hipLaunchKernelGGL(merge_segment_kernel, dim3((unsigned)B), dim3(STHREADS),
                        (size_t)P_small * 8, st, fv, fi, kprime, cand, ld_cand, slots, counts,
-                       ld_counts, (int)n_groups, P_small, row_offset, eo, er, ovf, 1);
-    const int rc = launch_check("merge_segment_kernel");
+                       ld_counts, (int)n_groups, P_small, row_offset, eo, er, ovf, 1, B);
+    int rc = launch_check("merge_segment_kernel");
     if (rc) return rc;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    const int64_t g2 = B < cus ? B : cus;
+    hipLaunchKernelGGL(merge_segment_kernel, dim3((unsigned)g2), dim3(STHREADS),
+                       (size_t)P_max * 8, st, fv, fi, kprime, cand, ld_cand, slots, counts,
+                       ld_counts, (int)n_groups, P_max, row_offset, eo, er, ovf, 2, B);
+    return launch_check("merge_segment_kernel");
   }
   hipLaunchKernelGGL(merge_segment_kernel, dim3((unsigned)B), dim3(STHREADS), (size_t)P_max * 8,
                      st, fv, fi, kprime, cand, ld_cand, slots, counts, ld_counts, (int)n_groups,
-                     P_max, row_offset, eo, er, ovf, P_small < P_max ? 2 : 0);
+                     P_max, row_offset, eo, er, ovf, 0, B);
   return launch_check("merge_segment_kernel");
 }
 
