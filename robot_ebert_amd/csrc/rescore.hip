@@ -258,6 +258,192 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
   }
 }
 
+// The same rescore with the candidate rows gathered into LDS by LDS-DMA
+// (global_load_lds_dwordx4: per-lane source addresses, no VGPRs held by the data), R rows per
+// batch: the workgroup keeps R * row_bytes (about 24 KiB) in flight per round trip instead of two
+// rows per wave, so a query whose rows are gathered in ~15 dependent round trips needs ~8 (C2:
+// ~123 rows of 1.5 KiB per query, latency-bound, not bandwidth-bound). Arithmetic, order of
+// summation and every decision are those of rescore_kernel: bit-identical results.
+typedef __attribute__((address_space(3))) void rs_lds_void;
+typedef __attribute__((address_space(1))) const void rs_gbl_cvoid;
+
+template <int DT>
+__global__ __launch_bounds__(RTHREADS) void rescore_lds_kernel(
+    const double* __restrict__ q64, int d, const void* __restrict__ cat, int64_t ld,
+    const double* __restrict__ gnorm, int64_t row_offset, const float* __restrict__ cand_vals,
+    const int64_t* __restrict__ cand_rows, int kprime, int kpp, int k, int64_t n_rows,
+    const float* __restrict__ eps, const double* __restrict__ t_floor, double* __restrict__ out_s,
+    int64_t* __restrict__ out_r, int32_t* __restrict__ certified, const int* __restrict__ ovf_cnt,
+    int ovf_cap, int R) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int ES = (DT == EBT_F64) ? 8 : (DT == EBT_F32 ? 4 : 2);
+  constexpr int PER = 16 / ES;
+  constexpr int NW = RTHREADS / 64;
+  const int cpr = d / PER;                    // 16-byte chunks per row
+  const int rb = cpr * 16;
+  char* stage = smem;                         // R rows, padded to whole 1 KiB pieces
+  const int stage_bytes = (R * cpr + 63) / 64 * 1024;
+  double* qs = (double*)(smem + stage_bytes);
+  double* sc = qs + ((d + 1) & ~1);
+  int64_t* rw = (int64_t*)(sc + kpp);
+  int* pl = (int*)(rw + kpp);
+  int* sel = pl + ((kpp + 1) & ~1);
+  double* gsc = (double*)(sel + ((kpp + 1) & ~1));  // the batch rows' gnorm (R)
+  __shared__ int nvalid, corrupt, nkeep, ntop, nsel;
+  __shared__ unsigned long long smin_key;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = blockIdx.x;
+  if (tid == 0) {
+    nvalid = 0;
+    corrupt = 0;
+    nkeep = 0;
+    ntop = 0;
+    smin_key = ~0ull;
+  }
+  for (int j = tid; j < d; j += RTHREADS) qs[j] = q64[b * d + j];
+  const int64_t* cr = cand_rows + b * kprime;
+  const float* cv = cand_vals + b * kprime;
+  double cut = (double)cv[k - 1] - 2.0 * (double)eps[b];
+  if (t_floor && t_floor[b] - (double)eps[b] > cut) cut = t_floor[b] - (double)eps[b];
+  __syncthreads();
+  for (int c0 = 0; c0 < kprime; c0 += RTHREADS) {
+    const int c = c0 + tid;
+    int64_t row = -1;
+    float v = 0.f;
+    if (c < kprime) {
+      row = cr[c];
+      v = cv[c];
+    }
+    const bool bad = c < kprime && row >= n_rows;
+    const bool valid = c < kprime && row >= 0 && !bad;
+    const bool keep = valid && !((double)v < cut);
+    if (bad) corrupt = 1;
+    const uint64_t vb = __ballot(valid), kb = __ballot(keep);
+    int base = 0;
+    if (lane == 0) {
+      if (vb) atomicAdd(&nvalid, __popcll(vb));
+      if (kb) base = atomicAdd(&nkeep, __popcll(kb));
+    }
+    base = __shfl(base, 0, 64);
+    if (keep) {
+      const int at = base + __popcll(kb & ((1ull << lane) - 1));
+      rw[at] = row;
+      sc[at] = (double)v;
+      pl[at] = c;
+    }
+  }
+  __syncthreads();
+  const int nk = nkeep;
+  // the positions a pass scores, compacted into sel[0, nsel) (list order)
+  auto select = [&](bool top, double cut2) {
+    if (tid == 0) nsel = 0;
+    __syncthreads();
+    for (int j0 = 0; j0 < nk; j0 += RTHREADS) {
+      const int j = j0 + tid;
+      bool take = false;
+      if (j < nk) {
+        take = (pl[j] < k) == top && (top || !(sc[j] < cut2));
+        if (!top && pl[j] >= k && !take) sc[j] = -__builtin_inf();  // below the two-stage cut
+      }
+      const uint64_t tb = __ballot(take);
+      int base = 0;
+      if (lane == 0 && tb) base = atomicAdd(&nsel, __popcll(tb));
+      base = __shfl(base, 0, 64);
+      if (take) sel[base + __popcll(tb & ((1ull << lane) - 1))] = j;
+    }
+    __syncthreads();
+  };
+  auto score = [&]() {
+    const int m = nsel;
+    for (int s0 = 0; s0 < m; s0 += R) {
+      const int nr = m - s0 < R ? m - s0 : R;
+      const int nch = nr * cpr;
+      const int ninstr = (nch + 63) / 64;
+      for (int it = wave; it < ninstr; it += NW) {
+        int c = it * 64 + lane;
+        c = c < nch ? c : nch - 1;  // lanes past the batch re-read its last chunk
+        const int r = c / cpr, w = c - r * cpr;
+        const char* src = (const char*)cat + (rw[sel[s0 + r]] * ld) * ES + (int64_t)w * 16;
+        __builtin_amdgcn_global_load_lds((rs_gbl_cvoid*)src, (rs_lds_void*)(stage + it * 1024),
+                                         16, 0, 0);
+      }
+      if (tid < nr) gsc[tid] = gnorm[rw[sel[s0 + tid]]];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      for (int r = wave; r < nr; r += NW) {
+        const char* rowp = stage + r * rb;
+        double acc = 0.0;
+        for (int ch = lane; ch < cpr; ch += 64)
+          acc += chunk_dot<DT>(qs, ch * PER, *(const uint4*)(rowp + ch * 16));
+        acc = wave_sum_f64(acc);
+        if (lane == 0) {
+          const double v = acc / gsc[r];
+          sc[sel[s0 + r]] = (v == v) ? v : -__builtin_inf();
+        }
+      }
+      __syncthreads();  // the stage is overwritten by the next batch
+    }
+  };
+  select(true, 0.0);
+  score();
+  for (int j = tid; j < nk; j += RTHREADS) {
+    if (pl[j] < k) {
+      atomicAdd(&ntop, 1);
+      const double x = sc[j];
+      unsigned long long key = (unsigned long long)__double_as_longlong(x);
+      key = (key >> 63) ? ~key : (key | 0x8000000000000000ull);
+      if (x == x) atomicMin(&smin_key, key);
+    }
+  }
+  __syncthreads();
+  double cut2 = cut;
+  if (ntop == k && smin_key != ~0ull && eps[b] > 0.f) {
+    const unsigned long long key = smin_key;
+    const double smin = __longlong_as_double(
+        (long long)((key >> 63) ? (key & 0x7fffffffffffffffull) : ~key));
+    if (smin - (double)eps[b] > cut2) cut2 = smin - (double)eps[b];
+  }
+  select(false, cut2);
+  score();
+  int P = 1;
+  while (P < nk || P < k) P <<= 1;
+  for (int c = nk + tid; c < P; c += RTHREADS) {
+    sc[c] = -__builtin_inf();
+    rw[c] = INT64_MAX;
+  }
+  __syncthreads();
+  bitonic_pairs(sc, rw, P);
+  for (int j = tid; j < k; j += RTHREADS) {
+    const int64_t r = rw[j];
+    if (r == INT64_MAX) {
+      out_s[b * k + j] = __builtin_nan("");
+      out_r[b * k + j] = -1;
+    } else {
+      out_s[b * k + j] = sc[j];
+      out_r[b * k + j] = r + row_offset;
+    }
+  }
+  if (tid == 0) {
+    int ok = 1;
+    if (nvalid >= kprime && n_rows > kprime) {
+      const double amin = (double)cv[kprime - 1];
+      ok = amin < cut2;
+    }
+    if (ovf_cnt && ovf_cnt[b] > ovf_cap) ok = -1;
+    if (corrupt) ok = -2;
+    certified[b] = ok;
+  }
+}
+
+// LDS of rescore_lds_kernel for R rows per batch (0 when the layout does not apply)
+static size_t rescore_lds_stage_total(int d, int es, int kprime, int R) {
+  const int kpp = next_pow2_h(kprime);
+  const int cpr = d * es / 16;
+  const size_t stage = (size_t)(R * cpr + 63) / 64 * 1024;
+  return stage + 8 * (size_t)((d + 1) & ~1) + 16 * (size_t)kpp + 8 * (size_t)((kpp + 1) & ~1) +
+         8 * (size_t)R;
+}
+
 size_t rescore_lds_bytes(int d, int kprime) {
   const int kpp = next_pow2_h(kprime);
   return 8 * (size_t)((d + 1) & ~1) + 20 * (size_t)kpp;
@@ -285,6 +471,33 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
   const bool vec = (((uintptr_t)cat & 15) == 0) && ((ld * es) % 16 == 0) &&
                    (((int64_t)d * es) % 16 == 0);
   dim3 grid((unsigned)B), block(RTHREADS);
+#ifndef EBT_RESCORE_REGISTERS
+  // LDS-DMA gather when 4 workgroups per CU still fit (<= 38 KiB each) with >= 2 rows per batch:
+  // about 24 KiB of rows per batch (C2: 16 rows of 1.5 KiB; C3 f32 rows of 6 KiB: 3)
+  if (vec) {
+    const int row_bytes = d * es;
+    int R = (24 << 10) / row_bytes;
+    R = R > 64 ? 64 : R;
+    while (R >= 2 && rescore_lds_stage_total(d, es, kprime, R) > (38u << 10)) --R;
+    if (R >= 2) {
+      const size_t lds2 = rescore_lds_stage_total(d, es, kprime, R);
+#define EBT_RSL(DT)                                                                             \
+  (void)hipFuncSetAttribute((const void*)rescore_lds_kernel<DT>,                                \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);             \
+  hipLaunchKernelGGL((rescore_lds_kernel<DT>), grid, block, lds2, st, q64, d, cat, ld, gnorm,   \
+                     row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps, t_floor,    \
+                     out_s, out_r, certified, ovf_cnt, ovf_cap, R);
+      switch (dtype) {
+        case EBT_F32: EBT_RSL(EBT_F32) break;
+        case EBT_BF16: EBT_RSL(EBT_BF16) break;
+        case EBT_F16: EBT_RSL(EBT_F16) break;
+        default: EBT_RSL(EBT_F64) break;
+      }
+#undef EBT_RSL
+      return launch_check("rescore_lds_kernel");
+    }
+  }
+#endif
 #define EBT_RS(DT)                                                                              \
   (void)hipFuncSetAttribute((const void*)rescore_kernel<DT, true>,                              \
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
