@@ -217,7 +217,11 @@ static bool spec_params(int64_t B_pad, int64_t n_rows, int32_t kprime, int64_t* 
   // lambda = k' m / n, and the threshold at the j-th (j ~ lambda + 5 sqrt(lambda) + 6), so the
   // hits per query ~ j n / m fall roughly as 1 / m while lambda is small: C5 (50M rows, k' = 1256)
   // 64 -> 512 tiles takes ~21.6K hits per query to ~5.4K for 0.3 % more GEMM rows
-  const int64_t pmax = full / 200 > 64 ? (full / 200 < 512 ? full / 200 : 512) : 64;
+#ifndef EBT_SPEC_SAMPLE_DIV
+#define EBT_SPEC_SAMPLE_DIV 200
+#endif
+  const int64_t pdiv = full / EBT_SPEC_SAMPLE_DIV;
+  const int64_t pmax = pdiv > 64 ? (pdiv < 512 ? pdiv : 512) : 64;
   P = P > pmax ? pmax : P;
   // whole rounds of workgroups: P x (query tiles) a multiple of 256 when that keeps >= 8 tiles
   const int64_t per = 256 / (B_pad / 256) > 0 ? 256 / (B_pad / 256) : 1;

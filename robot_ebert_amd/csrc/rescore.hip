@@ -472,14 +472,16 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
                    (((int64_t)d * es) % 16 == 0);
   dim3 grid((unsigned)B), block(RTHREADS);
 #ifndef EBT_RESCORE_REGISTERS
-  // LDS-DMA gather when 4 workgroups per CU still fit (<= 38 KiB each) with >= 2 rows per batch:
-  // about 24 KiB of rows per batch (C2: 16 rows of 1.5 KiB; C3 f32 rows of 6 KiB: 3)
+  // LDS-DMA gather when 4 workgroups per CU still fit (<= 38 KiB each) with more than 8 rows
+  // per batch: about 24 KiB of rows per batch (C2 / C4: 16 rows of 1.5 KiB); large rows (C3's
+  // 6 KiB f32 rows: 3 per batch) keep the register form's 8 rows in flight per workgroup
   if (vec) {
     const int row_bytes = d * es;
     int R = (24 << 10) / row_bytes;
     R = R > 64 ? 64 : R;
     while (R >= 2 && rescore_lds_stage_total(d, es, kprime, R) > (38u << 10)) --R;
-    if (R >= 2) {
+    // only where it keeps more rows in flight than the register form (8 per workgroup)
+    if (R > 8) {
       const size_t lds2 = rescore_lds_stage_total(d, es, kprime, R);
 #define EBT_RSL(DT)                                                                             \
   (void)hipFuncSetAttribute((const void*)rescore_lds_kernel<DT>,                                \
