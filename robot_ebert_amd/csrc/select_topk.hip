@@ -438,16 +438,39 @@ __device__ __forceinline__ void merge_segment_one(
   const uint8_t* cr = counts + b * ld_counts;
   const uint64_t* cb = cand + b * ld_cand;
   if (tid == 0) flag = 0;
-  // this thread's groups and hit count
-  const int per = (n_groups + STHREADS - 1) / STHREADS;
-  const int g0 = tid * per;
-  const int g1 = g0 + per < n_groups ? g0 + per : n_groups;
+  // this thread's groups: [g0, g0 + per16), per16 a multiple of 16, their counts read as
+  // 16-byte vectors (one memory round trip, not one per group)
+  const int per16 = ((n_groups + STHREADS - 1) / STHREADS + 15) & ~15;
+  const int g0 = tid * per16;
+  const int g1 = g0 + per16 < n_groups ? g0 + per16 : n_groups;
+  const bool vec_counts = ((uintptr_t)cr & 15) == 0;
+  auto counts16 = [&](int gv, uint32_t (&w)[4]) {  // counts of groups gv .. gv + 15 (0 past g1)
+    if (vec_counts && gv + 16 <= g1) {
+      const uint4 v = *(const uint4*)(cr + gv);
+      w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        w[q] = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int g = gv + q * 4 + e;
+          w[q] |= (g < g1 ? (uint32_t)cr[g] : 0u) << (8 * e);
+        }
+      }
+    }
+  };
   int mine = 0;
   bool over = false;
-  for (int g = g0; g < g1; ++g) {
-    const int c = cr[g];
-    over |= c > slots;
-    mine += c < slots ? c : slots;
+  for (int gv = g0; gv < g1; gv += 16) {
+    uint32_t w[4];
+    counts16(gv, w);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int c = (w[e >> 2] >> (8 * (e & 3))) & 255;
+      over |= c > slots;
+      mine += c < slots ? c : slots;
+    }
   }
   // block exclusive scan
   int incl = mine;
@@ -464,30 +487,67 @@ __device__ __forceinline__ void merge_segment_one(
     base += w < wave ? wsum[w] : 0;
     total += wsum[w];
   }
-  int pos = base + incl - mine;
   const int room = P_max - kprime;
   if (tier == 1 && total > room) {  // block-uniform
     if (tid == 0) ovf[b] = ovf_in | MERGE_DEFER;
     return;
   }
   if (total > room) over = true;
+  // the hits' slot positions: gbase[g] = the first position of group g's hits (exclusive prefix
+  // over groups, LDS, u16: positions past `room` are dropped anyway), gbase[n_groups] = total
+  uint16_t* gbase = (uint16_t*)(mkeep + P_max);
+  {
+    int run = base - mine;
+    for (int gv = g0; gv < g1; gv += 16) {
+      uint32_t w[4];
+      counts16(gv, w);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int g = gv + e;
+        const int c = (w[e >> 2] >> (8 * (e & 3))) & 255;
+        if (g < g1) gbase[g] = (uint16_t)(run < 65535 ? run : 65535);
+        run += c < slots ? c : slots;
+      }
+    }
+    if (tid == 0) gbase[n_groups] = (uint16_t)(total < 65535 ? total : 65535);
+  }
+  __syncthreads();
+  // every hit h < min(total, room): its group by binary search over gbase, four loads in flight
+  // per thread before any is used
+  const int nh = total < room ? total : room;
   const int64_t elo = eo ? eo[b] : 0, ehi = eo ? eo[b + 1] : 0;
-  for (int g = g0; g < g1; ++g) {
-    int c = cr[g];
-    c = c < slots ? c : slots;
-    for (int p = 0; p < c; ++p, ++pos) {
-      uint64_t comp = cb[(int64_t)g * slots + p];
+  for (int h0 = tid; h0 < nh; h0 += 4 * STHREADS) {
+    uint64_t comp[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int h = h0 + u * STHREADS;
+      comp[u] = 0ull;
+      if (h < nh) {
+        int lo = 0, hi = n_groups;  // the last g with gbase[g] <= h
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if ((int)gbase[mid] <= h) lo = mid;
+          else hi = mid;
+        }
+        comp[u] = cb[(int64_t)lo * slots + (h - (int)gbase[lo])];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int h = h0 + u * STHREADS;
+      if (h >= nh) continue;
+      uint64_t cu = comp[u];
       if (ehi > elo) {
-        const int64_t gr = (int64_t)(~(uint32_t)comp) + row_offset;
+        const int64_t gr = (int64_t)(~(uint32_t)cu) + row_offset;
         int64_t lo = elo, hi = ehi;
         while (lo < hi) {
           const int64_t mid = (lo + hi) >> 1;
           if (er[mid] < gr) lo = mid + 1;
           else hi = mid;
         }
-        if (lo < ehi && er[lo] == gr) comp = 0ull;
+        if (lo < ehi && er[lo] == gr) cu = 0ull;
       }
-      if (pos < room) mkeep[kprime + pos] = comp;
+      mkeep[kprime + h] = cu;
     }
   }
   for (int i = tid; i < kprime; i += STHREADS) {
@@ -551,8 +611,15 @@ int merge_segment(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t*
   }
   if (B == 0) return EBT_OK;
   const int P_max = merge_entries(kprime);
+  // LDS: the P entries, then the u16 group positions (n_groups + 1)
+  const size_t gb_bytes = ((size_t)(n_groups + 1) * 2 + 15) & ~(size_t)15;
+  if ((size_t)P_max * 8 + gb_bytes > 160 * 1024) {
+    set_error("merge_segment: %lld groups do not fit the LDS", (long long)n_groups);
+    return EBT_EINVAL;
+  }
   (void)hipFuncSetAttribute((const void*)merge_segment_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, P_max * 8);
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)((size_t)P_max * 8 + gb_bytes));
   // with an expected hit count (and an ovf array for the deferral bit): a first pass with room
   // for 3x the expected hits, at 4+ workgroups per CU instead of 1, then the full-size pass for
   // the (rare) queries that did not fit
@@ -567,8 +634,8 @@ int merge_segment(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t*
   }
   if (P_small < P_max) {
     hipLaunchKernelGGL(merge_segment_kernel, dim3((unsigned)B), dim3(STHREADS),
-                       (size_t)P_small * 8, st, fv, fi, kprime, cand, ld_cand, slots, counts,
-                       ld_counts, (int)n_groups, P_small, row_offset, eo, er, ovf, 1, B);
+                       (size_t)P_small * 8 + gb_bytes, st, fv, fi, kprime, cand, ld_cand, slots,
+                       counts, ld_counts, (int)n_groups, P_small, row_offset, eo, er, ovf, 1, B);
     int rc = launch_check("merge_segment_kernel");
     if (rc) return rc;
     int dev = 0, cus = 256;
@@ -578,13 +645,13 @@ int merge_segment(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t*
       cus = 256;
     const int64_t g2 = B < cus ? B : cus;
     hipLaunchKernelGGL(merge_segment_kernel, dim3((unsigned)g2), dim3(STHREADS),
-                       (size_t)P_max * 8, st, fv, fi, kprime, cand, ld_cand, slots, counts,
-                       ld_counts, (int)n_groups, P_max, row_offset, eo, er, ovf, 2, B);
+                       (size_t)P_max * 8 + gb_bytes, st, fv, fi, kprime, cand, ld_cand, slots,
+                       counts, ld_counts, (int)n_groups, P_max, row_offset, eo, er, ovf, 2, B);
     return launch_check("merge_segment_kernel");
   }
-  hipLaunchKernelGGL(merge_segment_kernel, dim3((unsigned)B), dim3(STHREADS), (size_t)P_max * 8,
-                     st, fv, fi, kprime, cand, ld_cand, slots, counts, ld_counts, (int)n_groups,
-                     P_max, row_offset, eo, er, ovf, 0, B);
+  hipLaunchKernelGGL(merge_segment_kernel, dim3((unsigned)B), dim3(STHREADS),
+                     (size_t)P_max * 8 + gb_bytes, st, fv, fi, kprime, cand, ld_cand, slots,
+                     counts, ld_counts, (int)n_groups, P_max, row_offset, eo, er, ovf, 0, B);
   return launch_check("merge_segment_kernel");
 }
 
