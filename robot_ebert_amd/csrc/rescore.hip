@@ -471,10 +471,10 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
   const bool vec = (((uintptr_t)cat & 15) == 0) && ((ld * es) % 16 == 0) &&
                    (((int64_t)d * es) % 16 == 0);
   dim3 grid((unsigned)B), block(RTHREADS);
-#ifndef EBT_RESCORE_REGISTERS
-  // LDS-DMA gather when 4 workgroups per CU still fit (<= 38 KiB each) with more than 8 rows
-  // per batch: about 24 KiB of rows per batch (C2 / C4: 16 rows of 1.5 KiB); large rows (C3's
-  // 6 KiB f32 rows: 3 per batch) keep the register form's 8 rows in flight per workgroup
+#ifdef EBT_RESCORE_LDS
+  // Measured and not the default (profiles/r3/rescore_lds_ab.txt): the LDS-DMA batches
+  // (16 rows of 1.5 KiB per round trip at C2) took 71-75 us per C2 step against 59-60 us for the
+  // register gather, interleaved on one MI355X; C3 0.616 vs 0.564 ms. Kept for that A/B.
   if (vec) {
     const int row_bytes = d * es;
     int R = (24 << 10) / row_bytes;

@@ -497,7 +497,7 @@ __device__ __forceinline__ void merge_segment_one(
   // over groups, LDS, u16: positions past `room` are dropped anyway), gbase[n_groups] = total
   uint16_t* gbase = (uint16_t*)(mkeep + P_max);
   {
-    int run = base - mine;
+    int run = base + incl - mine;  // this thread's exclusive prefix
     for (int gv = g0; gv < g1; gv += 16) {
       uint32_t w[4];
       counts16(gv, w);
