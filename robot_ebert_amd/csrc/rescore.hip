@@ -25,7 +25,7 @@ __device__ void bitonic_pairs(double* sc, int64_t* rw, int P) {
   for (int size = 2; size <= P; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int t = tid; t < (P >> 1); t += blockDim.x) {
-        const int lo = 2 * stride * (t / stride) + (t % stride);
+        const int lo = ((t & ~(stride - 1)) << 1) | (t & (stride - 1));  // stride: a power of 2
         const int hi = lo + stride;
         const double a = sc[lo], b = sc[hi];
         const int64_t ra = rw[lo], rb = rw[hi];

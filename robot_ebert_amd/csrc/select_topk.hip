@@ -195,7 +195,8 @@ __device__ void bitonic_desc(uint64_t* keep, int P) {
   for (int size = 2; size <= P; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int t = tid; t < (P >> 1); t += STHREADS) {
-        const int lo = 2 * stride * (t / stride) + (t % stride);
+        // stride is a power of two: 2 stride (t / stride) + t % stride without a division
+        const int lo = ((t & ~(stride - 1)) << 1) | (t & (stride - 1));
         const int hi = lo + stride;
         const uint64_t a = keep[lo], b = keep[hi];
         const bool desc = (lo & size) == 0;
@@ -556,17 +557,60 @@ __device__ __forceinline__ void merge_segment_one(
     mkeep[i] = (key != 0u && ix >= 0) ? (((uint64_t)key << 32) | (uint64_t)(~(uint32_t)ix)) : 0ull;
   }
   if (over) flag = 1;
-  const int used = kprime + (total < room ? total : room);
-  int P = 2;
-  while (P < used) P <<= 1;
-  for (int i = used + tid; i < P; i += STHREADS) mkeep[i] = 0ull;
+  const int used = kprime + nh;
+  // A sorted list (the streaming select's, or this kernel's own output) merges with the hits
+  // sorted alone: a bitonic sort of the next power of two >= nh, then a merge-path merge of the
+  // two descending runs into the first kprime outputs -- instead of re-sorting list + hits
+  // (the bitonic sort of P >= kprime + nh entries is LDS-bandwidth bound: ~16 B per entry and
+  // stage). Anything else (a partitioned list) takes the full sort.
+  int Ph = 2;
+  while (Ph < nh) Ph <<= 1;
   __syncthreads();
-  bitonic_desc(mkeep, P);
-  for (int i = tid; i < kprime; i += STHREADS) {
-    const uint64_t comp = mkeep[i];
-    const uint32_t key = (uint32_t)(comp >> 32);
-    fv[b * kprime + i] = key ? key2f(key) : -__builtin_inff();
-    fi[b * kprime + i] = key ? (int64_t)(~(uint32_t)comp) : -1;
+  int bad = 0;
+  for (int i = tid; i + 1 < kprime; i += STHREADS) bad |= mkeep[i] < mkeep[i + 1] ? 1 : 0;
+  const bool sorted_list = !__syncthreads_or(bad) && kprime + Ph <= P_max;
+  if (sorted_list) {
+    uint64_t* hb = mkeep + kprime;
+    for (int i = nh + tid; i < Ph; i += STHREADS) hb[i] = 0ull;
+    __syncthreads();
+    if (nh > 1) bitonic_desc(hb, Ph);
+    // outputs [o0, o1) of this thread: the merge path's split at diagonal o0 (A = the list,
+    // B = the hits, both descending; A first on equal composites -- only empty 0s can be equal)
+    const int per = (kprime + STHREADS - 1) / STHREADS;
+    const int o0 = tid * per < kprime ? tid * per : kprime;
+    const int o1 = o0 + per < kprime ? o0 + per : kprime;
+    if (o0 < o1) {
+      int lo = o0 > nh ? o0 - nh : 0, hi = o0 < kprime ? o0 : kprime;
+      while (lo < hi) {  // the number of list entries among the first o0 outputs
+        const int mid = (lo + hi) >> 1;
+        if (mkeep[mid] >= hb[o0 - 1 - mid]) lo = mid + 1;
+        else hi = mid;
+      }
+      int i = lo, j = o0 - lo;
+      for (int o = o0; o < o1; ++o) {
+        const uint64_t a = i < kprime ? mkeep[i] : 0ull;
+        const uint64_t c = j < nh ? hb[j] : 0ull;
+        const bool take_a = j >= nh || (i < kprime && a >= c);
+        const uint64_t comp = take_a ? a : c;
+        i += take_a ? 1 : 0;
+        j += take_a ? 0 : 1;
+        const uint32_t key = (uint32_t)(comp >> 32);
+        fv[b * kprime + o] = key ? key2f(key) : -__builtin_inff();
+        fi[b * kprime + o] = key ? (int64_t)(~(uint32_t)comp) : -1;
+      }
+    }
+  } else {
+    int P = 2;
+    while (P < used) P <<= 1;
+    for (int i = used + tid; i < P; i += STHREADS) mkeep[i] = 0ull;
+    __syncthreads();
+    bitonic_desc(mkeep, P);
+    for (int i = tid; i < kprime; i += STHREADS) {
+      const uint64_t comp = mkeep[i];
+      const uint32_t key = (uint32_t)(comp >> 32);
+      fv[b * kprime + i] = key ? key2f(key) : -__builtin_inff();
+      fi[b * kprime + i] = key ? (int64_t)(~(uint32_t)comp) : -1;
+    }
   }
   if (tid == 0 && (flag || tier == 2)) ovf[b] = (ovf_in & ~MERGE_DEFER) | (flag ? 1 : 0);
 }
