@@ -578,6 +578,140 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_kernel(const double* __re
   }
 }
 
+// The same merge by co-ranks when every list is sorted (what ebt_cosine_topk returns): the
+// position of entry j of list r in the merged order is j + the entries of the other lists that
+// precede it (binary search in each: (score desc, row asc); equal keys -- the -inf/-1 padding --
+// ordered by list). Only a prefix of each list can reach the top k: with kr = ceil(k / R), the
+// R kr entries at list positions < kr all precede-or-equal m0 = the LAST of the R entries at
+// position kr - 1, so the k-th best does too, and an entry after m0 is in no top k. Entries up
+// to m0 (about k + R per query on untied data, of the R k) are placed by R - 1 searches within
+// the other lists' prefixes, instead of a bitonic network over next_pow2(R k) slots (log^2
+// stages of 16-byte LDS swaps). A list found unsorted sends the query down the bitonic network
+// (same result).
+constexpr int MERGE_CORANK_CAP = 8192;   // R k entries in LDS (16 B each)
+constexpr int MERGE_CORANK_RMAX = 1024;  // lists (a 4-byte prefix length each in LDS)
+
+__device__ __forceinline__ bool mt_before(double xs, int64_t xr, double es, int64_t er) {
+  return xs > es || (xs == es && xr < er);
+}
+
+size_t merge_corank_lds(int R, int P) {
+  return (size_t)P * 16 + RTHREADS * 16 + (((size_t)R * 4 + 15) & ~(size_t)15);
+}
+
+__global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
+    const double* __restrict__ scores, const int64_t* __restrict__ rows, int R, int64_t B, int k,
+    int P, double* __restrict__ out_s, int64_t* __restrict__ out_r) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int n = R * k;
+  double* sc = (double*)smem;
+  int64_t* rw = (int64_t*)(sc + P);   // P = next_pow2(n) >= n
+  double* red_s = (double*)(rw + P);
+  int64_t* red_r = (int64_t*)(red_s + RTHREADS / 2);
+  int* plen = (int*)(red_r + RTHREADS / 2);
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+#pragma unroll 4
+  for (int e = tid; e < n; e += RTHREADS) {
+    const int rr = e / k, j = e - rr * k;
+    const int64_t off = ((int64_t)rr * B + b) * k + j;
+    const int64_t row = rows[off];
+    const double v = scores[off];
+    const bool pad = row < 0;
+    sc[e] = pad || v != v ? -__builtin_inf() : v;
+    rw[e] = pad ? INT64_MAX : row;
+  }
+  __syncthreads();
+  int bad = 0;
+  for (int e = tid; e < n; e += RTHREADS) {
+    const int j = e % k;
+    if (j + 1 < k && mt_before(sc[e + 1], rw[e + 1], sc[e], rw[e])) bad = 1;
+  }
+  if (__syncthreads_or(bad)) {
+    // unsorted input: the bitonic network over P >= n slots
+    for (int e = n + tid; e < P; e += RTHREADS) {
+      sc[e] = -__builtin_inf();
+      rw[e] = INT64_MAX;
+    }
+    __syncthreads();
+    bitonic_pairs(sc, rw, P);
+    for (int j = tid; j < k; j += RTHREADS) {
+      const int64_t r = rw[j];
+      out_s[b * k + j] = r == INT64_MAX ? __builtin_nan("") : sc[j];
+      out_r[b * k + j] = r == INT64_MAX ? -1 : r;
+    }
+    return;
+  }
+  // m0: the last (in merged order) of the lists' entries at position kr - 1
+  const int kr = (k + R - 1) / R;
+  double ms = __builtin_inf();
+  int64_t mr = -1;   // "before everything": the identity of the max
+  for (int r = tid; r < R; r += RTHREADS) {
+    const double xs = sc[r * k + kr - 1];
+    const int64_t xr = rw[r * k + kr - 1];
+    if (mt_before(ms, mr, xs, xr)) {
+      ms = xs;
+      mr = xr;
+    }
+  }
+  for (int h = RTHREADS / 2; h >= 1; h >>= 1) {
+    if (tid >= h && tid < 2 * h) {
+      red_s[tid - h] = ms;
+      red_r[tid - h] = mr;
+    }
+    __syncthreads();
+    if (tid < h && mt_before(ms, mr, red_s[tid], red_r[tid])) {
+      ms = red_s[tid];
+      mr = red_r[tid];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    red_s[0] = ms;
+    red_r[0] = mr;
+  }
+  __syncthreads();
+  ms = red_s[0];
+  mr = red_r[0];
+  // each list's prefix of entries preceding-or-equal m0
+  for (int r = tid; r < R; r += RTHREADS) {
+    const double* os = sc + r * k;
+    const int64_t* orw = rw + r * k;
+    int lo = kr, hi = k;   // positions < kr precede-or-equal m0 by construction
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (!mt_before(ms, mr, os[mid], orw[mid])) lo = mid + 1; else hi = mid;
+    }
+    plen[r] = lo;
+  }
+  __syncthreads();
+  for (int e = tid; e < n; e += RTHREADS) {
+    const int rr = e / k, j = e - rr * k;
+    if (j >= plen[rr]) continue;
+    const double es = sc[e];
+    const int64_t er = rw[e];
+    int pos = j;
+    for (int o = 0; o < R && pos < k; ++o) {
+      if (o == rr) continue;
+      const double* os = sc + o * k;
+      const int64_t* orw = rw + o * k;
+      // entries of list o before e: those preceding it, and equal ones when o < rr
+      int lo = 0, hi = plen[o];
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const bool before = mt_before(os[mid], orw[mid], es, er) ||
+                            (o < rr && os[mid] == es && orw[mid] == er);
+        if (before) lo = mid + 1; else hi = mid;
+      }
+      pos += lo;
+    }
+    if (pos < k) {
+      out_s[b * k + pos] = er == INT64_MAX ? __builtin_nan("") : es;
+      out_r[b * k + pos] = er == INT64_MAX ? -1 : er;
+    }
+  }
+}
+
 int merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, int32_t k,
                double* out_s, int64_t* out_r, hipStream_t st) {
   if (!scores || !rows || !out_s || !out_r || R < 1 || B < 0 || k < 1 || k > MERGE_CAP / 2) {
@@ -586,6 +720,15 @@ int merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, 
   }
   if (B == 0) return EBT_OK;
   const int64_t n = (int64_t)R * k;
+  if (R > 1 && R <= MERGE_CORANK_RMAX && n <= MERGE_CORANK_CAP) {
+    const int P = next_pow2_h((int)n);
+    const size_t lds = merge_corank_lds(R, P);
+    (void)hipFuncSetAttribute((const void*)merge_topk_corank_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(merge_topk_corank_kernel, dim3((unsigned)B), dim3(RTHREADS), lds, st,
+                       scores, rows, R, B, k, P, out_s, out_r);
+    return launch_check("merge_topk_corank_kernel");
+  }
   const int P = next_pow2_h((int)(n < MERGE_CAP ? n : MERGE_CAP));
   (void)hipFuncSetAttribute((const void*)merge_topk_kernel,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)(P * 16));

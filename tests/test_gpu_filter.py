@@ -81,11 +81,14 @@ def test_filter_matches_store(cuda_device, density, d, scaled):
           f"{int((~fits).sum())} overflowing groups")
 
 
-@pytest.mark.parametrize("R,k", [(2, 100), (8, 1000), (16, 1000), (3, 4096), (64, 128)])
-def test_merge_topk_any_rank_count(cuda_device, R, k):
-    """ebt_merge_topk (the post-all-gather merge) for R * k above one LDS sort (8192): rounds
-    that keep the running top k; equals a numpy (score desc, row asc) merge, with ties across
-    ranks, empty (-1) slots and NaN scores sorting last."""
+@pytest.mark.parametrize("shuffle", [False, True])
+@pytest.mark.parametrize("R,k", [(2, 100), (8, 100), (8, 1000), (16, 1000), (3, 4096), (64, 128),
+                                 (2, 1), (5, 3)])
+def test_merge_topk_any_rank_count(cuda_device, R, k, shuffle):
+    """ebt_merge_topk (the post-all-gather merge): sorted lists with R * k <= 8192 by co-ranks,
+    above that in bitonic rounds that keep the running top k, unsorted lists (shuffle) by the
+    bitonic network; equals a numpy (score desc, row asc) merge, with ties across ranks, empty
+    (-1) slots and NaN scores sorting last."""
     from robot_ebert_amd import _lib as L
     dev = cuda_device
     B = 6
@@ -100,6 +103,8 @@ def test_merge_topk_any_rank_count(cuda_device, R, k):
         for b in range(B):
             key = np.where(rows[r, b] < 0, -np.inf, np.where(np.isnan(s[r, b]), -np.inf, s[r, b]))
             o = np.lexsort((np.where(rows[r, b] < 0, np.iinfo(np.int64).max, rows[r, b]), -key))
+            if shuffle and r == R // 2:
+                o = rng.permutation(o)
             s[r, b], rows[r, b] = s[r, b][o], rows[r, b][o]
     ts = torch.tensor(s, device=dev)
     tr = torch.tensor(rows, device=dev)
