@@ -596,7 +596,7 @@ __device__ __forceinline__ bool mt_before(double xs, int64_t xr, double es, int6
 }
 
 size_t merge_corank_lds(int R, int P) {
-  return (size_t)P * 16 + RTHREADS * 16 + (((size_t)R * 4 + 15) & ~(size_t)15);
+  return (size_t)P * 16 + RTHREADS * 16 + (((size_t)(2 * R + 1) * 4 + 15) & ~(size_t)15);
 }
 
 __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
@@ -611,15 +611,29 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
   int* plen = (int*)(red_r + RTHREADS / 2);
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x;
-#pragma unroll 4
-  for (int e = tid; e < n; e += RTHREADS) {
-    const int rr = e / k, j = e - rr * k;
-    const int64_t off = ((int64_t)rr * B + b) * k + j;
-    const int64_t row = rows[off];
-    const double v = scores[off];
-    const bool pad = row < 0;
-    sc[e] = pad || v != v ? -__builtin_inf() : v;
-    rw[e] = pad ? INT64_MAX : row;
+  // four entries per thread in flight (a loop over e would wait for each load in turn: the
+  // compiler peels the trip count's remainder into a serial loop)
+  for (int e0 = tid; e0 < n; e0 += 4 * RTHREADS) {
+    int64_t rv[4];
+    double sv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * RTHREADS;
+      const int ec = e < n ? e : n - 1;
+      const int rr = ec / k, j = ec - rr * k;
+      const int64_t off = ((int64_t)rr * B + b) * k + j;
+      rv[u] = rows[off];
+      sv[u] = scores[off];
+    }
+    // unconditional stores (an index past n rewrites entry n - 1 with its own value): a
+    // guarded store would let the compiler sink its load behind the previous one's wait
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * RTHREADS < n ? e0 + u * RTHREADS : n - 1;
+      const bool pad = rv[u] < 0;
+      sc[e] = pad || sv[u] != sv[u] ? -__builtin_inf() : sv[u];
+      rw[e] = pad ? INT64_MAX : rv[u];
+    }
   }
   __syncthreads();
   int bad = 0;
@@ -642,52 +656,114 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
     }
     return;
   }
-  // m0: the last (in merged order) of the lists' entries at position kr - 1
+  // m0: the last (in merged order) of the lists' entries at position kr - 1; then each list's
+  // prefix of entries preceding-or-equal m0 (plen) and the prefixes' starts (cst) in the
+  // compact enumeration of the candidates
   const int kr = (k + R - 1) / R;
-  double ms = __builtin_inf();
-  int64_t mr = -1;   // "before everything": the identity of the max
-  for (int r = tid; r < R; r += RTHREADS) {
-    const double xs = sc[r * k + kr - 1];
-    const int64_t xr = rw[r * k + kr - 1];
-    if (mt_before(ms, mr, xs, xr)) {
-      ms = xs;
-      mr = xr;
+  int* cst = plen + R;   // R + 1
+  if (R <= 64) {
+    // one wave, no barriers: shuffle reduction and scan over lanes r < R
+    if (tid < 64) {
+      double ms = __builtin_inf();
+      int64_t mr = -1;   // "before everything": the identity of the max
+      if (tid < R) {
+        ms = sc[tid * k + kr - 1];
+        mr = rw[tid * k + kr - 1];
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double xs = __shfl_xor(ms, o, 64);
+        const int64_t xr = __shfl_xor(mr, o, 64);
+        if (mt_before(ms, mr, xs, xr)) {
+          ms = xs;
+          mr = xr;
+        }
+      }
+      int len = 0;
+      if (tid < R) {
+        const double* os = sc + tid * k;
+        const int64_t* orw = rw + tid * k;
+        int lo = kr, hi = k;   // positions < kr precede-or-equal m0 by construction
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (!mt_before(ms, mr, os[mid], orw[mid])) lo = mid + 1; else hi = mid;
+        }
+        len = lo;
+      }
+      int incl = len;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (tid >= o) incl += y;
+      }
+      if (tid < R) {
+        plen[tid] = len;
+        cst[tid] = incl - len;
+      }
+      if (tid == 63) cst[R] = incl;
     }
-  }
-  for (int h = RTHREADS / 2; h >= 1; h >>= 1) {
-    if (tid >= h && tid < 2 * h) {
-      red_s[tid - h] = ms;
-      red_r[tid - h] = mr;
+  } else {
+    double ms = __builtin_inf();
+    int64_t mr = -1;
+    for (int r = tid; r < R; r += RTHREADS) {
+      const double xs = sc[r * k + kr - 1];
+      const int64_t xr = rw[r * k + kr - 1];
+      if (mt_before(ms, mr, xs, xr)) {
+        ms = xs;
+        mr = xr;
+      }
+    }
+    for (int h = RTHREADS / 2; h >= 1; h >>= 1) {
+      if (tid >= h && tid < 2 * h) {
+        red_s[tid - h] = ms;
+        red_r[tid - h] = mr;
+      }
+      __syncthreads();
+      if (tid < h && mt_before(ms, mr, red_s[tid], red_r[tid])) {
+        ms = red_s[tid];
+        mr = red_r[tid];
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      red_s[0] = ms;
+      red_r[0] = mr;
     }
     __syncthreads();
-    if (tid < h && mt_before(ms, mr, red_s[tid], red_r[tid])) {
-      ms = red_s[tid];
-      mr = red_r[tid];
+    ms = red_s[0];
+    mr = red_r[0];
+    for (int r = tid; r < R; r += RTHREADS) {
+      const double* os = sc + r * k;
+      const int64_t* orw = rw + r * k;
+      int lo = kr, hi = k;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (!mt_before(ms, mr, os[mid], orw[mid])) lo = mid + 1; else hi = mid;
+      }
+      plen[r] = lo;
     }
     __syncthreads();
-  }
-  if (tid == 0) {
-    red_s[0] = ms;
-    red_r[0] = mr;
+    if (tid == 0) {
+      int c = 0;
+      for (int r = 0; r < R; ++r) {
+        cst[r] = c;
+        c += plen[r];
+      }
+      cst[R] = c;
+    }
   }
   __syncthreads();
-  ms = red_s[0];
-  mr = red_r[0];
-  // each list's prefix of entries preceding-or-equal m0
-  for (int r = tid; r < R; r += RTHREADS) {
-    const double* os = sc + r * k;
-    const int64_t* orw = rw + r * k;
-    int lo = kr, hi = k;   // positions < kr precede-or-equal m0 by construction
+  // candidate c -> (list rr, position j): one candidate per thread, so a wave's searches run
+  // side by side instead of once per list position the wave strides over
+  const int C = cst[R];
+  for (int c = tid; c < C; c += RTHREADS) {
+    int lo = 0, hi = R - 1;   // the last list whose start <= c
     while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (!mt_before(ms, mr, os[mid], orw[mid])) lo = mid + 1; else hi = mid;
+      const int mid = (lo + hi + 1) >> 1;
+      if (cst[mid] <= c) lo = mid; else hi = mid - 1;
     }
-    plen[r] = lo;
-  }
-  __syncthreads();
-  for (int e = tid; e < n; e += RTHREADS) {
-    const int rr = e / k, j = e - rr * k;
-    if (j >= plen[rr]) continue;
+    const int rr = lo, j = c - cst[rr];
+    const int e = rr * k + j;
     const double es = sc[e];
     const int64_t er = rw[e];
     int pos = j;
@@ -696,14 +772,14 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
       const double* os = sc + o * k;
       const int64_t* orw = rw + o * k;
       // entries of list o before e: those preceding it, and equal ones when o < rr
-      int lo = 0, hi = plen[o];
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
+      int lo2 = 0, hi2 = plen[o];
+      while (lo2 < hi2) {
+        const int mid = (lo2 + hi2) >> 1;
         const bool before = mt_before(os[mid], orw[mid], es, er) ||
                             (o < rr && os[mid] == es && orw[mid] == er);
-        if (before) lo = mid + 1; else hi = mid;
+        if (before) lo2 = mid + 1; else hi2 = mid;
       }
-      pos += lo;
+      pos += lo2;
     }
     if (pos < k) {
       out_s[b * k + pos] = er == INT64_MAX ? __builtin_nan("") : es;

@@ -83,7 +83,7 @@ def test_filter_matches_store(cuda_device, density, d, scaled):
 
 @pytest.mark.parametrize("shuffle", [False, True])
 @pytest.mark.parametrize("R,k", [(2, 100), (8, 100), (8, 1000), (16, 1000), (3, 4096), (64, 128),
-                                 (2, 1), (5, 3)])
+                                 (2, 1), (5, 3), (100, 20), (1024, 8)])
 def test_merge_topk_any_rank_count(cuda_device, R, k, shuffle):
     """ebt_merge_topk (the post-all-gather merge): sorted lists with R * k <= 8192 by co-ranks,
     above that in bitonic rounds that keep the running top k, unsorted lists (shuffle) by the
