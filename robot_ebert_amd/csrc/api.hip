@@ -61,6 +61,8 @@ int kth_threshold(const float*, int64_t, int64_t, int64_t, int, const float*, fl
                   hipStream_t);
 int pool_kth(const float*, int64_t, int64_t, int64_t, int, int, float*, hipStream_t,
              float* fv = nullptr, int64_t* fi = nullptr, int kprime = 0, int* ovf = nullptr);
+int spec_given_init(const float*, int64_t, int64_t, float*, float*, int64_t*, int, int*,
+                    hipStream_t);
 int screen_gemm_pool(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
                      const float*, const float*, int64_t, float*, int64_t, hipStream_t);
 int merge_segment(float*, int64_t*, int64_t, int, const uint64_t*, int64_t, int, const uint8_t*,
@@ -669,14 +671,8 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
   const int64_t m = L.head;
   const bool given = a.theta != nullptr;  // ebt_cosine_screen_at: the caller's threshold
   if (given) {
-    const float inf = __builtin_inff();
-    uint32_t bits;
-    memcpy(&bits, &inf, 4);
-    rc = hip_check(hipMemcpyAsync(tspec, a.theta, (size_t)B * 4, hipMemcpyDeviceToDevice, st),
-                   "hipMemcpyAsync");
-    if (!rc && B_pad > B)
-      rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)(tspec + B), (int)bits,
-                                       (size_t)(B_pad - B), st), "hipMemsetD32Async");
+    // the threshold, the empty list (-inf / -1), no overflow yet: one launch
+    rc = spec_given_init(a.theta, B, B_pad, tspec, fv, fi, kprime, ovf, st);
     if (rc) return rc;
   } else {
     {
@@ -694,17 +690,6 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
     if (rc) return rc;
   }
   const double spec_hits = given ? (a.hits > 0.0 ? a.hits : 1.0) : L.spec_hits;
-  if (given) {  // empty list (-inf / -1), no overflow yet
-    const float ninf = -__builtin_inff();
-    uint32_t bits;
-    memcpy(&bits, &ninf, 4);
-    rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)fv, (int)bits, (size_t)B * kprime, st),
-                   "hipMemsetD32Async");
-    if (!rc)
-      rc = hip_check(hipMemsetAsync(fi, 0xff, (size_t)B * kprime * 8, st), "hipMemsetAsync");
-    if (!rc) rc = hip_check(hipMemsetAsync(ovf, 0, (size_t)B_pad * 4, st), "hipMemsetAsync");
-    if (rc) return rc;
-  }
   // hits per group ~ H group_rows / n (per query; its threshold's own spread ~ 1/sqrt(j) on
   // top): slots for 4x that + 4, and at least enough that a group overflow (which costs its
   // query an unfused rerun of the whole catalog) is expected less than once per thousand batches

@@ -416,6 +416,76 @@ __global__ __launch_bounds__(256) void query_prep_kernel(
   }
 }
 
+// The same for 16-byte-aligned rows with d % 8 == 0 and d <= 2048 (every BASELINE shape): one
+// wave per query, lane l holding 8-element chunks l, l + 64, ... from 16-byte vector loads, the
+// sums by wave shuffles (no block barriers), q64 and the image written in 64- and 16-byte
+// pieces. Arithmetic per element as above (x = v / g, img = round(x)); the sums' order differs
+// (within float64 round-off of the norms).
+constexpr int QPW_CH = 4;   // chunks of 8 per lane: d <= 64 * 8 * 4
+template <int DT, int IMG>
+__global__ __launch_bounds__(256) void query_prep_wave_kernel(
+    const void* __restrict__ q, int64_t B, int64_t B_pad, int d, int64_t ldq, int native_q,
+    float u_cat, double* __restrict__ q64, uint16_t* __restrict__ qimg, int ld_img,
+    float* __restrict__ qscale, float* __restrict__ eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B_pad) return;
+  uint16_t* orow = qimg + b * ld_img;
+  const int nch = d >> 3, cpr = ld_img >> 3;
+  if (b >= B) {  // padding rows
+    for (int c = lane; c < cpr; c += 64) *(u16x8_t*)(orow + c * 8) = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    if (lane == 0) {
+      qscale[b] = 1.f;
+      eps[b] = 0.f;
+    }
+    return;
+  }
+  double v[QPW_CH][8];
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < QPW_CH; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      load8_f64<DT>(q, b * ldq + c * 8, v[i]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] = 0.0;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[i][e] * v[i][e];
+  }
+  const double g = guard_norm(sqrt(wave_sum_f64(s)));
+  double s2 = 0.0;
+#pragma unroll
+  for (int i = 0; i < QPW_CH; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      double x[8];
+      u16x8_t o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        x[e] = v[i][e] / g;
+        s2 += x[e] * x[e];
+        o[e] = f64_to_img<IMG>(x[e]);
+      }
+      double2* dst = (double2*)(q64 + b * d + c * 8);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dst[e] = make_double2(x[2 * e], x[2 * e + 1]);
+      if (native_q) o = *(const u16x8_t*)((const uint16_t*)q + b * ldq + c * 8);
+      *(u16x8_t*)(orow + c * 8) = o;
+    }
+  }
+  for (int c = nch + lane; c < cpr; c += 64) *(u16x8_t*)(orow + c * 8) = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  const double qnrm = sqrt(wave_sum_f64(s2));
+  if (lane == 0) {
+    qscale[b] = native_q ? (float)(1.0 / g) : 1.f;
+    const double uq = native_q ? 0.0 : (IMG == EBT_F16 ? 0x1p-11 : 0x1p-8);
+    const double uc = (double)u_cat;
+    eps[b] = (float)(1.05 * (qnrm * (uq + uc + uq * uc) + (d + 8) * 0x1p-24 * (qnrm + 1.0)) +
+                     1e-9);
+  }
+}
+
 int query_prep(const void* q, int dtype, int64_t B, int64_t B_pad, int32_t d, int64_t ldq,
                int img_dtype, int native_q, float u_cat, double* q64, void* qimg, int32_t ld_img,
                float* qscale, float* eps, hipStream_t st) {
@@ -427,10 +497,18 @@ int query_prep(const void* q, int dtype, int64_t B, int64_t B_pad, int32_t d, in
     return EBT_EINVAL;
   }
   if (B_pad == 0) return EBT_OK;
-  dim3 grid((unsigned)B_pad), block(256);
-#define EBT_QP(DT, IMG)                                                                      \
-  hipLaunchKernelGGL((query_prep_kernel<DT, IMG>), grid, block, 0, st, q, B, d, ldq, native_q, \
-                     u_cat, q64, (uint16_t*)qimg, ld_img, qscale, eps)
+  const int es = dtype == EBT_F64 ? 8 : (dtype == EBT_F32 ? 4 : 2);
+  const bool wave = d % 8 == 0 && d <= 64 * 8 * QPW_CH && ((uintptr_t)q & 15) == 0 &&
+                    (ldq * es) % 16 == 0 && ((uintptr_t)q64 & 15) == 0 &&
+                    ((uintptr_t)qimg & 15) == 0;
+  dim3 grid(wave ? (unsigned)ceil_div(B_pad, 4) : (unsigned)B_pad), block(256);
+#define EBT_QP(DT, IMG)                                                                        \
+  if (wave)                                                                                    \
+    hipLaunchKernelGGL((query_prep_wave_kernel<DT, IMG>), grid, block, 0, st, q, B, B_pad, d,  \
+                       ldq, native_q, u_cat, q64, (uint16_t*)qimg, ld_img, qscale, eps);       \
+  else                                                                                         \
+    hipLaunchKernelGGL((query_prep_kernel<DT, IMG>), grid, block, 0, st, q, B, d, ldq,         \
+                       native_q, u_cat, q64, (uint16_t*)qimg, ld_img, qscale, eps)
   const bool f16 = img_dtype == EBT_F16;
   switch (dtype) {
     case EBT_F32: if (f16) { EBT_QP(EBT_F32, EBT_F16); } else { EBT_QP(EBT_F32, EBT_BF16); } break;
@@ -439,7 +517,7 @@ int query_prep(const void* q, int dtype, int64_t B, int64_t B_pad, int32_t d, in
     default: if (f16) { EBT_QP(EBT_F64, EBT_F16); } else { EBT_QP(EBT_F64, EBT_BF16); } break;
   }
 #undef EBT_QP
-  return launch_check("query_prep_kernel");
+  return launch_check(wave ? "query_prep_wave_kernel" : "query_prep_kernel");
 }
 
 // ------------------------------------------------------------------------- exclusions ------

@@ -1169,6 +1169,38 @@ int pool_kth(const float* pool, int64_t ld, int64_t B, int64_t B_pad, int G, int
   return launch_check("pool_kth_kernel");
 }
 
+// The caller-threshold screen's set-up in one launch (it was a copy and three fills): the
+// threshold (+inf on padding rows), the empty list (-inf / -1) and no overflow.
+__global__ __launch_bounds__(256) void spec_given_init_kernel(const float* __restrict__ theta,
+                                                              int64_t B, int64_t B_pad,
+                                                              float* __restrict__ tspec,
+                                                              float* __restrict__ fv,
+                                                              int64_t* __restrict__ fi,
+                                                              int64_t n_list, int* __restrict__ ovf) {
+  const int64_t n = n_list > B_pad ? n_list : B_pad;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    if (i < B_pad) {
+      tspec[i] = i < B ? theta[i] : __builtin_inff();
+      ovf[i] = 0;
+    }
+    if (i < n_list) {
+      fv[i] = -__builtin_inff();
+      fi[i] = -1;
+    }
+  }
+}
+
+int spec_given_init(const float* theta, int64_t B, int64_t B_pad, float* tspec, float* fv,
+                    int64_t* fi, int kprime, int* ovf, hipStream_t st) {
+  const int64_t n_list = B * (int64_t)kprime;
+  const int64_t n = n_list > B_pad ? n_list : B_pad;
+  int64_t blocks = ceil_div(n, 256);
+  blocks = blocks < 4096 ? blocks : 4096;
+  hipLaunchKernelGGL(spec_given_init_kernel, dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(256),
+                     0, st, theta, B, B_pad, tspec, fv, fi, n_list, ovf);
+  return launch_check("spec_given_init_kernel");
+}
+
 int spec_threshold(const float* vals, int64_t ld, int64_t B, int64_t B_pad, int k,
                    const float* eps, const float* thr_spec, float* thr, int* ovf, int mode,
                    hipStream_t st) {
