@@ -14,6 +14,7 @@
 namespace ebt {
 
 constexpr int RTHREADS = 256;
+constexpr int RESCORE_RANK_MAX = 512;   // kept rows ordered by counting (else bitonic)
 
 __device__ __forceinline__ bool pair_before(double sa, int64_t ra, double sb, int64_t rb) {
   return sa > sb || (sa == sb && ra < rb);
@@ -225,23 +226,47 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     if (smin - (double)eps[b] > cut2) cut2 = smin - (double)eps[b];
   }
   exact_pass(false, cut2);
-  // 3. sort the kept rows (padded to a power of two >= k); slots past them read NaN / -1
-  int P = 1;
-  while (P < nk || P < k) P <<= 1;
-  for (int c = nk + tid; c < P; c += RTHREADS) {
-    sc[c] = -__builtin_inf();
-    rw[c] = INT64_MAX;
-  }
-  __syncthreads();
-  bitonic_pairs(sc, rw, P);
-  for (int j = tid; j < k; j += RTHREADS) {
-    const int64_t r = rw[j];
-    if (r == INT64_MAX) {
+  // 3. order the kept rows (score desc, row asc); positions past them read NaN / -1
+  if (nk <= RESCORE_RANK_MAX) {
+    // few rows (C2 / C3: ~120-150): each row's position is the number of rows before it,
+    // counted over LDS broadcast reads -- one barrier instead of a bitonic network's ~36
+    __syncthreads();
+    for (int j = tid; j < nk; j += RTHREADS) {
+      const double s = sc[j];
+      const int64_t r = rw[j];
+      int pos = 0;
+      for (int i = 0; i < nk; ++i) {
+        const double si = sc[i];
+        const int64_t ri = rw[i];
+        pos += (pair_before(si, ri, s, r) || (si == s && ri == r && i < j)) ? 1 : 0;
+      }
+      if (pos < k) {
+        out_s[b * k + pos] = s;
+        out_r[b * k + pos] = r + row_offset;
+      }
+    }
+    for (int j = nk + tid; j < k; j += RTHREADS) {
       out_s[b * k + j] = __builtin_nan("");
       out_r[b * k + j] = -1;
-    } else {
-      out_s[b * k + j] = sc[j];
-      out_r[b * k + j] = r + row_offset;
+    }
+  } else {
+    int P = 1;
+    while (P < nk || P < k) P <<= 1;
+    for (int c = nk + tid; c < P; c += RTHREADS) {
+      sc[c] = -__builtin_inf();
+      rw[c] = INT64_MAX;
+    }
+    __syncthreads();
+    bitonic_pairs(sc, rw, P);
+    for (int j = tid; j < k; j += RTHREADS) {
+      const int64_t r = rw[j];
+      if (r == INT64_MAX) {
+        out_s[b * k + j] = __builtin_nan("");
+        out_r[b * k + j] = -1;
+      } else {
+        out_s[b * k + j] = sc[j];
+        out_r[b * k + j] = r + row_offset;
+      }
     }
   }
   if (tid == 0) {
