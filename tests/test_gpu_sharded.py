@@ -395,9 +395,11 @@ def test_shared_threshold_liked_users(cuda_device):
         assert_topk_equal(s[sample], r[sample], want_s, want_r)
 
 
-@pytest.mark.parametrize("R,k,kk", [(8, 100, 100), (3, 7, 16), (2, 1000, 1000)])
+@pytest.mark.parametrize("R,k,kk", [(8, 100, 100), (3, 7, 16), (2, 1000, 1000), (64, 10, 32),
+                                    (33, 20, 64), (8, 1000, 1000), (9, 1000, 1000)])
 def test_union_floor_kernel_matches_torch(cuda_device, R, k, kk):
-    """ebt_union_floor (one wave per query, bisection over 64-bit keys) equals the torch
+    """ebt_union_floor (bisection over 64-bit keys: keys in registers, one wave per query up to
+    2048 values, one workgroup up to 8192, the strided form beyond) equals the torch
     restatement (the k-th largest of approx - eps over all shards), with -inf padding, NaNs and
     ties."""
     from robot_ebert_amd.search import union_floor_gathered
