@@ -1171,7 +1171,7 @@ __global__ __launch_bounds__(256) void union_floor_kernel(const float* __restric
 }
 
 // The same bisection with the query's R*(ld-1) keys held in registers (up to 32 per lane), made
-// once, and the counts as ballot popcounts: W = 1 (one wave per query, n <= 2048: C3/8 has
+// once (all loads issued before the search), and the counts as ballot popcounts: W = 1 (one wave per query, n <= 2048: C3/8 has
 // 8 x 100) or 4 (one 256-thread workgroup per query, n <= 8192: C5/8 has 8 x 1000; the waves'
 // counts meet in LDS). The strided form above re-read every value from memory, with a
 // division, in each of its 64 steps (0.39 ms per 4096-query C3/8 batch).
@@ -1188,19 +1188,14 @@ __global__ __launch_bounds__(256) void union_floor_reg_kernel(const float* __res
   const int t0 = W == 1 ? lane : tid;
   constexpr int STEP = 64 * W;
   uint64_t key[UF_PL];
-  // entry i = t0 + STEP e: list r = i / per, position j = i % per, advanced without a division
-  int r = t0 / per, j = t0 - r * per;
 #pragma unroll
   for (int e = 0; e < UF_PL; ++e) {
     key[e] = 0ull;
-    if (t0 + STEP * e < n) {
+    const int i = t0 + STEP * e;   // entry i: list i / per, position i % per
+    if (i < n) {
+      const int r = i / per, j = i - r * per;
       const float* row = g + ((int64_t)r * B + b) * ld;
       key[e] = d2key((double)row[j] - (double)row[per]);
-    }
-    j += STEP;
-    while (j >= per && r < R) {
-      j -= per;
-      ++r;
     }
   }
   uint64_t lo = 0ull, hi = ~0ull;

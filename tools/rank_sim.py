@@ -76,6 +76,8 @@ def main():
         b0, b1 = shard_range(cfg["n"], r, W)
         cats.append(ebt.Catalog(bench.make_catalog_shard(cfg, b0, b1, dev), row_offset=b0,
                                 n_global=cfg["n"]))
+        torch.cuda.synchronize()
+        print(f"shard {r}: rows [{b0}, {b1})", file=sys.stderr, flush=True)
     q = bench.make_queries(cfg, dev)
     shared = {"world": W, "slots": [None] * W, "barrier": threading.Barrier(W, timeout=300),
               "record": []}
@@ -92,6 +94,7 @@ def main():
     for t in ts:
         t.join()
     torch.cuda.synchronize()
+    print("thread ranks done", file=sys.stderr, flush=True)
     record = shared["record"]
     per_step = len(record) // a.steps if a.steps else 0
     ref = outs[0]
