@@ -687,11 +687,29 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
   const int kr = (k + R - 1) / R;
   int* cst = plen + R;   // R + 1
   if (R <= 64) {
-    // one wave, no barriers: shuffle reduction and scan over lanes r < R
+    // one wave, no barriers: lane r < R owns list r. Padding (row -1: a shard with fewer than
+    // k rows above the floor cut -- at C3/8 about 18 of a list's 100) sorts last and is never a
+    // candidate: V_r = the list's entries before its first padding entry. When at least k
+    // entries lie in the "long" lists' first kr (V_r >= kr), m0 = the last of those lists'
+    // kr-th entries bounds the k-th best as above; otherwise every non-padding entry is a
+    // candidate (they are then few) and padding fills the positions past them.
     if (tid < 64) {
+      int V = 0;
+      if (tid < R) {
+        const int64_t* orw = rw + tid * k;
+        const double* os = sc + tid * k;
+        int lo = 0, hi = k;   // first padding entry (sorted lists: padding is a suffix)
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (!(orw[mid] == INT64_MAX && os[mid] == -__builtin_inf())) lo = mid + 1; else hi = mid;
+        }
+        V = lo;
+      }
+      const bool is_long = tid < R && V >= kr;
+      const int n_long = __popcll(__ballot(is_long));
       double ms = __builtin_inf();
       int64_t mr = -1;   // "before everything": the identity of the max
-      if (tid < R) {
+      if (is_long) {
         ms = sc[tid * k + kr - 1];
         mr = rw[tid * k + kr - 1];
       }
@@ -704,16 +722,20 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
           mr = xr;
         }
       }
+      const bool bounded = n_long * kr >= k;
       int len = 0;
       if (tid < R) {
-        const double* os = sc + tid * k;
-        const int64_t* orw = rw + tid * k;
-        int lo = kr, hi = k;   // positions < kr precede-or-equal m0 by construction
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (!mt_before(ms, mr, os[mid], orw[mid])) lo = mid + 1; else hi = mid;
+        len = V;
+        if (bounded) {
+          const double* os = sc + tid * k;
+          const int64_t* orw = rw + tid * k;
+          int lo = is_long ? kr : 0, hi = V;   // long lists: positions < kr are <= m0
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (!mt_before(ms, mr, os[mid], orw[mid])) lo = mid + 1; else hi = mid;
+          }
+          len = lo;
         }
-        len = lo;
       }
       int incl = len;
 #pragma unroll
@@ -810,6 +832,11 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
       out_s[b * k + pos] = er == INT64_MAX ? __builtin_nan("") : es;
       out_r[b * k + pos] = er == INT64_MAX ? -1 : er;
     }
+  }
+  // fewer candidates than k (all of them non-padding): padding takes the rest
+  for (int j = C + tid; j < k; j += RTHREADS) {
+    out_s[b * k + j] = __builtin_nan("");
+    out_r[b * k + j] = -1;
   }
 }
 
@@ -1198,13 +1225,46 @@ __global__ __launch_bounds__(256) void union_floor_reg_kernel(const float* __res
       key[e] = d2key((double)row[j] - (double)row[per]);
     }
   }
-  uint64_t lo = 0ull, hi = ~0ull;
+  const int ne = (n + STEP - 1) / STEP;   // key slots in use (wave-uniform)
+  if (n < k) {   // fewer values than k: no k-th largest (the bisection below would return 0)
+    if (t0 == 0) t_floor[b] = -__builtin_inf();
+    return;
+  }
+  // the k-th largest key lies in [min key, max key]: bisect that bracket, not all 64 bits
+  uint64_t mn = ~0ull, mx = 0ull;
+#pragma unroll
+  for (int e = 0; e < UF_PL; ++e)
+    if (e < ne && t0 + STEP * e < n) {
+      mn = key[e] < mn ? key[e] : mn;
+      mx = key[e] > mx ? key[e] : mx;
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t a = __shfl_xor(mn, o, 64), c = __shfl_xor(mx, o, 64);
+    mn = a < mn ? a : mn;
+    mx = c > mx ? c : mx;
+  }
+  __shared__ uint64_t wmm[2][4];
+  if (W > 1) {
+    if (lane == 0) {
+      wmm[0][tid >> 6] = mn;
+      wmm[1][tid >> 6] = mx;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      mn = wmm[0][w] < mn ? wmm[0][w] : mn;
+      mx = wmm[1][w] > mx ? wmm[1][w] : mx;
+    }
+  }
+  uint64_t lo = mn, hi = mx;   // count(key >= mn) = n >= k
   int parity = 0;
   while (lo < hi) {
     const uint64_t mid = lo + ((hi - lo) >> 1) + 1;
     int c = 0;
 #pragma unroll
-    for (int e = 0; e < UF_PL; ++e) c += __popcll(__ballot(key[e] >= mid));
+    for (int e = 0; e < UF_PL; ++e)
+      if (e < ne) c += __popcll(__ballot(key[e] >= mid));
     if (W > 1) {
       if (lane == 0) wc[parity][tid >> 6] = c;
       __syncthreads();

@@ -81,23 +81,32 @@ def test_filter_matches_store(cuda_device, density, d, scaled):
           f"{int((~fits).sum())} overflowing groups")
 
 
-@pytest.mark.parametrize("shuffle", [False, True])
+@pytest.mark.parametrize("lists", ["full", "shuffle", "ragged"])
 @pytest.mark.parametrize("R,k", [(2, 100), (8, 100), (8, 1000), (16, 1000), (3, 4096), (64, 128),
                                  (2, 1), (5, 3), (100, 20), (1024, 8)])
-def test_merge_topk_any_rank_count(cuda_device, R, k, shuffle):
+def test_merge_topk_any_rank_count(cuda_device, R, k, lists):
     """ebt_merge_topk (the post-all-gather merge): sorted lists with R * k <= 8192 by co-ranks,
     above that in bitonic rounds that keep the running top k, unsorted lists (shuffle) by the
     bitonic network; equals a numpy (score desc, row asc) merge, with ties across ranks, empty
-    (-1) slots and NaN scores sorting last."""
+    (-1) slots and NaN scores sorting last; ragged: each list padded (-1) after a random number
+    of entries, 0 to k, as the per-shard lists are after the floor cut (C3/8: ~18 of 100)."""
     from robot_ebert_amd import _lib as L
     dev = cuda_device
     B = 6
+    shuffle = lists == "shuffle"
     rng = np.random.default_rng(R * 7 + k)
     s = np.round(rng.standard_normal((R, B, k)), 2)          # many exact ties across ranks
     rows = rng.permutation(R * B * k * 2)[:R * B * k].reshape(R, B, k).astype(np.int64)
     s[:, :, -3:] = np.nan
     rows[:, :, -1] = -1
     s[:, 0, :] = 0.5                                          # one query all tied
+    if lists == "ragged":
+        V = rng.integers(0, k + 1, (R, B))
+        V[:, 1] = max(1, k // (2 * R))                        # every list short, a few valid
+        V[:, 2] = 0                                           # nothing valid at all
+        for r in range(R):
+            for b in range(B):
+                rows[r, b, V[r, b]:] = -1
     # each rank's list sorted (score desc, row asc), NaN / -1 last
     for r in range(R):
         for b in range(B):

@@ -118,11 +118,35 @@ def main():
     run(timer)
     torch.cuda.synchronize()
     stages = {n: round(timer.query(n)[0] / a.steps, 4) for n in _lib.STAGES}
+    # the post-gather merge alone on the last recorded results (the last two gathers)
+    from robot_ebert_amd.search import merge_topk
+    gs, gr = record[-2], record[-1]
+    merge_topk(gs, gr, k)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        merge_topk(gs, gr, k)
+    e1.record()
+    torch.cuda.synchronize()
+    merge_alone = e0.elapsed_time(e1) / 10
+    # the gathered lists: sorted (score desc, row asc)? candidates of the co-rank merge (entries
+    # up to m0 = the last of the lists' ceil(k/R)-th entries)
+    sc_, rw_ = gs.double().cpu(), gr.cpu()
+    nxt_before = (sc_[:, :, 1:] > sc_[:, :, :-1]) | ((sc_[:, :, 1:] == sc_[:, :, :-1]) &
+                                                     (rw_[:, :, 1:] < rw_[:, :, :-1]))
+    unsorted_lists = int(nxt_before.any(2).sum())
+    kr = -(-k // W)
+    m0 = sc_[:, :, kr - 1].min(0).values                       # [B] (ties by row ignored)
+    cands = (sc_ >= m0[None, :, None]).sum((0, 2)).double()
+    diag = {"unsorted_lists": unsorted_lists, "lists": W * sc_.shape[1],
+            "candidates_mean": round(float(cands.mean()), 1),
+            "candidates_max": int(cands.max())}
     print(json.dumps({"config": a.config, "world": W, "shard_rows": cat0.n,
                       "gathers_recorded": len(record), "gathers_per_step": per_step,
                       "wall_ms_per_step": round(wall, 3), "replay_equals_threads": same,
                       "stages_ms_per_step_timed_run": stages,
-                      "stage_sum_ms": round(sum(stages.values()), 3)}), flush=True)
+                      "stage_sum_ms": round(sum(stages.values()), 3),
+                      "merge_alone_ms": round(merge_alone, 4), "merge_lists": diag}), flush=True)
 
 
 if __name__ == "__main__":
