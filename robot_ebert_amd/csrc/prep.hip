@@ -440,19 +440,33 @@ __global__ __launch_bounds__(256) void query_prep_wave_kernel(
     }
     return;
   }
+  // every chunk's raw 16-byte pieces loaded before any is used (a guarded load per chunk
+  // would wait for each in turn); chunks past the row re-read its first chunk, then count 0
+  constexpr int ES = DT == EBT_F64 ? 8 : (DT == EBT_F32 ? 4 : 2);
+  constexpr int PC = ES / 2;   // 16-byte pieces per 8-element chunk
+  uint4 raw[QPW_CH][PC];
+#pragma unroll
+  for (int i = 0; i < QPW_CH; ++i) {
+    const int c = lane + 64 * i < nch ? lane + 64 * i : 0;
+    const uint4* src = (const uint4*)((const char*)q + (b * ldq + (int64_t)c * 8) * ES);
+#pragma unroll
+    for (int p = 0; p < PC; ++p) raw[i][p] = src[p];
+  }
   double v[QPW_CH][8];
   double s = 0.0;
 #pragma unroll
   for (int i = 0; i < QPW_CH; ++i) {
-    const int c = lane + 64 * i;
-    if (c < nch) {
-      load8_f64<DT>(q, b * ldq + c * 8, v[i]);
-    } else {
+    const bool in = lane + 64 * i < nch;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[i][e] = 0.0;
+    for (int e = 0; e < 8; ++e) {
+      double x;
+      if constexpr (DT == EBT_F32) x = (double)((const float*)raw[i])[e];
+      else if constexpr (DT == EBT_F64) x = ((const double*)raw[i])[e];
+      else if constexpr (DT == EBT_BF16) x = bf16_bits_to_f64(((const uint16_t*)raw[i])[e]);
+      else x = f16_bits_to_f64(((const uint16_t*)raw[i])[e]);
+      v[i][e] = in ? x : 0.0;
+      s += v[i][e] * v[i][e];
     }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s += v[i][e] * v[i][e];
   }
   const double g = guard_norm(sqrt(wave_sum_f64(s)));
   double s2 = 0.0;
@@ -471,7 +485,7 @@ __global__ __launch_bounds__(256) void query_prep_wave_kernel(
       double2* dst = (double2*)(q64 + b * d + c * 8);
 #pragma unroll
       for (int e = 0; e < 4; ++e) dst[e] = make_double2(x[2 * e], x[2 * e + 1]);
-      if (native_q) o = *(const u16x8_t*)((const uint16_t*)q + b * ldq + c * 8);
+      if (native_q) o = *(const u16x8_t*)raw[i];   // native (DT == IMG): the query's own bits
       *(u16x8_t*)(orow + c * 8) = o;
     }
   }

@@ -44,6 +44,24 @@ __device__ void bitonic_pairs(double* sc, int64_t* rw, int P) {
   }
 }
 
+// dst[0, d) = src[0, d) by the workgroup, eight loads per thread in flight (a plain strided loop
+// waits for each load before the next); past-the-end slots re-copy entry d - 1 (same value).
+__device__ __forceinline__ void stage_f64(double* dst, const double* __restrict__ src, int d) {
+  for (int j0 = threadIdx.x; j0 < d; j0 += 8 * RTHREADS) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + u * RTHREADS;
+      v[u] = src[j < d ? j : d - 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + u * RTHREADS;
+      dst[j < d ? j : d - 1] = v[u];
+    }
+  }
+}
+
 static int next_pow2_h(int v) {
   int p = 1;
   while (p < v) p <<= 1;
@@ -96,7 +114,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     ntop = 0;
     smin_key = ~0ull;
   }
-  for (int j = tid; j < d; j += RTHREADS) qs[j] = q64[b * d + j];
+  stage_f64(qs, q64 + b * d, d);
   const int64_t* cr = cand_rows + b * kprime;
   // Candidates whose approx score is below approx[k-1] - 2 eps cannot be in the top k (the k
   // best candidates all have exact >= approx[k-1] - eps > their exact), so their rows are not
@@ -325,7 +343,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_lds_kernel(
     ntop = 0;
     smin_key = ~0ull;
   }
-  for (int j = tid; j < d; j += RTHREADS) qs[j] = q64[b * d + j];
+  stage_f64(qs, q64 + b * d, d);
   const int64_t* cr = cand_rows + b * kprime;
   const float* cv = cand_vals + b * kprime;
   double cut = (double)cv[k - 1] - 2.0 * (double)eps[b];
@@ -1000,7 +1018,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_owned_kernel(
   double* qs = (double*)smem;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
-  for (int j = tid; j < d; j += RTHREADS) qs[j] = q64[b * d + j];
+  stage_f64(qs, q64 + b * d, d);
   __syncthreads();
   const float* cv = cand_vals + b * kprime;
   const double cut = (double)cv[k - 1] - 2.0 * (double)eps[b];
@@ -1203,48 +1221,54 @@ __global__ __launch_bounds__(256) void union_floor_kernel(const float* __restric
 // counts meet in LDS). The strided form above re-read every value from memory, with a
 // division, in each of its 64 steps (0.39 ms per 4096-query C3/8 batch).
 constexpr int UF_PL = 32;
-template <int W>
+// PL: key slots per lane, a compile-time bound (the launch picks the smallest of 4/8/16/32 that
+// holds n): the count loop is then a fixed sequence of compare + popcount, no per-slot test.
+// The bisection bounds are wave-uniform (readfirstlane): a scalar loop.
+template <int W, int PL>
 __global__ __launch_bounds__(256) void union_floor_reg_kernel(const float* __restrict__ g, int R,
                                                               int64_t B, int ld, int k,
                                                               double* __restrict__ t_floor) {
   __shared__ int wc[2][4];
+  __shared__ uint64_t wmm[2][4];
   const int tid = threadIdx.x, lane = tid & 63;
   const int64_t b = W == 1 ? (int64_t)blockIdx.x * 4 + (tid >> 6) : (int64_t)blockIdx.x;
   if (W == 1 && b >= B) return;
   const int per = ld - 1, n = R * per;
   const int t0 = W == 1 ? lane : tid;
   constexpr int STEP = 64 * W;
-  uint64_t key[UF_PL];
-#pragma unroll
-  for (int e = 0; e < UF_PL; ++e) {
-    key[e] = 0ull;
-    const int i = t0 + STEP * e;   // entry i: list i / per, position i % per
-    if (i < n) {
-      const int r = i / per, j = i - r * per;
-      const float* row = g + ((int64_t)r * B + b) * ld;
-      key[e] = d2key((double)row[j] - (double)row[per]);
-    }
-  }
-  const int ne = (n + STEP - 1) / STEP;   // key slots in use (wave-uniform)
-  if (n < k) {   // fewer values than k: no k-th largest (the bisection below would return 0)
+  if (n < k) {   // fewer values than k: no k-th largest
     if (t0 == 0) t_floor[b] = -__builtin_inf();
     return;
   }
-  // the k-th largest key lies in [min key, max key]: bisect that bracket, not all 64 bits
+  // every slot's two loads issued before any is used (a guarded load per slot would wait for
+  // each in turn): indices past n re-read entry n - 1 and are masked to key 0 afterwards
+  float v[PL], ev[PL];
+#pragma unroll
+  for (int e = 0; e < PL; ++e) {
+    const int i0 = t0 + STEP * e, i = i0 < n ? i0 : n - 1;   // entry i: list i / per, i % per
+    const int r = i / per, j = i - r * per;
+    const float* row = g + ((int64_t)r * B + b) * ld;
+    v[e] = row[j];
+    ev[e] = row[per];
+  }
+  uint64_t key[PL];
   uint64_t mn = ~0ull, mx = 0ull;
 #pragma unroll
-  for (int e = 0; e < UF_PL; ++e)
-    if (e < ne && t0 + STEP * e < n) {
+  for (int e = 0; e < PL; ++e) {
+    const bool in = t0 + STEP * e < n;
+    key[e] = in ? d2key((double)v[e] - (double)ev[e]) : 0ull;
+    if (in) {
       mn = key[e] < mn ? key[e] : mn;
       mx = key[e] > mx ? key[e] : mx;
     }
+  }
+  // the k-th largest key lies in [min key, max key]: bisect that bracket, not all 64 bits
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const uint64_t a = __shfl_xor(mn, o, 64), c = __shfl_xor(mx, o, 64);
     mn = a < mn ? a : mn;
     mx = c > mx ? c : mx;
   }
-  __shared__ uint64_t wmm[2][4];
   if (W > 1) {
     if (lane == 0) {
       wmm[0][tid >> 6] = mn;
@@ -1257,20 +1281,25 @@ __global__ __launch_bounds__(256) void union_floor_reg_kernel(const float* __res
       mx = wmm[1][w] > mx ? wmm[1][w] : mx;
     }
   }
-  uint64_t lo = mn, hi = mx;   // count(key >= mn) = n >= k
+  auto uni = [](uint64_t x) {
+    const uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)x);
+    const uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+    return ((uint64_t)hi32 << 32) | lo32;
+  };
+  uint64_t lo = uni(mn), hi = uni(mx);   // count(key >= mn) = n >= k
   int parity = 0;
   while (lo < hi) {
     const uint64_t mid = lo + ((hi - lo) >> 1) + 1;
     int c = 0;
 #pragma unroll
-    for (int e = 0; e < UF_PL; ++e)
-      if (e < ne) c += __popcll(__ballot(key[e] >= mid));
+    for (int e = 0; e < PL; ++e) c += __popcll(__ballot(key[e] >= mid));
     if (W > 1) {
       if (lane == 0) wc[parity][tid >> 6] = c;
       __syncthreads();
       c = wc[parity][0] + wc[parity][1] + wc[parity][2] + wc[parity][3];
       parity ^= 1;   // the other buffer next step: no second barrier before the next write
     }
+    c = __builtin_amdgcn_readfirstlane(c);
     if (c >= k) lo = mid;
     else hi = mid - 1;
   }
@@ -1301,16 +1330,21 @@ extern "C" int ebt_union_floor(const float* gathered, int32_t R, int64_t B, int3
   }
   if (B == 0) return EBT_OK;
   const int64_t n = (int64_t)R * (ld - 1);
-  if (n <= 64 * UF_PL) {
-    hipLaunchKernelGGL(union_floor_reg_kernel<1>, dim3((unsigned)ceil_div(B, 4)), dim3(256), 0,
-                       (hipStream_t)stream, gathered, R, B, ld, k, t_floor);
-    return launch_check("union_floor_reg_kernel<1>");
+  const hipStream_t st = (hipStream_t)stream;
+  const dim3 g1((unsigned)ceil_div(B, 4)), g4((unsigned)B), blk(256);
+#define EBT_UF(W, PL, G)                                                                       \
+  {                                                                                           \
+    hipLaunchKernelGGL((union_floor_reg_kernel<W, PL>), G, blk, 0, st, gathered, R, B, ld, k, \
+                       t_floor);                                                              \
+    return launch_check("union_floor_reg_kernel");                                            \
   }
-  if (n <= 256 * UF_PL) {
-    hipLaunchKernelGGL(union_floor_reg_kernel<4>, dim3((unsigned)B), dim3(256), 0,
-                       (hipStream_t)stream, gathered, R, B, ld, k, t_floor);
-    return launch_check("union_floor_reg_kernel<4>");
-  }
+  if (n <= 64 * 4) EBT_UF(1, 4, g1)
+  if (n <= 64 * 8) EBT_UF(1, 8, g1)
+  if (n <= 64 * 16) EBT_UF(1, 16, g1)
+  if (n <= 64 * UF_PL) EBT_UF(1, 32, g1)
+  if (n <= 256 * 16) EBT_UF(4, 16, g4)
+  if (n <= 256 * UF_PL) EBT_UF(4, 32, g4)
+#undef EBT_UF
   hipLaunchKernelGGL(union_floor_kernel, dim3((unsigned)ceil_div(B, 4)), dim3(256), 0,
                      (hipStream_t)stream, gathered, R, B, ld, k, t_floor);
   return launch_check("union_floor_kernel");
