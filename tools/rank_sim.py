@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--config", default="C3", choices=sorted(bench.CONFIGS))
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--profile", action="store_true",
+                    help="also cProfile the replayed steps (host time by function, to stderr)")
     a = ap.parse_args()
     cfg = bench.CONFIGS[a.config]
     dev = torch.device("cuda:0")
@@ -114,6 +116,17 @@ def main():
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) * 1e3 / a.steps
     same = bool(torch.equal(r, ref[1]) and torch.equal(s.nan_to_num(-9.0), ref[0].nan_to_num(-9.0)))
+    if a.profile:
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        run()
+        torch.cuda.synchronize()
+        pr.disable()
+        st = pstats.Stats(pr, stream=sys.stderr)
+        st.sort_stats("tottime").print_stats(30)
+        st.sort_stats("cumulative").print_stats(40)
     timer = ebt.Timer()
     run(timer)
     torch.cuda.synchronize()
