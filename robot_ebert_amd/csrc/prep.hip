@@ -125,28 +125,54 @@ __global__ __launch_bounds__(256) void screen_image_kernel(const void* __restric
                                                             int normalize,
                                                             uint16_t* __restrict__ img,
                                                             int ld_img) {
+  constexpr int SI_CH = 4;     // chunks per lane whose loads are in flight together
   const int cpr = ld_img / 8;  // 16-byte chunks per image row
   const int lane = threadIdx.x & 63;
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
   for (int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); row < n;
        row += waves) {
     const double s = normalize ? 1.0 / gnorm[row] : 1.0;
-    for (int c = lane; c < cpr; c += 64) {
-      u16x8_t o;
-      if (VEC && c * 8 + 8 <= d) {
-        double v[8];
-        load8_f64<DT>(x, row * ld + c * 8, v);
+    for (int c0 = lane; c0 < cpr; c0 += 64 * SI_CH) {
+      if (VEC) {
+        // all of the lane's full chunks loaded before any is converted (a loop that converts
+        // each chunk as it arrives waits for every load in turn); a chunk past d (or past the
+        // row) re-reads chunk 0 and is replaced below
+        double v[SI_CH][8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = f64_to_img<IMG>(v[e] * s);
+        for (int u = 0; u < SI_CH; ++u) {
+          const int c = c0 + 64 * u;
+          load8_f64<DT>(x, row * ld + (c * 8 + 8 <= d ? c * 8 : 0), v[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < SI_CH; ++u) {
+          const int c = c0 + 64 * u;
+          if (c >= cpr) continue;
+          u16x8_t o;
+          if (c * 8 + 8 <= d) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = f64_to_img<IMG>(v[u][e] * s);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const int jj = c * 8 + e;
+              const double w = jj < d ? load_as_f64<DT>(x, row * ld + jj) * s : 0.0;
+              o[e] = f64_to_img<IMG>(w);
+            }
+          }
+          *(u16x8_t*)(img + row * ld_img + c * 8) = o;
+        }
       } else {
+        for (int c = c0; c < cpr && c < c0 + 64 * SI_CH; c += 64) {
+          u16x8_t o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int jj = c * 8 + e;
-          const double v = jj < d ? load_as_f64<DT>(x, row * ld + jj) * s : 0.0;
-          o[e] = f64_to_img<IMG>(v);
+          for (int e = 0; e < 8; ++e) {
+            const int jj = c * 8 + e;
+            const double w = jj < d ? load_as_f64<DT>(x, row * ld + jj) * s : 0.0;
+            o[e] = f64_to_img<IMG>(w);
+          }
+          *(u16x8_t*)(img + row * ld_img + c * 8) = o;
         }
       }
-      *(u16x8_t*)(img + row * ld_img + c * 8) = o;
     }
   }
 }
@@ -162,7 +188,7 @@ int screen_image(const void* x, int dtype, int64_t n, int32_t d, int64_t ld,
   }
   if (n == 0) return EBT_OK;
   int64_t blocks = ceil_div(n, 4);  // one wave per row, 4 waves per block
-  if (blocks > 8192) blocks = 8192;
+  if (blocks > (1 << 20)) blocks = 1 << 20;
   dim3 grid((unsigned)blocks), block(256);
   const int es = dtype == EBT_F64 ? 8 : (dtype == EBT_F32 ? 4 : 2);
   const bool vec = ((uintptr_t)x & 15) == 0 && (ld * es) % 16 == 0;
