@@ -44,8 +44,13 @@ __device__ void bitonic_pairs(double* sc, int64_t* rw, int P) {
   }
 }
 
+// Marks v as used here, unconditionally: a load feeding only a guarded store would otherwise be
+// sunk into the guard's block and waited for there, one load at a time.
+__device__ __forceinline__ void issued(double v) { asm volatile("" : : "v"(v)); }
+__device__ __forceinline__ void issued(int64_t v) { asm volatile("" : : "v"(v)); }
+
 // dst[0, d) = src[0, d) by the workgroup, eight loads per thread in flight (a plain strided loop
-// waits for each load before the next); past-the-end slots re-copy entry d - 1 (same value).
+// waits for each load before the next); past-the-end slots load entry d - 1 and store nothing.
 __device__ __forceinline__ void stage_f64(double* dst, const double* __restrict__ src, int d) {
   for (int j0 = threadIdx.x; j0 < d; j0 += 8 * RTHREADS) {
     double v[8];
@@ -57,7 +62,8 @@ __device__ __forceinline__ void stage_f64(double* dst, const double* __restrict_
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int j = j0 + u * RTHREADS;
-      dst[j < d ? j : d - 1] = v[u];
+      issued(v[u]);
+      if (j < d) dst[j] = v[u];
     }
   }
 }
@@ -668,14 +674,16 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
       rv[u] = rows[off];
       sv[u] = scores[off];
     }
-    // unconditional stores (an index past n rewrites entry n - 1 with its own value): a
-    // guarded store would let the compiler sink its load behind the previous one's wait
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * RTHREADS < n ? e0 + u * RTHREADS : n - 1;
-      const bool pad = rv[u] < 0;
-      sc[e] = pad || sv[u] != sv[u] ? -__builtin_inf() : sv[u];
-      rw[e] = pad ? INT64_MAX : rv[u];
+      const int e = e0 + u * RTHREADS;
+      issued(rv[u]);
+      issued(sv[u]);
+      if (e < n) {
+        const bool pad = rv[u] < 0;
+        sc[e] = pad || sv[u] != sv[u] ? -__builtin_inf() : sv[u];
+        rw[e] = pad ? INT64_MAX : rv[u];
+      }
     }
   }
   __syncthreads();
