@@ -1078,7 +1078,15 @@ static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_
   const uint16_t* C = (const uint16_t*)cimg;
   if (big) {
     // persistent: one 148 KiB-LDS workgroup per CU walks ceil(tiles / CUs) tiles
-    const int64_t G = nwg < n_cus() ? nwg : n_cus();
+    int64_t G = nwg < n_cus() ? nwg : n_cus();
+#ifdef EBT_GRID_OVERRIDE
+    // ablation build only: EBT_QP_GRID=<workgroups> runs the persistent grid on fewer CUs (the
+    // GEMM's rate on a CU subset, for overlap experiments); never in the shipped library
+    if (const char* g = getenv("EBT_QP_GRID")) {
+      const int64_t v = atoll(g) & ~7LL;
+      if (v >= 8 && v < G) G = v;
+    }
+#endif
     const int ktiles = d_pad / 64;
     dim3 grid((unsigned)G), block(QP_THREADS);
     auto k = (ktiles & 1) ? (img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, EPI, true>
