@@ -284,6 +284,80 @@ __global__ __launch_bounds__(256) void query_liked_kernel(const void* __restrict
   }
 }
 
+// The same sums for 16-byte-aligned rows (ld * size and the base 16-byte aligned, d a multiple of
+// the elements per 16 bytes): the query's rows and norms staged in LDS, each thread owning whole
+// 16-byte chunks of the row, UL liked rows' chunks loaded before any is added (the loop above
+// waits for every element load in turn). The per-element sum runs over the liked rows in the
+// same order with the same operations: bit-identical to query_liked_kernel.
+constexpr int QL_STAGE = 256;   // liked rows staged per round
+constexpr int QL_UL = 8;        // liked rows in flight per chunk
+template <int DT>
+__global__ __launch_bounds__(256) void query_liked_vec_kernel(
+    const void* __restrict__ cat, int d, int64_t ld, const double* __restrict__ gnorm,
+    const int64_t* __restrict__ off, const int64_t* __restrict__ rows, int64_t row_offset,
+    int64_t n_local, double* __restrict__ q64) {
+  constexpr int ES = DT == EBT_F64 ? 8 : (DT == EBT_F32 ? 4 : 2);
+  constexpr int PER = 16 / ES;   // elements per 16-byte chunk
+  __shared__ int64_t srow[QL_STAGE];
+  __shared__ double sg[QL_STAGE];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t l0 = off[b], l1 = off[b + 1];
+  const int nch = d / PER;
+  // a thread's chunks: c = tid, tid + 256, ... (at most QL_CPT of them: d <= 256 * PER * QL_CPT)
+  constexpr int QL_CPT = 2;
+  double acc[QL_CPT][PER];
+#pragma unroll
+  for (int i = 0; i < QL_CPT; ++i)
+#pragma unroll
+    for (int e = 0; e < PER; ++e) acc[i][e] = 0.0;
+  for (int64_t s0 = l0; s0 < l1; s0 += QL_STAGE) {
+    const int ns = l1 - s0 < QL_STAGE ? (int)(l1 - s0) : QL_STAGE;
+    __syncthreads();
+    if (tid < ns) {
+      const int64_t r = rows[s0 + tid] - row_offset;
+      const bool skip = n_local > 0 && (r < 0 || r >= n_local);   // another shard's row
+      srow[tid] = skip ? -1 : r;
+      sg[tid] = skip ? 1.0 : gnorm[r];
+    }
+    __syncthreads();
+    for (int u0 = 0; u0 < ns; u0 += QL_UL) {
+#pragma unroll
+      for (int i = 0; i < QL_CPT; ++i) {
+        const int c = tid + 256 * i;
+        if (c >= nch) break;
+        uint4 raw[QL_UL];
+#pragma unroll
+        for (int u = 0; u < QL_UL; ++u) {   // loads first (a skipped / past-the-end row reads row 0)
+          const int64_t r = u0 + u < ns ? srow[u0 + u] : -1;
+          raw[u] = *(const uint4*)((const char*)cat + ((r >= 0 ? r : 0) * ld + (int64_t)c * PER) * ES);
+        }
+#pragma unroll
+        for (int u = 0; u < QL_UL; ++u) {
+          if (u0 + u >= ns || srow[u0 + u] < 0) continue;
+          const double g = sg[u0 + u];
+#pragma unroll
+          for (int e = 0; e < PER; ++e) {
+            double x;
+            if constexpr (DT == EBT_F32) x = (double)((const float*)&raw[u])[e];
+            else if constexpr (DT == EBT_F64) x = ((const double*)&raw[u])[e];
+            else if constexpr (DT == EBT_BF16) x = bf16_bits_to_f64(((const uint16_t*)&raw[u])[e]);
+            else x = f16_bits_to_f64(((const uint16_t*)&raw[u])[e]);
+            acc[i][e] += x / g;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < QL_CPT; ++i) {
+    const int c = tid + 256 * i;
+    if (c >= nch) break;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) q64[b * d + (int64_t)c * PER + e] = acc[i][e];
+  }
+}
+
 // rows are catalog rows + row_offset (the self-contained path passes GLOBAL rows; the caller
 // guarantees every row lies inside the catalog)
 int query_liked_sum(const void* cat, int dtype, int32_t d, int64_t ld, const double* gnorm,
@@ -295,6 +369,21 @@ int query_liked_sum(const void* cat, int dtype, int32_t d, int64_t ld, const dou
   }
   if (B == 0) return EBT_OK;
   dim3 grid((unsigned)B), block(256);
+  const int es = dtype == EBT_F64 ? 8 : (dtype == EBT_F32 ? 4 : 2);
+  const int per = 16 / es;
+  if (((uintptr_t)cat & 15) == 0 && (ld * es) % 16 == 0 && d % per == 0 && d <= 256 * per * 2) {
+#define EBT_QLV(DT)                                                                            \
+  hipLaunchKernelGGL(query_liked_vec_kernel<DT>, grid, block, 0, st, cat, d, ld, gnorm, off,   \
+                     rows, row_offset, n_local, q64)
+    switch (dtype) {
+      case EBT_F32: EBT_QLV(EBT_F32); break;
+      case EBT_BF16: EBT_QLV(EBT_BF16); break;
+      case EBT_F16: EBT_QLV(EBT_F16); break;
+      default: EBT_QLV(EBT_F64); break;
+    }
+#undef EBT_QLV
+    return launch_check("query_liked_vec_kernel");
+  }
   switch (dtype) {
     case EBT_F32: hipLaunchKernelGGL(query_liked_kernel<EBT_F32>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, row_offset, n_local, q64); break;
     case EBT_BF16: hipLaunchKernelGGL(query_liked_kernel<EBT_BF16>, grid, block, 0, st, cat, d, ld, gnorm, off, rows, row_offset, n_local, q64); break;

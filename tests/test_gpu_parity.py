@@ -1066,3 +1066,31 @@ def test_route_recommendations_matches_reference(cuda_device, k):
                                    atol=SCORE_ATOL)
         if not want:
             assert got == []
+
+
+@pytest.mark.parametrize("dt,d", [("f32", 1536), ("bf16", 768), ("f16", 200), ("f64", 64)])
+def test_liked_prep_vector_form_bitwise(cuda_device, dt, d):
+    """ebt_query_liked_sum's vector form (16-byte-aligned rows: staged row ids, eight liked rows'
+    chunks in flight) writes exactly what the element form writes (same per-element order of
+    additions): the same catalog once with aligned rows and once as a column slice of a wider
+    matrix (ld = d + 1: the element form). Users with 0, 1 and 300 liked rows, duplicates."""
+    ebt, L = _ebt()
+    n = 20_000
+    x = gaussian(51, n, d + 1, dt)
+    wide = _t(x, dt, cuda_device)
+    narrow = wide[:, :d].contiguous()
+    cat_v = ebt.Catalog(narrow)                 # ld = d: the vector form
+    cat_s = ebt.Catalog(wide[:, :d])            # ld = d + 1: the element form
+    rng = np.random.default_rng(52)
+    liked = [[5], rng.choice(n, 300, replace=False).tolist(), [7, 7, 19999],
+             rng.choice(n, 17, replace=False).tolist()]
+    from robot_ebert_amd.search import csr_from_lists
+    lk = csr_from_lists(liked, cuda_device)
+    assert cat_v.ld == d and cat_s.ld == d + 1
+    # the same row norms for both (the norm kernel's own vector / element forms may round apart)
+    cat_s.gnorm.copy_(cat_v.gnorm)
+    qv = ebt.prepare_queries(cat_v, liked=lk)
+    qs = ebt.prepare_queries(cat_s, liked=lk)
+    assert torch.equal(qv.q64, qs.q64)
+    assert torch.equal(qv.qimg.view(torch.int16), qs.qimg.view(torch.int16))
+    assert torch.equal(qv.eps, qs.eps)
