@@ -911,12 +911,27 @@ __global__ __launch_bounds__(256) void screen_exact_kernel(
   const int64_t r0 = (int64_t)blockIdx.x * XT, b0 = (int64_t)blockIdx.y * XT;
   double acc[4][4] = {};
   for (int k0 = 0; k0 < d; k0 += XK) {
-    for (int e = tid; e < XT * XK; e += 256) {
+    // the tile's 4 elements per thread loaded before any is stored (guarded loads would each
+    // be waited for in turn): out-of-range indices read a clamped in-range element, then 0
+    constexpr int NE = XT * XK / 256;
+    double cv[NE], qv[NE];
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + 256 * u;
+      const int rr = e / XK, kk = e % XK;
+      const int64_t row = r0 + rr, qb = b0 + rr;
+      const int kc = k0 + kk < d ? k0 + kk : d - 1;
+      cv[u] = load_as_f64<DT>(cat, (row < n_rows ? row : n_rows - 1) * ld + kc);
+      qv[u] = q64[(qb < B ? qb : B - 1) * d + kc];
+    }
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+      const int e = tid + 256 * u;
       const int rr = e / XK, kk = e % XK;
       const int64_t row = r0 + rr, qb = b0 + rr;
       const bool kin = k0 + kk < d;
-      cs[kk][rr] = (kin && row < n_rows) ? load_as_f64<DT>(cat, row * ld + k0 + kk) : 0.0;
-      qs[kk][rr] = (kin && qb < B) ? q64[qb * d + k0 + kk] : 0.0;
+      cs[kk][rr] = (kin && row < n_rows) ? cv[u] : 0.0;
+      qs[kk][rr] = (kin && qb < B) ? qv[u] : 0.0;
     }
     __syncthreads();
 #pragma unroll
