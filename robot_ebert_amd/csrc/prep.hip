@@ -430,12 +430,26 @@ __global__ __launch_bounds__(256) void query_image_kernel(
     return;
   }
   double s = 0.0, sn = 0.0;
-  for (int j = threadIdx.x; j < d; j += blockDim.x) {
-    const double v = q64[b * d + j];
-    s += v * v;
-    if (native_q) {
-      const double w = IMG == EBT_F16 ? f16_bits_to_f64(qn[b * ldq + j]) : bf16_bits_to_f64(qn[b * ldq + j]);
-      sn += w * w;
+  // eight of a thread's elements loaded before any is summed (same order of additions as one at
+  // a time; a plain strided loop waits for each load in turn)
+  for (int j0 = threadIdx.x; j0 < d; j0 += 8 * blockDim.x) {
+    double v[8];
+    uint16_t h[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + u * blockDim.x;
+      const int jc = j < d ? j : d - 1;
+      v[u] = q64[b * d + jc];
+      h[u] = native_q ? qn[b * ldq + jc] : (uint16_t)0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (j0 + u * (int)blockDim.x >= d) break;
+      s += v[u] * v[u];
+      if (native_q) {
+        const double w = IMG == EBT_F16 ? f16_bits_to_f64(h[u]) : bf16_bits_to_f64(h[u]);
+        sn += w * w;
+      }
     }
   }
   const double qnrm = sqrt(block_sum_f64(s, red));
