@@ -210,7 +210,11 @@ __device__ void bitonic_desc(uint64_t* keep, int P) {
   }
 }
 
-template <bool HAS_IDX, bool VEC>
+// TPI tiles per iteration: the next TPI tiles are loaded while the current TPI are admitted
+// one tile at a time (the buffer check and the admission per tile as for TPI = 1), so a
+// workgroup keeps TPI x 16 KiB in flight. With two workgroups per CU (the LDS buffer), one tile
+// in flight is 32 KiB per CU -- below what HBM needs in flight to stream at full rate.
+template <bool HAS_IDX, bool VEC, int TPI>
 __global__ __launch_bounds__(STHREADS, 2) void select_topk_kernel(
     const float* __restrict__ vals, const int64_t* __restrict__ idxs, int64_t ld, int64_t n,
     int64_t seg_len, int64_t idx_base, int kprime, float* __restrict__ out_vals,
@@ -245,13 +249,15 @@ __global__ __launch_bounds__(STHREADS, 2) void select_topk_kernel(
   };
   float tf = thr_f(thr);
 
-  // one tile in flight (a second one, 32 KiB per workgroup, measured 20 % slower)
-  float cur[SE], nxt[SE];
-  int64_t curi[SE], nxti[SE];
-  auto load_tile = [&](int64_t t0, float* v, int64_t* ix) {
+  constexpr int TE = SE * TPI;  // values per lane in flight
+  float cur[TE], nxt[TE];
+  int64_t curi[HAS_IDX ? TE : 1], nxti[HAS_IDX ? TE : 1];
+  // tiles t0, t0 + STILE, ... (TPI of them); element e of tile h at
+  // t0 + h * STILE + (e >> 2) * (STHREADS * 4) + tid * 4 + (e & 3)
+  auto load_tiles = [&](int64_t t0, float* v, int64_t* ix) {
 #pragma unroll
-    for (int j = 0; j < SE / 4; ++j) {
-      const int64_t p = t0 + j * (STHREADS * 4) + tid * 4;
+    for (int j = 0; j < TE / 4; ++j) {
+      const int64_t p = t0 + (j / (SE / 4)) * STILE + (j % (SE / 4)) * (STHREADS * 4) + tid * 4;
       if constexpr (VEC) {
         if (p < s1) {
           const float4 f = *(const float4*)(vrow + p);
@@ -282,62 +288,106 @@ __global__ __launch_bounds__(STHREADS, 2) void select_topk_kernel(
     }
   };
 
+#if defined(EBT_SEL_DIAG)
+  float dsum = 0.f;
+#endif
   const int64_t ntiles = (s1 - s0 + STILE - 1) / STILE;
-  if (ntiles > 0) load_tile(s0, cur, curi);
-  for (int64_t t = 0; t < ntiles; ++t) {
-    const int64_t t0 = s0 + t * STILE;
-    if (nbuf + STILE > Lo.cap) {
-      const uint64_t theta = compact(bkey, bidx, nbuf, kprime, keep, hist, red, misc);
-      nbuf = kprime;
-      const uint32_t tau = (uint32_t)(theta >> 32);
-      thr = HAS_IDX ? tau : tau + 1u;
-      tf = thr_f(thr);
-      if (tid == 0) misc[3] = (uint32_t)nbuf;
-      lds_barrier();
-    }
-    if (t + 1 < ntiles) load_tile(t0 + STILE, nxt, nxti);
-    // fast test: once the threshold has risen, almost no tile has a value to admit; the wave
-    // then skips the per-value ballots (a superset test: entries past the segment read -inf,
-    // excluded (idx < 0) ones are dropped below)
-    bool any = false;
+  const int64_t niter = (ntiles + TPI - 1) / TPI;
+  if (ntiles > 0) load_tiles(s0, cur, curi);
+  for (int64_t it = 0; it < niter; ++it) {
+    const int64_t i0 = s0 + it * (int64_t)(TPI * STILE);
+    if (it + 1 < niter) load_tiles(i0 + TPI * STILE, nxt, nxti);
 #pragma unroll
-    for (int e = 0; e < SE; ++e) any |= cur[e] >= tf;
-    if (__ballot(any) != 0ull)
+    for (int h = 0; h < TPI; ++h) {
+      const int64_t t0 = i0 + h * STILE;
+      if (t0 >= s1) break;  // uniform: past the segment's last tile
+#if defined(EBT_SEL_DIAG) && EBT_SEL_DIAG == 1
+      // diagnostic build only: the stream alone (no admission, no barrier)
 #pragma unroll
-    for (int e = 0; e < SE; ++e) {
-      const int64_t p = t0 + (e >> 2) * (STHREADS * 4) + tid * 4 + (e & 3);
-      uint32_t key = p < s1 ? f2key(cur[e]) : 0u;
-      uint32_t ix;
-      if constexpr (HAS_IDX) {
-        if (curi[e] < 0) key = 0u;
-        ix = (uint32_t)curi[e];
-      } else {
-        ix = (uint32_t)p;
+      for (int e = 0; e < SE; ++e) dsum += cur[h * SE + e];
+      continue;
+#elif defined(EBT_SEL_DIAG) && EBT_SEL_DIAG == 2
+      // diagnostic build only: nothing is admitted, the per-tile test and barrier stay
+      thr = 0xffffffffu;
+      tf = __builtin_inff();
+#endif
+      if (nbuf + STILE > Lo.cap) {
+        const uint64_t theta = compact(bkey, bidx, nbuf, kprime, keep, hist, red, misc);
+        nbuf = kprime;
+        const uint32_t tau = (uint32_t)(theta >> 32);
+        thr = HAS_IDX ? tau : tau + 1u;
+        tf = thr_f(thr);
+        if (tid == 0) misc[3] = (uint32_t)nbuf;
+        lds_barrier();
       }
-      const bool take = key >= thr;
-      const uint64_t m = __ballot(take);
-      if (m) {
-        uint32_t wb = 0;
-        if (lane == 0) wb = atomicAdd(&misc[3], (uint32_t)__popcll(m));
-        wb = __shfl(wb, 0, 64);
-        if (take) {
-          const uint32_t pos = wb + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-          bkey[pos] = key;
-          bidx[pos] = ix;
+      // fast test: once the threshold has risen, few tiles have a value to admit; a wave with
+      // none skips the admission (a superset test: entries past the segment read -inf, excluded
+      // (idx < 0) ones are dropped below)
+      bool any = false;
+#pragma unroll
+      for (int e = 0; e < SE; ++e) any |= cur[h * SE + e] >= tf;
+      if (__ballot(any) != 0ull) {
+        // admission: a lane's admitted values as a bit mask, a wave scan of the lane counts and
+        // ONE LDS atomic per wave for the wave's total; each lane then writes its own entries.
+        // The threshold only rises at a compaction, so between two of them a wave admits a few
+        // values in most tiles: a ballot + atomic per value slot cost ~16 LDS round trips per
+        // wave and tile, the whole difference between this kernel and its bare stream.
+        // The buffer order differs from a per-slot admission; the result does not (compaction
+        // and the final sort order unique composites).
+        // f2key(v) >= thr  <=>  v >= tf for every v (thr_f above; NaN compares false), so the
+        // mask needs no key: a float compare and the segment end in 32 bits
+        const int lim = (int)(s1 - t0 < STILE ? s1 - t0 : STILE);
+        uint32_t msk = 0;
+#pragma unroll
+        for (int e = 0; e < SE; ++e) {
+          const int o = (e >> 2) * (STHREADS * 4) + tid * 4 + (e & 3);
+          bool take = o < lim && cur[h * SE + e] >= tf;
+          if constexpr (HAS_IDX) take = take && curi[h * SE + e] >= 0;
+          msk |= (take ? 1u : 0u) << e;
+        }
+        // exclusive prefix of the lane counts (0..16, five bits) from one ballot per bit: no
+        // cross-lane LDS traffic (a shuffle scan is six dependent ds_bpermute round trips)
+        const uint32_t cnt = (uint32_t)__popc(msk);
+        uint32_t excl = 0, tot = 0;
+#pragma unroll
+        for (int bit = 0; bit < 5; ++bit) {
+          const uint64_t bm = __ballot((cnt >> bit) & 1u);
+          const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+              (uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+          excl += below << bit;
+          tot += (uint32_t)__popcll(bm) << bit;
+        }
+        if (tot) {
+          uint32_t wb = 0;
+          if (lane == 0) wb = atomicAdd(&misc[3], tot);
+          wb = (uint32_t)__builtin_amdgcn_readfirstlane((int)wb);  // lane 0: exec is full here
+          uint32_t pos = wb + excl;
+#pragma unroll
+          for (int e = 0; e < SE; ++e) {
+            if ((msk >> e) & 1u) {
+              bkey[pos] = f2key(cur[h * SE + e]);
+              if constexpr (HAS_IDX) bidx[pos] = (uint32_t)curi[h * SE + e];
+              else bidx[pos] = (uint32_t)t0 + (uint32_t)((e >> 2) * (STHREADS * 4) + tid * 4 + (e & 3));
+              ++pos;
+            }
+          }
         }
       }
+      lds_barrier();
+      nbuf = (int)misc[3];
     }
-    lds_barrier();
-    nbuf = (int)misc[3];
-    if (t + 1 < ntiles) {
+    if (it + 1 < niter) {
 #pragma unroll
-      for (int e = 0; e < SE; ++e) {
+      for (int e = 0; e < TE; ++e) {
         cur[e] = nxt[e];
         if constexpr (HAS_IDX) curi[e] = nxti[e];
       }
     }
   }
 
+#if defined(EBT_SEL_DIAG)
+  if (dsum == 1.2345f) misc[3] = 0;  // keeps the diagnostic stream live
+#endif
   // final: exactly min(kprime, nbuf) survivors, sorted
   int nk = nbuf;
   if (nbuf > kprime) {
@@ -366,6 +416,13 @@ __global__ __launch_bounds__(STHREADS, 2) void select_topk_kernel(
 
 size_t select_lds_bytes(int kprime) { return sel_layout(kprime).bytes; }
 
+// tiles in flight per workgroup: two for a plain score row; one when int64 row ids travel with
+// the values (three times the registers per value)
+#ifndef EBT_SEL_TPI
+#define EBT_SEL_TPI 2
+#endif
+#define SEL_TPI(H) ((H) ? 1 : EBT_SEL_TPI)
+
 static int select_launch(const float* vals, const int64_t* idx, int64_t ld, int64_t B,
                          int64_t n, int64_t idx_base, int32_t kprime, int32_t segs,
                          float* out_vals, int64_t* out_idx, int64_t ld_out, hipStream_t stream) {
@@ -384,10 +441,10 @@ static int select_launch(const float* vals, const int64_t* idx, int64_t ld, int6
   const size_t lds = select_lds_bytes(kprime);
   dim3 grid((unsigned)B, (unsigned)segs), block(STHREADS);
 #define EBT_SEL_LAUNCH(H, V)                                                                  \
-  (void)hipFuncSetAttribute((const void*)select_topk_kernel<H, V>,                            \
+  (void)hipFuncSetAttribute((const void*)select_topk_kernel<H, V, SEL_TPI(H)>,                \
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
-  hipLaunchKernelGGL((select_topk_kernel<H, V>), grid, block, lds, stream, vals, idx, ld, n, \
-                     seg_len, idx_base, (int)kprime, out_vals, out_idx, ld_out)
+  hipLaunchKernelGGL((select_topk_kernel<H, V, SEL_TPI(H)>), grid, block, lds, stream, vals, \
+                     idx, ld, n, seg_len, idx_base, (int)kprime, out_vals, out_idx, ld_out)
   if (idx) {
     if (vec) { EBT_SEL_LAUNCH(true, true); }
     else { EBT_SEL_LAUNCH(true, false); }

@@ -290,9 +290,13 @@ def _select_ref(v, k):
     return order
 
 
-@pytest.mark.parametrize("n,k,segs", [(1, 4, 1), (3, 8, 1), (4097, 100, 1), (100000, 256, 1),
-                                       (100000, 256, 7), (30000, 1000, 2), (9000, 4096, 1)])
-def test_select_topk_exact(cuda_device, n, k, segs):
+@pytest.mark.parametrize("n,k,segs,odd_ld", [
+    (1, 4, 1, False), (3, 8, 1, False), (4097, 100, 1, False), (100000, 256, 1, False),
+    (100000, 256, 7, False), (30000, 1000, 2, False), (9000, 4096, 1, False),
+    (50001, 200, 1, True), (20000, 300, 3, True)])
+def test_select_topk_exact(cuda_device, n, k, segs, odd_ld):
+    """Streaming select (select_topk.hip) vs a numpy lexsort: exact rows and values, ties by row,
+    -inf / NaN never selected; odd_ld: a row pitch that is not a multiple of 4 (scalar loads)."""
     ebt, L = _ebt()
     rng = np.random.default_rng(n + k)
     B = 6
@@ -301,7 +305,7 @@ def test_select_topk_exact(cuda_device, n, k, segs):
     v[2, ::3] = -np.inf                     # masked entries
     v[3, ::5] = np.nan
     v[4] = 0.5                              # all equal
-    ld = (n + 3) // 4 * 4
+    ld = n + 1 if odd_ld else (n + 3) // 4 * 4
     vt = torch.full((B, ld), -np.inf, device=cuda_device)
     vt[:, :n] = torch.from_numpy(v).to(cuda_device)
     ov = torch.empty((B, segs * k), device=cuda_device)
