@@ -3,10 +3,11 @@
 // Replaces `movie_scores.loc[unrated].sort_values(ascending=False)[:k]` (lib.py:55; pandas
 // core/series.py:3706-3716, a full O(N log N) argsort) with a single streaming pass per row
 // segment. One 256-thread workgroup owns a (row, segment); it streams the segment in 4096-entry
-// tiles (16 values per lane, float4 loads, next tile prefetched into registers) and keeps a
-// candidate buffer in LDS:
-//   * an entry is admitted when its order-preserving key >= thr (initially every valid entry);
-//     admission is wave-aggregated: one ballot + one LDS atomic per wave per value slot;
+// tiles (16 values per lane, float4 loads, the next two tiles prefetched into registers) and
+// keeps a candidate buffer in LDS:
+//   * an entry is admitted when its order-preserving key >= thr (initially every valid entry),
+//     tested as a float compare against thr's float form; admission is wave-aggregated: the
+//     lane counts' prefix from one ballot per count bit, one LDS atomic per wave and tile;
 //   * when the buffer cannot take another full tile, it is compacted to exactly its k' best
 //     entries by an adaptive-range radix select (11-bit histograms over the live [min, max] of
 //     the 64-bit composite (key, ~index), so hot bins stay spread out), and thr rises to the
