@@ -31,6 +31,19 @@ __host__ __device__ inline int next_pow2(int v) {
   return p;
 }
 
+// Buffer room beside the k' kept entries, in quarter tiles (> 4: a full tile's admissions must
+// fit without compacting every tile; exactly one tile of room measured 1.7x slower). Measured
+// alternative (-DEBT_SEL_ROOM=5 -DEBT_SEL_WGS=3): 1.25 tiles keep the LDS of k' <= ~500 at
+// ~51 KiB, three workgroups per CU: 4096 x 1M, k' = 200 in 3.13 ms against 3.45 with two tiles
+// of room and two workgroups per CU (each workgroup's per-tile admission is latency-bound, so
+// more of them per CU shortens the pass). Not the default until its select-path GPU tests run.
+#ifndef EBT_SEL_ROOM
+#define EBT_SEL_ROOM 8
+#endif
+#ifndef EBT_SEL_WGS
+#define EBT_SEL_WGS 2
+#endif
+
 struct SelLayout {
   int cap;       // buffer capacity (entries)
   int kpp;       // next pow2 >= kprime
@@ -39,9 +52,7 @@ struct SelLayout {
 
 __host__ __device__ inline SelLayout sel_layout(int kprime) {
   SelLayout L;
-  // two tiles of room: with one, every tile that admits anything past k' forces a compaction
-  // (measured 1.7x slower on 1M-entry rows)
-  L.cap = kprime + 2 * STILE;
+  L.cap = kprime + EBT_SEL_ROOM * (STILE / 4);
   L.kpp = next_pow2(kprime);
   L.off_key = 0;
   L.off_idx = L.off_key + 4 * (size_t)L.cap;
@@ -213,10 +224,9 @@ __device__ void bitonic_desc(uint64_t* keep, int P) {
 
 // TPI tiles per iteration: the next TPI tiles are loaded while the current TPI are admitted
 // one tile at a time (the buffer check and the admission per tile as for TPI = 1), so a
-// workgroup keeps TPI x 16 KiB in flight. With two workgroups per CU (the LDS buffer), one tile
-// in flight is 32 KiB per CU -- below what HBM needs in flight to stream at full rate.
+// workgroup keeps TPI x 16 KiB in flight (TPI = 2: 1-2 % faster than 1; 3 is slower).
 template <bool HAS_IDX, bool VEC, int TPI>
-__global__ __launch_bounds__(STHREADS, 2) void select_topk_kernel(
+__global__ __launch_bounds__(STHREADS, EBT_SEL_WGS) void select_topk_kernel(
     const float* __restrict__ vals, const int64_t* __restrict__ idxs, int64_t ld, int64_t n,
     int64_t seg_len, int64_t idx_base, int kprime, float* __restrict__ out_vals,
     int64_t* __restrict__ out_idx, int64_t ld_out) {
