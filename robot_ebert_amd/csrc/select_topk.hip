@@ -32,16 +32,16 @@ __host__ __device__ inline int next_pow2(int v) {
 }
 
 // Buffer room beside the k' kept entries, in quarter tiles (> 4: a full tile's admissions must
-// fit without compacting every tile; exactly one tile of room measured 1.7x slower). Measured
-// alternative (-DEBT_SEL_ROOM=5 -DEBT_SEL_WGS=3): 1.25 tiles keep the LDS of k' <= ~500 at
-// ~51 KiB, three workgroups per CU: 4096 x 1M, k' = 200 in 3.13 ms against 3.45 with two tiles
-// of room and two workgroups per CU (each workgroup's per-tile admission is latency-bound, so
-// more of them per CU shortens the pass). Not the default until its select-path GPU tests run.
+// fit without compacting every tile; exactly one tile of room measured 1.7x slower). 1.25 tiles
+// keep the LDS of k' <= ~500 at ~51 KiB, three workgroups per CU: 4096 x 1M, k' = 200 in
+// 3.13 ms against 3.45 with two tiles of room and two workgroups per CU (-DEBT_SEL_ROOM=8
+// -DEBT_SEL_WGS=2): each workgroup's per-tile admission is latency-bound, so more of them per
+// CU shortens the pass.
 #ifndef EBT_SEL_ROOM
-#define EBT_SEL_ROOM 8
+#define EBT_SEL_ROOM 5
 #endif
 #ifndef EBT_SEL_WGS
-#define EBT_SEL_WGS 2
+#define EBT_SEL_WGS 3
 #endif
 
 struct SelLayout {
