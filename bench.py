@@ -353,7 +353,7 @@ def launch_ranks(n: int, argv, budget_s: float, grace_s: float = 10.0) -> int:
     while live:
         for p in list(live):
             code = p.poll()
-            if code is None:
+            if code is None or p not in live:
                 continue
             live.remove(p)
             if code != 0 and rc == 0:
@@ -476,6 +476,10 @@ def main() -> None:
     ap.add_argument("--launch-timeout", type=float, default=1200.0,
                     help="wall-clock budget of a self-launched N > 1 run; the ranks are stopped "
                          "and the exit status is 124 when it is exceeded")
+    ap.add_argument("--sharded-path", default="capi", choices=["capi", "python"],
+                    help="N > 1: the C ABI's pipelined sharded step (ebt_cosine_topk_sharded_*, "
+                         "RCCL all-gathers inside libebert) or the Python pipeline "
+                         "(distributed.run_sharded_steps over torch.distributed)")
     ap.add_argument("--skip-collective-rank", type=int, default=-1,
                     help=argparse.SUPPRESS)   # --dry-run test hook (tests/test_bench_launch.py)
     args = ap.parse_args()
@@ -512,7 +516,8 @@ def main() -> None:
     dev = torch.device("cuda", local_rank)
 
     import robot_ebert_amd as ebt
-    from robot_ebert_amd.distributed import (run_sharded_steps, score_topk_sharded_local_stages,
+    from robot_ebert_amd.distributed import (RcclComm, ShardedTopk, TorchGatherComm,
+                                             run_sharded_steps, score_topk_sharded_local_stages,
                                              shard_range)
     ebt.load()
 
@@ -543,7 +548,21 @@ def main() -> None:
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                   for _ in range(max(1, args.streams) - 1)]
 
+    # N > 1 through the C ABI: the whole step (threshold, floor, rescore, retries, packed
+    # results exchange, merge) inside libebert, three batches in flight; the all-gathers are
+    # RCCL's (ebt_rccl_all_gather on the library's own communicator) -- or, on a one-GPU gloo
+    # rehearsal, torch.distributed's through a callback
+    eng, rccl = None, None
+    if world > 1 and args.sharded_path == "capi":
+        if args.share_gpu:
+            comm = TorchGatherComm(rank, world)
+        else:
+            rccl = comm = RcclComm()
+        eng = ShardedTopk(cat, k, cfg["b"], comm, timer=timer)
+
     def run_steps(n, log_every=0):
+        if eng is not None:
+            return eng.run(n, q)
         if world > 1:
             return run_sharded_steps(
                 lambda: score_topk_sharded_local_stages(cat, k, queries=q, timer=timer), n)
@@ -622,6 +641,7 @@ def main() -> None:
             "n_gpus": world,
             "rccl_world_size": (dist.get_world_size() if dist is not None and not args.share_gpu
                                 else (1 if dist is None else 0)),
+            "sharded_path": (args.sharded_path if world > 1 else None),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3),
@@ -636,7 +656,8 @@ def main() -> None:
                 "n_items": cfg["n"], "d": cfg["d"], "catalog_dtype": cfg["dtype"], "batch": cfg["b"],
                 "k": k, "parallelism": f"catalog row-sharded x{world}" +
                 ((", gloo" if args.share_gpu else ", RCCL") +
-                 " all-gather of per-shard top-k + merge" if world > 1 else ""),
+                 " all-gather of each shard's entries above the catalog-wide floor + merge"
+                 if world > 1 else ""),
                 "arith": "f16/bf16 MFMA screen (f32 acc) + exact f64 rescore of certified candidates",
             },
             "roofline": {
@@ -683,6 +704,9 @@ def main() -> None:
         if world == 1 and args.device_check > 0:
             out["device_parity"] = device_f64_check(emb, q, s, r, args.device_check)
         print(json.dumps(out), flush=True)
+    if rccl is not None:
+        torch.cuda.synchronize(dev)
+        rccl.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -207,6 +207,31 @@ int ebt_sort_exclusions(const int64_t* off, const int64_t* rows_in, int64_t* row
 int ebt_merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, int32_t k,
                    double* out_scores, int64_t* out_rows, void* stream);
 
+/* The compact form of that exchange (what the row-sharded step sends). After the catalog-wide
+ * floor (ebt_union_floor), a shard's entries below t_floor[b] -- a lower bound of query b's k-th
+ * best exact score over the WHOLE catalog -- cannot enter the global top k. ebt_shard_pack keeps
+ * of each sorted list (scores/rows [B][k], row < 0 = padding; t_floor NULL = keep every real
+ * entry) the prefix with score >= t_floor[b] and packs it into `send`
+ * (ebt_shard_pack_bytes(B, cap) bytes, device): u32 starts[B + 1] (query b's entries are
+ * [starts[b], starts[b + 1])) and block totals, then f64 scores[cap], then i32 GLOBAL rows[cap].
+ * Entries at positions >= cap are counted but not sent. After an all-gather of the R buffers
+ * (recv, R * ebt_shard_pack_bytes bytes, rank order), ebt_merge_packed writes the same global
+ * top-k as ebt_merge_topk over the full lists, and sets *incomplete (device int32; set to 1,
+ * never cleared) when some rank's entries did not all fit its cap: the caller must then merge
+ * the full lists instead (the rows of an incomplete batch are not final).
+ * ebt_shard_pack_cap: the cap the library uses, B * ebt_shard_list_width(k, world), or 0 when
+ * the compact form does not apply (world < 2, world * k > 8192, n_global >= 2^31).
+ * ebt_shard_list_width(k, world) = min(k, ceil(1.5 k / world) + 8): also the per-shard width of
+ * the floor all-gather (a shard's widest share of the global top k, with margin; a narrower
+ * floor is still a valid lower bound). */
+int64_t ebt_shard_list_width(int32_t k, int32_t world);
+int64_t ebt_shard_pack_cap(int64_t B, int32_t k, int32_t world, int64_t n_global);
+size_t ebt_shard_pack_bytes(int64_t B, int64_t cap);
+int ebt_shard_pack(const double* scores, const int64_t* rows, int64_t B, int32_t k,
+                   const double* t_floor, int64_t cap, void* send, void* stream);
+int ebt_merge_packed(const void* recv, int32_t R, int64_t B, int32_t k, int64_t cap,
+                     double* out_scores, int64_t* out_rows, int32_t* incomplete, void* stream);
+
 /* Exact screen: scores[b*ld_scores + j] = (float)((q64_b . c_j) / gnorm64_j) in float64
  * arithmetic for every row j < n_rows (no replacement in the reference: the fallback screen of
  * EBT_FLAG_EXACT, whose only error is the final f32 rounding). */
@@ -370,15 +395,22 @@ int ebt_cosine_topk_finish(ebt_pending* pending);
  * inside the library, for a host without Python: every rank holds one shard (an ebt_catalog
  * whose row_offset is the shard's first GLOBAL row) and calls ebt_cosine_topk_sharded with the
  * same queries, k and exclusions; every rank returns the same GLOBAL top-k, equal to
- * ebt_cosine_topk over the whole catalog (rows bit-exact, float64 scores). Per batch:
+ * ebt_cosine_topk over the whole catalog (rows bit-exact, float64 scores). For liked queries
+ * that holds when each user's liked rows are listed in ascending order (the order
+ * lib.user_query_lists produces): the shards' partial sums are added in rank order, which is
+ * then the single-GPU order of additions; an unsorted list gives the same query up to float64
+ * round-off of its sum (near-tied rows may then swap). Per batch:
  *   query prep (liked rows: each shard sums its own, one all-gather of the [B][d] float64
  *   partial sums completes the means); when the shards are small (<= 200K rows, >= 2 ranks, the
  *   fused screen) a catalog-wide screening threshold from every shard's sample maxima (one
  *   all-gather); the shard's screen; the catalog-wide floor of the k-th exact score (one
  *   all-gather of [B][k+1] float32) so each shard rescores only rows that can enter the global
- *   top k; the float64 rescore + certificate; the local retries (no collective: every rank
- *   issues the same all-gathers in the same order whatever its retries); two all-gathers of the
- *   shard results ([B][k] float64 scores, int64 rows) and the merge (ebt_merge_topk).
+ *   top k (each shard sends its ebt_shard_list_width best approx, [B][w+1] float32); the
+ *   float64 rescore + certificate; the local retries (no collective: every rank issues the same
+ *   all-gathers in the same order whatever its retries); one all-gather of the shards' entries
+ *   above that floor (ebt_shard_pack: int32 rows behind per-query starts) and the merge
+ *   (ebt_merge_packed) -- or, when the compact form does not apply or a rank's entries exceed
+ *   its capacity, two all-gathers of the full [B][k] lists and ebt_merge_topk.
  * The caller supplies the collective, an all-gather over its communicator:
  *   all_gather(ctx, send, recv, bytes, stream): recv (device, world * bytes) receives every
  *   rank's `bytes` from send (device) in rank order. It is called after the work producing
@@ -389,8 +421,7 @@ int ebt_cosine_topk_finish(ebt_pending* pending);
  *   then left in their next all_gather: the caller's collective timeout must end them).
  * Limits: k <= 4096 (the merge); B, k, the queries and the exclusions equal on every rank
  * (argument errors are then detected alike everywhere before the first collective). The call
- * returns when the results are final (the stream is synchronised once per retry round and at
- * the end). Workspace: ebt_sharded_workspace_bytes (device). */
+ * returns when the results are final. Workspace: ebt_sharded_workspace_bytes (device). */
 typedef int (*ebt_allgather_fn)(void* ctx, const void* send, void* recv, size_t bytes,
                                 void* stream);
 typedef struct ebt_comm {
@@ -399,8 +430,51 @@ typedef struct ebt_comm {
   ebt_allgather_fn all_gather;
   void* ctx;
 } ebt_comm;
+/* An RCCL communicator for an ebt_comm: the library opens librccl.so.1 at first use (it does not
+ * link it). Rank 0 calls ebt_rccl_unique_id (128 bytes) and hands the id to every rank out of
+ * band (e.g. a torch.distributed broadcast); each rank calls ebt_rccl_comm_init with its HIP
+ * device current; then comm.all_gather = ebt_rccl_all_gather, comm.ctx = the handle
+ * (ncclAllGather of `bytes` int8 on `stream`). EBT_EUNSUPPORTED when RCCL cannot be loaded. */
+int ebt_rccl_unique_id(void* id_out, size_t bytes);
+int ebt_rccl_comm_init(const void* id, int32_t rank, int32_t world, void** comm_out);
+int ebt_rccl_comm_destroy(void* comm);
+int ebt_rccl_all_gather(void* comm, const void* send, void* recv, size_t bytes, void* stream);
 size_t ebt_sharded_workspace_bytes(const ebt_catalog* cat, const ebt_comm* comm, int64_t B,
                                    int32_t k, const ebt_options* opt);
+/* The same in three calls, so that a caller can keep batches in flight (the collectives and
+ * the host's waits of one batch behind the GPU work of the next):
+ *   _submit enqueues query prep, the threshold and floor all-gathers, the screen, the rescore
+ *     and the certificates' copy to host[0 .. B] (caller's host memory, B + 2 int32; pinned
+ *     keeps the copy asynchronous) and fills *pending;
+ *   _finish waits for THAT batch's certificates, runs the shard's local retries, packs the
+ *     shard's entries above the catalog-wide floor (ebt_shard_pack), all-gathers them, merges
+ *     (ebt_merge_packed) into out_scores / out_rows on the stream and copies the merge's
+ *     "incomplete" flag to host[B + 1];
+ *   _wait waits for that flag (an event) and, when a rank's entries did not fit its packed
+ *     capacity, re-merges from the full lists (two more all-gathers: every rank sees the same
+ *     flag). The results are final when _wait returns.
+ * Every rank must make the same sequence of calls (each issues collectives). Workspace, host
+ * buffer and outputs belong to the batch until its _wait returns, so a pipelined caller cycles
+ * through (at least) three workspaces, e.g. per step: submit(i), finish(i-1), wait(i-2).
+ * ebt_cosine_topk_sharded = submit + finish + wait. */
+typedef struct ebt_sharded_pending {
+  ebt_pending local;  /* the shard's own first pass and retries */
+  ebt_comm comm;
+  double* out_scores;
+  int64_t* out_rows;
+  int32_t* host;
+  void* event;
+  int32_t stage;      /* 1 submitted, 2 finished, 0 done */
+} ebt_sharded_pending;
+int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm, const void* q,
+                                   int q_dtype, int64_t B, int64_t ldq,
+                                   const int64_t* liked_off, const int64_t* liked_rows,
+                                   int32_t k, const int64_t* excl_off, const int64_t* excl_rows,
+                                   const ebt_options* opt, void* workspace, size_t ws_bytes,
+                                   double* out_scores, int64_t* out_rows, int32_t* host,
+                                   ebt_sharded_pending* pending, void* timer, void* stream);
+int ebt_cosine_topk_sharded_finish(ebt_sharded_pending* pending);
+int ebt_cosine_topk_sharded_wait(ebt_sharded_pending* pending);
 int ebt_cosine_topk_sharded(const ebt_catalog* cat, const ebt_comm* comm, const void* q,
                             int q_dtype, int64_t B, int64_t ldq, const int64_t* liked_off,
                             const int64_t* liked_rows, int32_t k, const int64_t* excl_off,
@@ -466,6 +540,13 @@ int ebt_cosine_screen_at(const double* q64, const void* qimg, const float* qscal
  * (NaN counts as -inf): a lower bound of query b's k-th best exact score over the catalog. */
 int ebt_union_floor(const float* gathered, int32_t R, int64_t B, int32_t ld, int32_t k,
                     double* t_floor, void* stream);
+/* What a shard sends for that floor: out[b] = (the w largest of list_vals[b*ld + 0 .. n),
+ * n = min(k_eff, ld), -inf padded to w; then eps[b]) as [B][w + 1] float32. The list may be
+ * partitioned (any order): the w largest are selected. w = ebt_shard_list_width(k, world)
+ * narrows the gather: the k-th largest over a subset of the shards' values is still a lower
+ * bound, and with w >= a shard's share of the global top k it is the same bound. */
+int ebt_floor_pack(const float* list_vals, int64_t ld, int64_t B, int32_t k_eff, int32_t w,
+                   const float* eps, float* out, void* stream);
 /* cert[b] = -1 (rerun unfused) where ovf[b] != 0, or where theta (if not NULL) may have dropped
  * a global top-k row: !(theta[b] <= t_floor[b] - eps[b]); a -2 (corrupt list) stays. */
 int ebt_certify_cut(int32_t* cert, const int32_t* ovf, const float* theta,

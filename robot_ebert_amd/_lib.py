@@ -65,9 +65,17 @@ class EbtComm(ctypes.Structure):
                 ("all_gather", ALLGATHER_FN), ("ctx", _VP)]
 
 
+class EbtShardedPending(ctypes.Structure):
+    """include/ebert.h `ebt_sharded_pending`: a row-sharded batch in flight
+    (ebt_cosine_topk_sharded_submit / _finish / _wait)."""
+    _fields_ = [("local", EbtPending), ("comm", EbtComm), ("out_scores", _VP),
+                ("out_rows", _VP), ("host", _VP), ("event", _VP), ("stage", _I32)]
+
+
 _PCAT, _POPT, _PPEND = (ctypes.POINTER(EbtCatalog), ctypes.POINTER(EbtOptions),
                         ctypes.POINTER(EbtPending))
 _PCOMM = ctypes.POINTER(EbtComm)
+_PSPEND = ctypes.POINTER(EbtShardedPending)
 
 _SIGNATURES = {
     "ebt_catalog_state_bytes": ([_VP, _INT, _I64, _I32, _I64], _SZ),
@@ -81,6 +89,21 @@ _SIGNATURES = {
     "ebt_sharded_workspace_bytes": ([_PCAT, _PCOMM, _I64, _I32, _POPT], _SZ),
     "ebt_cosine_topk_sharded": ([_PCAT, _PCOMM, _VP, _INT, _I64, _I64, _VP, _VP, _I32, _VP, _VP,
                                  _POPT, _VP, _SZ, _VP, _VP, _VP, _VP], _INT),
+    "ebt_cosine_topk_sharded_submit": ([_PCAT, _PCOMM, _VP, _INT, _I64, _I64, _VP, _VP, _I32,
+                                        _VP, _VP, _POPT, _VP, _SZ, _VP, _VP, _VP, _PSPEND, _VP,
+                                        _VP], _INT),
+    "ebt_cosine_topk_sharded_finish": ([_PSPEND], _INT),
+    "ebt_cosine_topk_sharded_wait": ([_PSPEND], _INT),
+    "ebt_rccl_unique_id": ([_VP, _SZ], _INT),
+    "ebt_rccl_comm_init": ([_VP, _I32, _I32, ctypes.POINTER(_VP)], _INT),
+    "ebt_rccl_comm_destroy": ([_VP], _INT),
+    "ebt_rccl_all_gather": ([_VP, _VP, _VP, _SZ, _VP], _INT),
+    "ebt_shard_list_width": ([_I32, _I32], _I64),
+    "ebt_shard_pack_cap": ([_I64, _I32, _I32, _I64], _I64),
+    "ebt_shard_pack_bytes": ([_I64, _I64], _SZ),
+    "ebt_shard_pack": ([_VP, _VP, _I64, _I32, _VP, _I64, _VP, _VP], _INT),
+    "ebt_merge_packed": ([_VP, _I32, _I64, _I32, _I64, _VP, _VP, _VP, _VP], _INT),
+    "ebt_floor_pack": ([_VP, _I64, _I64, _I32, _I32, _VP, _VP, _VP], _INT),
     "ebt_version": ([], _INT),
     "ebt_last_error": ([], ctypes.c_char_p),
     "ebt_row_norms": ([_VP, _INT, _I64, _I32, _I64, _VP, _VP, _VP], _INT),

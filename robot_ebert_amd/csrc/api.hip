@@ -72,6 +72,7 @@ bool merge_wave_fits(int);
 int merge_wave_capacity();
 int merge_block_capacity(int);
 int64_t merge_wave_max_groups();
+int64_t merge_block_max_groups(int);
 int merge_segment_wave(float*, int64_t*, int64_t, int, int, const uint64_t*, int64_t, int,
                        const uint8_t*, int64_t, int64_t, int64_t, const int64_t*, const int64_t*,
                        int*, hipStream_t, const float* veps = nullptr,
@@ -425,7 +426,7 @@ using namespace ebt;
 
 extern "C" {
 
-int ebt_version(void) { return 100; }
+int ebt_version(void) { return 200; }  // 0.2.0: ebt_rescore gained `timer` (ABI break)
 
 const char* ebt_last_error(void) { return g_err; }
 
@@ -701,7 +702,8 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
     slots *= 2;
   const bool wave = merge_wave_fits(kprime);
   int64_t seg_cap = L.ld_cand / slots;
-  if (wave) seg_cap = seg_cap < merge_wave_max_groups() ? seg_cap : merge_wave_max_groups();
+  const int64_t max_groups = wave ? merge_wave_max_groups() : merge_block_max_groups(kprime);
+  seg_cap = seg_cap < max_groups ? seg_cap : max_groups;
   seg_cap *= L.group_rows;
   const double cap = (double)(wave ? merge_wave_capacity() : merge_block_capacity(kprime));
   // A query's hits are ~ Gamma(j) n / m around the expected H = j n / m (its threshold is the
@@ -858,8 +860,8 @@ static int run_screen(const PipeArgs& a, const WsLayout& L, char* ws, float* fv,
     if (n_rows - (r0 + seg) < seg / 2 && n_rows - r0 <= (grow + 1) * r0)
       seg = n_rows - r0;  // no small last segment
     int64_t seg_cap = L.ld_cand / slots * L.group_rows;
-    if (L.pilot && seg_cap > merge_wave_max_groups() * L.group_rows)
-      seg_cap = merge_wave_max_groups() * L.group_rows;
+    const int64_t max_groups = L.pilot ? merge_wave_max_groups() : merge_block_max_groups(kprime);
+    if (seg_cap > max_groups * L.group_rows) seg_cap = max_groups * L.group_rows;
     seg = seg < seg_cap ? seg : seg_cap;
     const int64_t groups = ceil_div(seg, L.group_rows);
     rc = kth_threshold(fv, kprime, B, B_pad, k, a.eps, thr, st);

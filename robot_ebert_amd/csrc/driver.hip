@@ -742,9 +742,11 @@ struct ShardLayout {
   DriverLayout D;
   int64_t tiles, G, RG;
   size_t screen_bytes;
+  int64_t fw, cap;  // floor gather width per shard and query; packed results per rank (0: full)
+  size_t pack_bytes;
   size_t off_spass, off_pool, off_gsamp, off_perm, off_theta, off_lv, off_lr, off_lloc, off_ovf,
       off_eps, off_fsend, off_frecv, off_tfloor, off_ls, off_lrr, off_gs, off_gr, off_scale,
-      off_qrecv, bytes;
+      off_qrecv, off_psend, off_precv, off_incomplete, bytes;
 };
 
 bool shard_layout(const ebt_catalog& c, const ebt_comm& cm, int64_t B, int32_t k,
@@ -800,10 +802,16 @@ bool shard_layout(const ebt_catalog& c, const ebt_comm& cm, int64_t B, int32_t k
   o = al(o + (size_t)B * 4);
   L.off_eps = o;
   o = al(o + (size_t)B * 4);
+  // the compact exchange (rescore.hip): each shard's w best approx for the floor, its entries
+  // above the floor for the results (int32 rows behind per-query starts)
+  L.fw = ebt_shard_list_width(k, (int32_t)R);
+  L.cap = ebt_shard_pack_cap(B, k, (int32_t)R, cm.n_global);
+  if (!L.cap) L.fw = k;
+  L.pack_bytes = L.cap ? ebt_shard_pack_bytes(B, L.cap) : 0;
   L.off_fsend = o;
-  o = al(o + (size_t)B * (k + 1) * 4);
+  o = al(o + (size_t)B * (L.fw + 1) * 4);
   L.off_frecv = o;
-  o = al(o + (size_t)R * B * (k + 1) * 4);
+  o = al(o + (size_t)R * B * (L.fw + 1) * 4);
   L.off_tfloor = o;
   o = al(o + (size_t)B * 8);
   L.off_ls = o;
@@ -818,21 +826,14 @@ bool shard_layout(const ebt_catalog& c, const ebt_comm& cm, int64_t B, int32_t k
   o = al(o + (size_t)B * 8);
   L.off_qrecv = o;
   o = al(o + (size_t)R * B * c.d * 8);  // the liked path's gathered partial sums
+  L.off_psend = o;
+  o = al(o + L.pack_bytes);
+  L.off_precv = o;
+  o = al(o + (size_t)R * L.pack_bytes);
+  L.off_incomplete = o;
+  o = al(o + 4);
   L.bytes = o;
   return true;
-}
-
-// fsend[b][0 .. k_req] = the shard's k_eff best approx scores, -inf up to k_req, then eps[b]
-__global__ void floor_pack_kernel(const float* __restrict__ lv, int kp, int k_eff, int k_req,
-                                  const float* __restrict__ eps, int64_t B,
-                                  float* __restrict__ out) {
-  const int64_t total = B * (k_req + 1);
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t b = t / (k_req + 1);
-    const int j = (int)(t - b * (k_req + 1));
-    out[t] = j == k_req ? eps[b] : (j < k_eff ? lv[b * kp + j] : -__builtin_inff());
-  }
 }
 
 // GLOBAL candidate rows -> rows of this shard (-1 stays empty)
@@ -933,6 +934,21 @@ int prep_liked_sharded(const ebt_catalog& c, const ebt_comm& cm, const int64_t* 
                          (float*)(base + P.eps), st);
 }
 
+// the full exchange: every shard's [B][k] exact list (f64 scores, i64 rows), ebt_merge_topk
+int sh_full_merge(const ShardLayout& S, const ebt_comm& cm, char* ws, int64_t B, int32_t k,
+                  double* out_s, int64_t* out_r, void* timer, hipStream_t st) {
+  double* ls = (double*)(ws + S.off_ls);
+  int64_t* lrr = (int64_t*)(ws + S.off_lrr);
+  double* gs = (double*)(ws + S.off_gs);
+  int64_t* gr = (int64_t*)(ws + S.off_gr);
+  int rc = sh_gather(cm, ls, gs, (size_t)B * k * 8, timer, st);
+  if (!rc) rc = sh_gather(cm, lrr, gr, (size_t)B * k * 8, timer, st);
+  if (rc) return rc;
+  if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SHARD_MERGE, st);
+  rc = ebt_merge_topk(gs, gr, cm.world, B, k, out_s, out_r, st);
+  if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SHARD_MERGE, st);
+  return rc;
+}
 }  // namespace
 }  // namespace ebt
 
@@ -946,16 +962,17 @@ size_t ebt_sharded_workspace_bytes(const ebt_catalog* cat, const ebt_comm* comm,
   return S.bytes;
 }
 
-int ebt_cosine_topk_sharded(const ebt_catalog* cat, const ebt_comm* comm, const void* q,
-                            int q_dtype, int64_t B, int64_t ldq, const int64_t* liked_off,
-                            const int64_t* liked_rows, int32_t k, const int64_t* excl_off,
-                            const int64_t* excl_rows, const ebt_options* opt, void* workspace,
-                            size_t ws_bytes, double* out_scores, int64_t* out_rows, void* timer,
-                            void* stream) {
+int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm, const void* q,
+                                   int q_dtype, int64_t B, int64_t ldq,
+                                   const int64_t* liked_off, const int64_t* liked_rows,
+                                   int32_t k, const int64_t* excl_off, const int64_t* excl_rows,
+                                   const ebt_options* opt, void* workspace, size_t ws_bytes,
+                                   double* out_scores, int64_t* out_rows, int32_t* host,
+                                   ebt_sharded_pending* pending, void* timer, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (!valid_catalog(cat) || !comm || !workspace || !out_scores || !out_rows || B < 1 ||
-      k < 1 || ((q == nullptr) == (liked_off == nullptr)) || (liked_off && !liked_rows) ||
-      ((excl_off == nullptr) != (excl_rows == nullptr)) ||
+  if (!valid_catalog(cat) || !comm || !workspace || !out_scores || !out_rows || !host ||
+      !pending || B < 1 || k < 1 || ((q == nullptr) == (liked_off == nullptr)) ||
+      (liked_off && !liked_rows) || ((excl_off == nullptr) != (excl_rows == nullptr)) ||
       (q && (q_dtype < 0 || q_dtype > 3 || ldq < cat->d))) {
     set_error("ebt_cosine_topk_sharded: bad arguments (B=%lld k=%d; pass exactly one of q / "
               "liked)", (long long)B, k);
@@ -1046,17 +1063,17 @@ int ebt_cosine_topk_sharded(const ebt_catalog* cat, const ebt_comm* comm, const 
                            L.flags, ws + S.off_spass, S.screen_bytes, lv, lr, ovf, eps, timer,
                            st);
   if (rc) return rc;
-  // 4. the catalog-wide floor: the k-th largest (approx - eps) over every shard
+  // 4. the catalog-wide floor: the k-th largest (approx - eps) over every shard's fw best
   float* fsend = (float*)(ws + S.off_fsend);
   float* frecv = (float*)(ws + S.off_frecv);
   double* tfloor = (double*)(ws + S.off_tfloor);
-  hipLaunchKernelGGL(floor_pack_kernel, dim3(grid_for(B * (k + 1))), dim3(256), 0, st, lv,
-                     L.kprime, L.k_eff, k, eps, B, fsend);
-  rc = launch_check("floor_pack_kernel");
-  if (!rc) rc = sh_gather(cm, fsend, frecv, (size_t)B * (k + 1) * 4, timer, st);
+  if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
+  rc = ebt_floor_pack(lv, L.kprime, B, L.k_eff, (int32_t)S.fw, eps, fsend, st);
+  if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
+  if (!rc) rc = sh_gather(cm, fsend, frecv, (size_t)B * (S.fw + 1) * 4, timer, st);
   if (rc) return rc;
   if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
-  rc = ebt_union_floor(frecv, R, B, k + 1, k, tfloor, st);
+  rc = ebt_union_floor(frecv, R, B, (int32_t)S.fw + 1, k, tfloor, st);
   if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
   if (rc) return rc;
   // 5. the rescore of the rows that can enter the global top k, the certificate
@@ -1086,11 +1103,9 @@ int ebt_cosine_topk_sharded(const ebt_catalog* cat, const ebt_comm* comm, const 
     rc = launch_check("csr_sorted_kernel");
     if (rc) return rc;
   }
-  // the local retries (ebt_cosine_topk_finish: unfused reruns, k' x 4, the float64 screen) on
-  // this shard alone: a retried query gets the shard's exact top k, which the merge accepts
-  std::vector<int32_t> cert_host((size_t)B + 1);
-  rc = hip_check(hipMemcpyAsync(cert_host.data(), cert, (size_t)(B + 1) * 4,
-                                hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+  // the certificates (and the exclusion flag) to the caller's host buffer; one event for them
+  rc = hip_check(hipMemcpyAsync(host, cert, (size_t)(B + 1) * 4, hipMemcpyDeviceToHost, st),
+                 "hipMemcpyAsync");
   if (rc) return rc;
   hipEvent_t ev;
   rc = hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
@@ -1100,37 +1115,132 @@ int ebt_cosine_topk_sharded(const ebt_catalog* cat, const ebt_comm* comm, const 
     (void)hipEventDestroy(ev);
     return rc;
   }
-  ebt_pending P{};
-  P.cat = cat;
-  P.opt = o;
-  P.B = B;
-  P.B_pad = L.B_pad;
-  P.chunk = L.chunk;
-  P.k = k;
-  P.k_eff = L.k_eff;
-  P.kprime = L.kprime;
-  P.excl_off = excl_off;
-  P.excl_rows = excl_rows;
-  P.ws = ws;
-  P.ws_bytes = ws_bytes;
-  P.out_scores = ls;
-  P.out_rows = lrr;
-  P.cert_host = cert_host.data();
-  P.event = ev;
-  P.timer = timer;
-  P.stream = stream;
-  rc = ebt_cosine_topk_finish(&P);
+  ebt_sharded_pending P{};
+  ebt_pending& lp = P.local;
+  lp.cat = cat;
+  lp.opt = o;
+  lp.B = B;
+  lp.B_pad = L.B_pad;
+  lp.chunk = L.chunk;
+  lp.k = k;
+  lp.k_eff = L.k_eff;
+  lp.kprime = L.kprime;
+  lp.excl_off = excl_off;
+  lp.excl_rows = excl_rows;
+  lp.ws = ws;
+  lp.ws_bytes = ws_bytes;
+  lp.out_scores = ls;
+  lp.out_rows = lrr;
+  lp.cert_host = host;
+  lp.event = ev;
+  lp.timer = timer;
+  lp.stream = stream;
+  P.comm = cm;
+  P.out_scores = out_scores;
+  P.out_rows = out_rows;
+  P.host = host;
+  P.event = nullptr;
+  P.stage = 1;
+  *pending = P;
+  return EBT_OK;
+}
+
+
+int ebt_cosine_topk_sharded_finish(ebt_sharded_pending* p) {
+  if (!p || p->stage != 1 || !p->local.cat) {
+    set_error("ebt_cosine_topk_sharded_finish: not a submitted batch");
+    return EBT_EINVAL;
+  }
+  ebt_pending& lp = p->local;
+  hipStream_t st = (hipStream_t)lp.stream;
+  ShardLayout S;
+  if (!shard_layout(*lp.cat, p->comm, lp.B, lp.k, lp.opt, &S)) {
+    set_error("ebt_cosine_topk_sharded_finish: bad pending batch");
+    return EBT_EINVAL;
+  }
+  // the local retries (ebt_cosine_topk_finish: unfused reruns, k' x 4, the float64 screen) on
+  // this shard alone: a retried query gets the shard's exact top k, which the merge accepts
+  int rc = ebt_cosine_topk_finish(&lp);
   if (rc) return rc;
-  // 6. every shard's exact top k, gathered and merged (the global answer on every rank)
-  double* gs = (double*)(ws + S.off_gs);
-  int64_t* gr = (int64_t*)(ws + S.off_gr);
-  rc = sh_gather(cm, ls, gs, (size_t)B * k * 8, timer, st);
-  if (!rc) rc = sh_gather(cm, lrr, gr, (size_t)B * k * 8, timer, st);
+  p->stage = 2;
+  char* ws = lp.ws;
+  const int64_t B = lp.B;
+  const int32_t k = lp.k;
+  void* timer = lp.timer;
+  p->host[B + 1] = 0;
+  if (S.cap) {
+    // 6. every shard's entries above the floor, packed (int32 rows), ONE all-gather, the merge
+    int32_t* incomplete = (int32_t*)(ws + S.off_incomplete);
+    rc = hip_check(hipMemsetAsync(incomplete, 0, 4, st), "hipMemsetAsync");
+    if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
+    if (!rc)
+      rc = ebt_shard_pack((const double*)(ws + S.off_ls), (const int64_t*)(ws + S.off_lrr), B, k,
+                          (const double*)(ws + S.off_tfloor), S.cap, ws + S.off_psend, st);
+    if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
+    if (!rc) rc = sh_gather(p->comm, ws + S.off_psend, ws + S.off_precv, S.pack_bytes, timer, st);
+    if (rc) return rc;
+    if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SHARD_MERGE, st);
+    rc = ebt_merge_packed(ws + S.off_precv, p->comm.world, B, k, S.cap, p->out_scores,
+                          p->out_rows, incomplete, st);
+    if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SHARD_MERGE, st);
+    if (!rc)
+      rc = hip_check(hipMemcpyAsync(p->host + B + 1, incomplete, 4, hipMemcpyDeviceToHost, st),
+                     "hipMemcpyAsync");
+  } else {
+    rc = sh_full_merge(S, p->comm, ws, B, k, p->out_scores, p->out_rows, timer, st);
+  }
   if (rc) return rc;
-  if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SHARD_MERGE, st);
-  rc = ebt_merge_topk(gs, gr, R, B, k, out_scores, out_rows, st);
-  if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SHARD_MERGE, st);
+  hipEvent_t ev;
+  rc = hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+  if (rc) return rc;
+  rc = hip_check(hipEventRecord(ev, st), "hipEventRecord");
+  if (rc) {
+    (void)hipEventDestroy(ev);
+    return rc;
+  }
+  p->event = ev;
+  return EBT_OK;
+}
+
+int ebt_cosine_topk_sharded_wait(ebt_sharded_pending* p) {
+  if (!p || p->stage != 2 || !p->event) {
+    set_error("ebt_cosine_topk_sharded_wait: not a finished batch");
+    return EBT_EINVAL;
+  }
+  ebt_pending& lp = p->local;
+  hipStream_t st = (hipStream_t)lp.stream;
+  hipEvent_t ev = (hipEvent_t)p->event;
+  int rc = hip_check(hipEventSynchronize(ev), "hipEventSynchronize");
+  (void)hipEventDestroy(ev);
+  p->event = nullptr;
+  p->stage = 0;
+  if (rc) return rc;
+  if (p->host[lp.B + 1] == 0) return EBT_OK;
+  // some rank's entries above the floor exceeded its packed capacity (every rank sees the same
+  // gathered starts, so every rank takes this branch): the full exchange
+  ShardLayout S;
+  if (!shard_layout(*lp.cat, p->comm, lp.B, lp.k, lp.opt, &S)) {
+    set_error("ebt_cosine_topk_sharded_wait: bad pending batch");
+    return EBT_EINVAL;
+  }
+  rc = sh_full_merge(S, p->comm, lp.ws, lp.B, lp.k, p->out_scores, p->out_rows, lp.timer, st);
   if (!rc) rc = hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+  return rc;
+}
+
+int ebt_cosine_topk_sharded(const ebt_catalog* cat, const ebt_comm* comm, const void* q,
+                            int q_dtype, int64_t B, int64_t ldq, const int64_t* liked_off,
+                            const int64_t* liked_rows, int32_t k, const int64_t* excl_off,
+                            const int64_t* excl_rows, const ebt_options* opt, void* workspace,
+                            size_t ws_bytes, double* out_scores, int64_t* out_rows, void* timer,
+                            void* stream) {
+  std::vector<int32_t> host((size_t)(B > 0 ? B : 0) + 2);
+  ebt_sharded_pending p{};
+  int rc = ebt_cosine_topk_sharded_submit(cat, comm, q, q_dtype, B, ldq, liked_off, liked_rows,
+                                          k, excl_off, excl_rows, opt, workspace, ws_bytes,
+                                          out_scores, out_rows, host.data(), &p, timer, stream);
+  if (!rc) rc = ebt_cosine_topk_sharded_finish(&p);
+  if (!rc) rc = ebt_cosine_topk_sharded_wait(&p);
   return rc;
 }
 

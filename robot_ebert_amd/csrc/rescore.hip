@@ -645,12 +645,39 @@ __device__ __forceinline__ bool mt_before(double xs, int64_t xr, double es, int6
 }
 
 size_t merge_corank_lds(int R, int P) {
-  return (size_t)P * 16 + RTHREADS * 16 + (((size_t)(2 * R + 1) * 4 + 15) & ~(size_t)15);
+  return (size_t)P * 16 + RTHREADS * 16 + (((size_t)(4 * R + 1) * 4 + 15) & ~(size_t)15);
 }
 
+// The lists' sources. DenseSrc: [R][B][k] f64 scores + i64 rows (row < 0 = padding).
+// PackedSrc: every rank's packed list of ebt_shard_pack (one all-gathered byte buffer, `stride`
+// bytes per rank): u32 starts[B + 1], then f64 scores[cap], then i32 rows[cap]; query b's
+// entries are [starts[b], starts[b + 1]) clipped to cap (the rest was not sent), the positions
+// past them padding.
+struct DenseSrc {
+  const double* scores;
+  const int64_t* rows;
+  static constexpr bool packed = false;
+};
+struct PackedSrc {
+  const char* recv;
+  int64_t stride, cap;
+  static constexpr bool packed = true;
+};
+
+__device__ __forceinline__ const uint32_t* pk_starts(const PackedSrc& p, int r) {
+  return (const uint32_t*)(p.recv + (int64_t)r * p.stride);
+}
+__device__ __forceinline__ const double* pk_scores(const PackedSrc& p, int r, int64_t B) {
+  return (const double*)(p.recv + (int64_t)r * p.stride + shard_pack_hdr_bytes(B));
+}
+__device__ __forceinline__ const int32_t* pk_rows(const PackedSrc& p, int r, int64_t B) {
+  return (const int32_t*)(p.recv + (int64_t)r * p.stride + shard_pack_hdr_bytes(B) + p.cap * 8);
+}
+
+template <class Src>
 __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
-    const double* __restrict__ scores, const int64_t* __restrict__ rows, int R, int64_t B, int k,
-    int P, double* __restrict__ out_s, int64_t* __restrict__ out_r) {
+    const Src src, int R, int64_t B, int k, int P, double* __restrict__ out_s,
+    int64_t* __restrict__ out_r, int32_t* __restrict__ incomplete) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = R * k;
   double* sc = (double*)smem;
@@ -660,6 +687,21 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
   int* plen = (int*)(red_r + RTHREADS / 2);
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x;
+  // packed lists: each rank's start and length for this query (LDS, after plen / cst); a list
+  // cut by its rank's capacity makes the query incomplete (the caller then merges the full lists)
+  int* pst = plen + 2 * R + 1;
+  int* pcn = pst + R;
+  if constexpr (Src::packed) {
+    for (int r = tid; r < R; r += RTHREADS) {
+      const uint32_t* st = pk_starts(src, r);
+      const int64_t s0 = st[b], s1 = st[b + 1];
+      const int64_t a = s0 < src.cap ? s0 : src.cap, e = s1 < src.cap ? s1 : src.cap;
+      pst[r] = (int)a;
+      pcn[r] = (int)(e - a < k ? e - a : k);
+      if (s1 > src.cap || s1 - s0 > k) incomplete[0] = 1;
+    }
+    __syncthreads();
+  }
   // four entries per thread in flight (a loop over e would wait for each load in turn: the
   // compiler peels the trip count's remainder into a serial loop)
   for (int e0 = tid; e0 < n; e0 += 4 * RTHREADS) {
@@ -670,9 +712,18 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
       const int e = e0 + u * RTHREADS;
       const int ec = e < n ? e : n - 1;
       const int rr = ec / k, j = ec - rr * k;
-      const int64_t off = ((int64_t)rr * B + b) * k + j;
-      rv[u] = rows[off];
-      sv[u] = scores[off];
+      if constexpr (Src::packed) {
+        // a clamped index loaded unconditionally, masked afterwards (all loads in flight)
+        int64_t ix = (int64_t)pst[rr] + (j < pcn[rr] ? j : 0);
+        ix = ix < src.cap ? ix : src.cap - 1;
+        rv[u] = pk_rows(src, rr, B)[ix];
+        sv[u] = pk_scores(src, rr, B)[ix];
+        if (j >= pcn[rr]) rv[u] = -1;
+      } else {
+        const int64_t off = ((int64_t)rr * B + b) * k + j;
+        rv[u] = src.rows[off];
+        sv[u] = src.scores[off];
+      }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -877,10 +928,10 @@ int merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, 
   if (R > 1 && R <= MERGE_CORANK_RMAX && n <= MERGE_CORANK_CAP) {
     const int P = next_pow2_h((int)n);
     const size_t lds = merge_corank_lds(R, P);
-    (void)hipFuncSetAttribute((const void*)merge_topk_corank_kernel,
+    (void)hipFuncSetAttribute((const void*)merge_topk_corank_kernel<DenseSrc>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(merge_topk_corank_kernel, dim3((unsigned)B), dim3(RTHREADS), lds, st,
-                       scores, rows, R, B, k, P, out_s, out_r);
+    hipLaunchKernelGGL(merge_topk_corank_kernel<DenseSrc>, dim3((unsigned)B), dim3(RTHREADS),
+                       lds, st, DenseSrc{scores, rows}, R, B, k, P, out_s, out_r, nullptr);
     return launch_check("merge_topk_corank_kernel");
   }
   const int P = next_pow2_h((int)(n < MERGE_CAP ? n : MERGE_CAP));
@@ -891,6 +942,97 @@ int merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, 
   return launch_check("merge_topk_kernel");
 }
 
+// ------------------------------------------------------------------------ compact exchange --
+// ebt_shard_pack: per query the prefix of its sorted exact list with score >= t_floor[b] (a
+// lower bound of the k-th best exact score over the whole catalog: every global top-k entry is
+// in it), packed behind per-query starts. Two launches: (1) one thread per query counts its
+// prefix (binary search: the predicate "real row and score >= floor" holds on a prefix of a
+// sorted list), a workgroup scan gives the starts within its 256 queries and its total;
+// (2) each workgroup adds the totals of the workgroups before it, writes the global starts and
+// copies its entries (one per thread, the owning query found by binary search in LDS).
+__global__ __launch_bounds__(SHARD_PACK_QPB) void shard_pack_count_kernel(
+    const double* __restrict__ scores, const int64_t* __restrict__ rows, int64_t B, int k,
+    const double* __restrict__ t_floor, uint32_t* __restrict__ hdr) {
+  __shared__ int wsum[SHARD_PACK_QPB / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = (int64_t)blockIdx.x * SHARD_PACK_QPB + tid;
+  int cnt = 0;
+  if (b < B) {
+    const double tf = t_floor ? t_floor[b] : -__builtin_inf();
+    const double* sr = scores + b * k;
+    const int64_t* rr = rows + b * k;
+    int lo = 0, hi = k;  // the first position failing the predicate
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (rr[mid] >= 0 && sr[mid] >= tf) lo = mid + 1;
+      else hi = mid;
+    }
+    cnt = lo;
+  }
+  int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  int base = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < SHARD_PACK_QPB / 64; ++w) {
+    base += w < wave ? wsum[w] : 0;
+    total += wsum[w];
+  }
+  if (b < B) hdr[b] = (uint32_t)(base + incl - cnt);  // start within the workgroup
+  if (tid == 0) hdr[B + 1 + blockIdx.x] = (uint32_t)total;
+}
+
+__global__ __launch_bounds__(SHARD_PACK_QPB) void shard_pack_copy_kernel(
+    const double* __restrict__ scores, const int64_t* __restrict__ rows, int64_t B, int k,
+    int64_t cap, char* __restrict__ send) {
+  __shared__ uint32_t lst[SHARD_PACK_QPB + 1];
+  __shared__ uint32_t gbase;
+  uint32_t* hdr = (uint32_t*)send;
+  double* os = (double*)(send + shard_pack_hdr_bytes(B));
+  int32_t* orow = (int32_t*)(send + shard_pack_hdr_bytes(B) + cap * 8);
+  const int tid = threadIdx.x;
+  const int64_t q0 = (int64_t)blockIdx.x * SHARD_PACK_QPB;
+  const int nq = B - q0 < SHARD_PACK_QPB ? (int)(B - q0) : SHARD_PACK_QPB;
+  const uint32_t* tot = hdr + B + 1;
+  if (tid < 64) {  // the totals of the workgroups before this one
+    uint32_t s = 0;
+    for (int i = tid; i < (int)blockIdx.x; i += 64) s += tot[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (tid == 0) gbase = s;
+  }
+  if (tid < nq) lst[tid] = hdr[q0 + tid];
+  if (tid == 0) lst[nq] = tot[blockIdx.x];
+  __syncthreads();
+  const uint32_t g0 = gbase, n = lst[nq];
+  if (tid < nq) hdr[q0 + tid] = g0 + lst[tid];
+  if (blockIdx.x == gridDim.x - 1 && tid == 0) hdr[B] = g0 + n;
+  for (uint32_t t = tid; t < n; t += SHARD_PACK_QPB) {
+    int lo = 0, hi = nq - 1;  // the last query whose start <= t
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (lst[mid] <= t) lo = mid;
+      else hi = mid - 1;
+    }
+    const int64_t b = q0 + lo, j = t - lst[lo], pos = (int64_t)g0 + t;
+    if (pos < cap) {
+      os[pos] = scores[b * k + j];
+      orow[pos] = (int32_t)rows[b * k + j];
+    }
+  }
+}
+
+int64_t shard_list_width(int32_t k, int32_t world) {
+  const int64_t w = (3 * (int64_t)k + 2 * world - 1) / (2 * world) + 8;  // ceil(1.5 k / R) + 8
+  return w < k ? w : k;
+}
+
+// ---------------------------------------------------------------------------------------------
 // ---------------------------------------------------------------------------------------------
 // Exact screen (EBT_FLAG_EXACT): S[b][j] = (float)((q64_b . c_j) / gnorm64_j), the rescore's own
 // float64 arithmetic rounded once to f32, for every row of a chunk. This is the last-resort
@@ -1384,4 +1526,164 @@ extern "C" int ebt_certify_cut(int32_t* cert, const int32_t* ovf, const float* t
   hipLaunchKernelGGL(certify_cut_kernel, dim3((unsigned)ceil_div(B, 256)), dim3(256), 0,
                      (hipStream_t)stream, cert, ovf, theta, t_floor, eps, B);
   return launch_check("certify_cut_kernel");
+}
+
+extern "C" int64_t ebt_shard_list_width(int32_t k, int32_t world) {
+  if (k < 1 || world < 1) return 0;
+  return ebt::shard_list_width(k, world);
+}
+
+extern "C" int64_t ebt_shard_pack_cap(int64_t B, int32_t k, int32_t world, int64_t n_global) {
+  using namespace ebt;
+  // the packed merge holds R k entries in LDS; rows travel as int32
+  if (B < 1 || k < 1 || world < 2 || world > MERGE_CORANK_RMAX ||
+      (int64_t)world * k > MERGE_CORANK_CAP || n_global >= (1LL << 31))
+    return 0;
+  const int64_t cap = B * shard_list_width(k, world);
+  return cap < (1LL << 31) ? cap : 0;
+}
+
+extern "C" size_t ebt_shard_pack_bytes(int64_t B, int64_t cap) {
+  if (B < 1 || cap < 1) return 0;
+  return (size_t)((ebt::shard_pack_hdr_bytes(B) + cap * 12 + 255) & ~(int64_t)255);
+}
+
+extern "C" int ebt_shard_pack(const double* scores, const int64_t* rows, int64_t B, int32_t k,
+                              const double* t_floor, int64_t cap, void* send, void* stream) {
+  using namespace ebt;
+  if (!scores || !rows || !send || B < 1 || B >= (1LL << 31) || k < 1 || cap < 1 ||
+      cap >= (1LL << 31)) {
+    set_error("ebt_shard_pack: bad arguments (B=%lld k=%d cap=%lld)", (long long)B, k,
+              (long long)cap);
+    return EBT_EINVAL;
+  }
+  const hipStream_t st = (hipStream_t)stream;
+  const unsigned grid = (unsigned)ceil_div(B, SHARD_PACK_QPB);
+  hipLaunchKernelGGL(shard_pack_count_kernel, dim3(grid), dim3(SHARD_PACK_QPB), 0, st, scores,
+                     rows, B, k, t_floor, (uint32_t*)send);
+  int rc = launch_check("shard_pack_count_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(shard_pack_copy_kernel, dim3(grid), dim3(SHARD_PACK_QPB), 0, st, scores, rows,
+                     B, k, cap, (char*)send);
+  return launch_check("shard_pack_copy_kernel");
+}
+
+extern "C" int ebt_merge_packed(const void* recv, int32_t R, int64_t B, int32_t k, int64_t cap,
+                                double* out_scores, int64_t* out_rows, int32_t* incomplete,
+                                void* stream) {
+  using namespace ebt;
+  if (!recv || !out_scores || !out_rows || !incomplete || R < 1 || R > MERGE_CORANK_RMAX ||
+      B < 1 || k < 1 || cap < 1 || (int64_t)R * k > MERGE_CORANK_CAP) {
+    set_error("ebt_merge_packed: bad arguments (R=%d B=%lld k=%d cap=%lld; R k <= %d)", R,
+              (long long)B, k, (long long)cap, MERGE_CORANK_CAP);
+    return EBT_EINVAL;
+  }
+  const int P = next_pow2_h(R * k);
+  const size_t lds = merge_corank_lds(R, P);
+  (void)hipFuncSetAttribute((const void*)merge_topk_corank_kernel<PackedSrc>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const PackedSrc src{(const char*)recv, (int64_t)ebt_shard_pack_bytes(B, cap), cap};
+  hipLaunchKernelGGL(merge_topk_corank_kernel<PackedSrc>, dim3((unsigned)B), dim3(RTHREADS), lds,
+                     (hipStream_t)stream, src, R, B, k, P, out_scores, out_rows, incomplete);
+  return launch_check("merge_topk_corank_kernel");
+}
+
+// ------------------------------------------------------------------------ floor all-gather --
+// ebt_floor_pack: out[b] = (the w largest of lv[b][0 .. n), n = min(k_eff, ld), then eps[b]) as
+// [B][w + 1] f32 -- what each shard sends for the catalog-wide floor. The list may be
+// partitioned (the wave merge's [0, k-1) in any order), so the w largest are selected: one wave
+// per query, order-preserving keys in registers, the w-th largest key by bisection (ballot
+// counts), then the keys above it and as many equal to it as fit, compacted by ballot prefix.
+// Only the multiset of values matters to ebt_union_floor, so ties at the cut may go either way.
+namespace ebt {
+template <int PL>
+__global__ __launch_bounds__(256) void floor_pack_kernel(const float* __restrict__ lv, int64_t ld,
+                                                         int64_t B, int n, int w,
+                                                         const float* __restrict__ eps,
+                                                         float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float* src = lv + b * ld;
+  float* dst = out + b * (w + 1);
+  uint32_t key[PL];
+#pragma unroll
+  for (int e = 0; e < PL; ++e) {  // clamped loads, all in flight, masked afterwards
+    const int j = lane + 64 * e;
+    const float v = n > 0 ? src[j < n ? j : n - 1] : 0.f;
+    key[e] = j < n ? f2key(v) : 0u;
+  }
+  uint32_t t = 0u;  // the w-th largest key (0: fewer than w valid values)
+  if (n > w) {
+    uint32_t mn = ~0u, mx = 0u;
+#pragma unroll
+    for (int e = 0; e < PL; ++e) {
+      if (key[e]) mn = key[e] < mn ? key[e] : mn;
+      mx = key[e] > mx ? key[e] : mx;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint32_t a = __shfl_xor(mn, o, 64), c = __shfl_xor(mx, o, 64);
+      mn = a < mn ? a : mn;
+      mx = c > mx ? c : mx;
+    }
+    auto count_ge = [&](uint32_t x) {
+      int c = 0;
+#pragma unroll
+      for (int e = 0; e < PL; ++e) c += __popcll(__ballot(key[e] >= x));
+      return c;
+    };
+    mn = __builtin_amdgcn_readfirstlane(mn);
+    mx = __builtin_amdgcn_readfirstlane(mx);
+    if (count_ge(mn) >= w) {  // else fewer than w valid values: t = 0
+      uint32_t lo = mn, hi = mx;  // invariant: count_ge(lo) >= w
+      while (lo < hi) {
+        const uint32_t mid = lo + ((hi - lo) >> 1) + 1u;
+        if (count_ge(mid) >= w) lo = mid;
+        else hi = mid - 1u;
+      }
+      t = lo;
+    }
+  }
+  // keys > t first, then keys == t (t > 0), at most w in all; -inf past them
+  int base = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int e = 0; e < PL; ++e) {
+      const bool pick = key[e] != 0u && (pass == 0 ? (n <= w || key[e] > t) : (n > w && t != 0u && key[e] == t));
+      const uint64_t m = __ballot(pick);
+      const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (pick && pos < w) dst[pos] = key2f(key[e]);
+      base += __popcll(m);
+    }
+  }
+  for (int j = (base < w ? base : w) + lane; j < w; j += 64) dst[j] = -__builtin_inff();
+  if (lane == 0) dst[w] = eps[b];
+}
+}  // namespace ebt
+
+extern "C" int ebt_floor_pack(const float* list_vals, int64_t ld, int64_t B, int32_t k_eff,
+                              int32_t w, const float* eps, float* out, void* stream) {
+  using namespace ebt;
+  if (!list_vals || !eps || !out || B < 0 || ld < 1 || k_eff < 0 || w < 1 || k_eff > 4096) {
+    set_error("ebt_floor_pack: bad arguments (ld=%lld k_eff=%d w=%d; k_eff <= 4096)",
+              (long long)ld, k_eff, w);
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  const int n = k_eff < ld ? k_eff : (int)ld;
+  const hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)ceil_div(B, 4)), blk(256);
+  if (n < 1) {  // nothing valid: -inf everywhere, then eps (PL = 1 over an empty list)
+    hipLaunchKernelGGL((floor_pack_kernel<1>), grid, blk, 0, st, list_vals, ld, B, 0, w, eps, out);
+    return launch_check("floor_pack_kernel");
+  }
+  if (n <= 64 * 4)
+    hipLaunchKernelGGL((floor_pack_kernel<4>), grid, blk, 0, st, list_vals, ld, B, n, w, eps, out);
+  else if (n <= 64 * 16)
+    hipLaunchKernelGGL((floor_pack_kernel<16>), grid, blk, 0, st, list_vals, ld, B, n, w, eps, out);
+  else
+    hipLaunchKernelGGL((floor_pack_kernel<64>), grid, blk, 0, st, list_vals, ld, B, n, w, eps, out);
+  return launch_check("floor_pack_kernel");
 }

@@ -485,6 +485,9 @@ int select_topk(const float* vals, const int64_t* idx, int64_t ld, int64_t B, in
 // the LDS holds sets ovf[b]: the query's certificate becomes -1 and it is rerun unfused.
 // ---------------------------------------------------------------------------------------------
 constexpr int MERGE_MAX = 16384;  // LDS entries (128 KiB)
+// dynamic LDS a merge workgroup may take: 160 KiB less the kernel's static LDS (its wsum / flag
+// words and the bitonic sort's: 288 bytes on gfx950 -- read from the kernel, merge_lds_dyn())
+constexpr size_t MERGE_LDS_CU = 160 * 1024;
 constexpr int MERGE_DEFER = 1 << 4;  // ovf bit: the query waits for the full-size merge
 
 static int merge_entries(int kprime) {
@@ -710,22 +713,26 @@ __global__ __launch_bounds__(STHREADS) void merge_segment_kernel(
   }
 }
 
-int merge_segment(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t* cand,
-                  int64_t ld_cand, int slots, const uint8_t* counts, int64_t ld_counts,
-                  int64_t n_groups,
-                  int64_t row_offset, const int64_t* eo, const int64_t* er, int* ovf,
-                  hipStream_t st, double expect_hits) {
-  if (B < 0 || B > 0x7fffffffLL || kprime < 1 || kprime > KPRIME_MAX || n_groups < 1 ||
-      n_groups > 0x7fffffffLL || ld_counts < n_groups ||
-      ld_cand < n_groups * slots) {
-    set_error("merge_segment: bad arguments");
-    return EBT_EINVAL;
-  }
-  if (B == 0) return EBT_OK;
+size_t merge_lds_dyn() {
+  static size_t dyn = [] {
+    hipFuncAttributes a{};
+    size_t st = 1024;  // a safe static estimate if the attributes cannot be read
+    if (hipFuncGetAttributes(&a, (const void*)merge_segment_kernel) == hipSuccess)
+      st = (a.sharedSizeBytes + 15) & ~(size_t)15;
+    return MERGE_LDS_CU - st;
+  }();
+  return dyn;
+}
+
+static int merge_segment_part(float* fv, int64_t* fi, int64_t B, int kprime,
+                              const uint64_t* cand, int64_t ld_cand, int slots,
+                              const uint8_t* counts, int64_t ld_counts, int64_t n_groups,
+                              int64_t row_offset, const int64_t* eo, const int64_t* er, int* ovf,
+                              hipStream_t st, double expect_hits) {
   const int P_max = merge_entries(kprime);
   // LDS: the P entries, then the u16 group positions (n_groups + 1)
   const size_t gb_bytes = ((size_t)(n_groups + 1) * 2 + 15) & ~(size_t)15;
-  if ((size_t)P_max * 8 + gb_bytes > 160 * 1024) {
+  if ((size_t)P_max * 8 + gb_bytes > merge_lds_dyn()) {
     set_error("merge_segment: %lld groups do not fit the LDS", (long long)n_groups);
     return EBT_EINVAL;
   }
@@ -765,6 +772,35 @@ int merge_segment(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t*
                      (size_t)P_max * 8 + gb_bytes, st, fv, fi, kprime, cand, ld_cand, slots,
                      counts, ld_counts, (int)n_groups, P_max, row_offset, eo, er, ovf, 0, B);
   return launch_check("merge_segment_kernel");
+}
+
+int64_t merge_block_max_groups(int kprime);
+
+// More groups than one block merge can index (its u16 group positions share the LDS with the
+// P_max entries): merge them in consecutive parts of whole 16-group blocks. Each part merges
+// the list with the hits of its groups, so the parts together give the k' best of the list and
+// every hit -- the same (key, row) composites, hence the same list, as one merge.
+int merge_segment(float* fv, int64_t* fi, int64_t B, int kprime, const uint64_t* cand,
+                  int64_t ld_cand, int slots, const uint8_t* counts, int64_t ld_counts,
+                  int64_t n_groups,
+                  int64_t row_offset, const int64_t* eo, const int64_t* er, int* ovf,
+                  hipStream_t st, double expect_hits) {
+  if (B < 0 || B > 0x7fffffffLL || kprime < 1 || kprime > KPRIME_MAX || n_groups < 1 ||
+      n_groups > 0x7fffffffLL || ld_counts < n_groups ||
+      ld_cand < n_groups * slots) {
+    set_error("merge_segment: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (B == 0) return EBT_OK;
+  const int64_t part = merge_block_max_groups(kprime) & ~(int64_t)15;
+  for (int64_t g0 = 0; g0 < n_groups; g0 += part) {
+    const int64_t ng = n_groups - g0 < part ? n_groups - g0 : part;
+    const int rc = merge_segment_part(fv, fi, B, kprime, cand + g0 * slots, ld_cand, slots,
+                                      counts + g0, ld_counts, ng, row_offset, eo, er, ovf, st,
+                                      expect_hits * (double)ng / (double)n_groups);
+    if (rc) return rc;
+  }
+  return EBT_OK;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1076,6 +1112,11 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
 bool merge_wave_fits(int kprime) { return kprime <= WMERGE_K; }
 // entries the block merge holds (list + hits) for this k'
 int merge_block_capacity(int kprime) { return merge_entries(kprime); }
+// groups one block merge can index: its LDS holds the P_max entries, then the u16 group
+// positions (n_groups + 1, rounded to 16 bytes) -- merge_segment's own limit
+int64_t merge_block_max_groups(int kprime) {
+  return (int64_t)(merge_lds_dyn() - (size_t)merge_entries(kprime) * 8) / 2 - 8;
+}
 int64_t merge_wave_max_groups() { return 64 * 16 * WCNT; }
 int merge_wave_capacity() { return WTOP_N; }
 

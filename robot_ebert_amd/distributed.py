@@ -218,10 +218,31 @@ def _gather_start(coll, t: torch.Tensor):
     return lambda: g
 
 
+def shard_list_width(k: int, world: int) -> int:
+    """min(k, ceil(1.5 k / world) + 8): the entries per query a shard sends for the floor (its
+    widest expected share of the global top k, with margin), and the packed results' capacity
+    per query (include/ebert.h ebt_shard_list_width)."""
+    return int(_lib.load().ebt_shard_list_width(k, world))
+
+
+def floor_send(vals: torch.Tensor, eps: torch.Tensor, w: int) -> torch.Tensor:
+    """[B, w + 1] f32: the w largest of each row of vals (a partitioned list is fine), -inf
+    padded, then eps (ebt_floor_pack)."""
+    B, ld = vals.shape
+    vals = vals.contiguous()
+    out = torch.empty((B, w + 1), dtype=torch.float32, device=vals.device)
+    call("ebt_floor_pack", ptr(vals), ld, B, ld, w, ptr(eps.contiguous()), ptr(out),
+         stream_of(vals.device))
+    return out
+
+
 def _gathered_floor(coll, vals: torch.Tensor, eps: torch.Tensor, k: int, timer=None):
-    """union_floor over every shard's (k best approx, eps), in ONE all-gather ([B, k+1] f32);
-    returns a future (the gather runs while the caller enqueues other work)."""
-    wait = _gather_start(coll, torch.cat([vals, eps[:, None]], 1))
+    """union_floor over every shard's (w best approx, eps), w = shard_list_width(k, R), in ONE
+    all-gather ([B, w+1] f32; the k-th largest over a subset of the values is still a lower
+    bound); returns a future (the gather runs while the caller enqueues other work)."""
+    with region(timer, "small", vals.device):
+        send = floor_send(vals, eps, shard_list_width(k, coll.world))
+    wait = _gather_start(coll, send)
     dev = vals.device
 
     def floor():
@@ -356,48 +377,310 @@ def score_topk_sharded_local_stages(catalog: Catalog, k: int,
 def score_topk_sharded_local_finish(sub) -> Tuple[torch.Tensor, torch.Tensor]:
     """Complete a submitted batch: its retries (local), the all-gather of the per-shard exact
     top-k and the merge."""
-    return score_topk_sharded_local_finish_start(sub)()
+    return score_topk_sharded_local_finish_start(sub)().settle()
+
+
+class ShardMerged:
+    """A merged batch whose packed exchange may still need the full one: ``settle()`` waits for
+    the merge's "incomplete" flag (an event) and, when some rank's entries above the floor did
+    not fit its packed capacity, all-gathers the full [B, k] lists and merges again (every rank
+    sees the same flag, so every rank issues the same collectives). Returns (scores, rows)."""
+
+    def __init__(self, out_s, out_r, flag_host=None, event=None, full=None, coll=None, k=0,
+                 timer=None):
+        self.out_s, self.out_r = out_s, out_r
+        self._flag, self._event, self._full = flag_host, event, full
+        self._coll, self._k, self._timer = coll, k, timer
+
+    def settle(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        if self._event is not None:
+            self._event.synchronize()
+            if int(self._flag[0]):
+                s, r = self._full
+                ws, wr = _gather_start(self._coll, s), _gather_start(self._coll, r)
+                gs, gr = ws(), wr()
+                fs, fr = merge_topk(gs, gr, self._k)
+                self.out_s.copy_(fs)
+                self.out_r.copy_(fr)
+            self._event = self._full = None
+        return self.out_s, self.out_r
+
+
+def pack_results(s: torch.Tensor, r: torch.Tensor, t_floor: Optional[torch.Tensor], world: int,
+                 n_global: int):
+    """(send buffer, cap) of ebt_shard_pack: a shard's entries with exact score >= t_floor
+    (int32 rows behind per-query starts), or None when the compact form does not apply."""
+    lib = _lib.load()
+    B, k = s.shape
+    cap = int(lib.ebt_shard_pack_cap(B, k, world, n_global))
+    if not cap:
+        return None
+    send = torch.empty(int(lib.ebt_shard_pack_bytes(B, cap)), dtype=torch.uint8, device=s.device)
+    call("ebt_shard_pack", ptr(s.contiguous()), ptr(r.contiguous()), B, k, ptr(t_floor), cap,
+         ptr(send), stream_of(s.device))
+    return send, cap
+
+
+def merge_packed(recv: torch.Tensor, world: int, B: int, k: int, cap: int):
+    """ebt_merge_packed over the all-gathered [R, bytes] packed lists: (scores, rows,
+    incomplete) with incomplete a device int32 [1]."""
+    dev = recv.device
+    out_s = torch.empty((B, k), dtype=torch.float64, device=dev)
+    out_r = torch.empty((B, k), dtype=torch.int64, device=dev)
+    inc = torch.zeros(1, dtype=torch.int32, device=dev)
+    call("ebt_merge_packed", ptr(recv.contiguous()), world, B, k, cap, ptr(out_s), ptr(out_r),
+         ptr(inc), stream_of(dev))
+    return out_s, out_r, inc
 
 
 def score_topk_sharded_local_finish_start(sub):
     """score_topk_sharded_local_finish up to STARTING the all-gather of the results; the
-    returned callable waits for it and merges (the stream then waits for the gather only from
-    that point)."""
+    returned callable waits for it, merges and returns a ShardMerged (settle() for the final
+    answer). The exchange is the compact one when it applies: each shard's entries above the
+    catalog-wide floor (pack_results), one all-gather, merge_packed."""
     pending, coll, k = sub
     s, r = score_topk_finish(pending)
-    ws, wr = _gather_start(coll, s), _gather_start(coll, r)
     timer = getattr(pending, "timer", None)
     dev = s.device
+    t_floor = getattr(pending, "t_floor", None)
+    packed = None
+    if t_floor is not None:
+        with region(timer, "small", dev):
+            packed = pack_results(s, r, t_floor, coll.world, pending.catalog.n_global)
+    if packed is None:
+        ws, wr = _gather_start(coll, s), _gather_start(coll, r)
 
-    def merge():
+        def merge():
+            with region(timer, "collective_wait", dev):
+                gs, gr = ws(), wr()
+            with region(timer, "shard_merge", dev):
+                return ShardMerged(*merge_topk(gs, gr, k))
+        return merge
+    send, cap = packed
+    wp = _gather_start(coll, send[None])
+
+    def merge_c():
         with region(timer, "collective_wait", dev):
-            gs, gr = ws(), wr()
+            g = wp()
         with region(timer, "shard_merge", dev):
-            return merge_topk(gs, gr, k)
-    return merge
+            out_s, out_r, inc = merge_packed(g, coll.world, s.shape[0], k, cap)
+        flag = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        flag.copy_(inc, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        return ShardMerged(out_s, out_r, flag, ev, (s, r), coll, k, timer)
+    return merge_c
 
 
 def run_sharded_steps(make_stages, n: int):
     """Drive n batches through score_topk_sharded_local_stages, two in flight: per step
     [stage 1 of i] [stage 3 of i-1] [stage 2 of i] [finish of i-1 up to its gather]
-    [merge of i-2]. make_stages() returns a fresh generator; returns the last batch's
-    (scores, rows)."""
+    [settle of i-3] [merge of i-2]. A merged batch is settled (ShardMerged.settle: its packed
+    exchange's completeness flag read) one step later, after a host wait that its merge precedes
+    on the stream, so the host never waits for the newest work. make_stages() returns a fresh
+    generator; returns the last batch's (scores, rows)."""
     if n < 1:
         return None
     prev = make_stages()
     next(prev)
     next(prev)
-    merge_prev, out = None, None
+    merge_prev, merged = None, None
     for _ in range(1, n):
         cur = make_stages()
         next(cur)                      # stage 1 of i: its threshold gather starts
         sub = next(prev)               # stage 3 of i-1: rescore (its floor gathered meanwhile)
         next(cur)                      # stage 2 of i: screen; its floor gather starts
         merge = score_topk_sharded_local_finish_start(sub)
+        if merged is not None:
+            merged.settle()
         if merge_prev is not None:
-            out = merge_prev()
+            merged = merge_prev()
         merge_prev, prev = merge, cur
     merge = score_topk_sharded_local_finish_start(next(prev))
+    if merged is not None:
+        merged.settle()
     if merge_prev is not None:
-        merge_prev()
-    return merge()
+        merge_prev().settle()
+    return merge().settle()
+
+
+# ------------------------------------------------------------------ the C ABI's sharded step --
+class RcclComm:
+    """An RCCL communicator owned by libebert (include/ebert.h ebt_rccl_*), for the C ABI's
+    row-sharded step: rank 0's unique id travels through the torch.distributed group (any
+    backend), every rank then joins with its HIP device current. ``comm(n_global)`` is the
+    ebt_comm whose all-gather is the library's own ncclAllGather (no Python per collective)."""
+
+    def __init__(self, group: Optional[dist.ProcessGroup] = None) -> None:
+        import ctypes
+        lib = _lib.load()
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        uid = ctypes.create_string_buffer(128)
+        if self.rank == 0:
+            call("ebt_rccl_unique_id", uid, 128)
+        obj = [uid.raw if self.rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        uid = ctypes.create_string_buffer(obj[0], 128)
+        h = ctypes.c_void_p()
+        call("ebt_rccl_comm_init", uid, self.rank, self.world, ctypes.byref(h))
+        self.handle = h.value
+        self._fn = ctypes.cast(lib.ebt_rccl_all_gather, _lib.ALLGATHER_FN)
+
+    def comm(self, n_global: int) -> "_lib.EbtComm":
+        return _lib.EbtComm(self.rank, self.world, n_global, self._fn, self.handle)
+
+    def close(self) -> None:
+        if self.handle:
+            _lib.load().ebt_rccl_comm_destroy(self.handle)
+            self.handle = None
+
+
+class TorchGatherComm:
+    """The same ebt_comm with the all-gather done by a Python callback over torch.distributed
+    (gloo on a one-GPU rehearsal, thread-simulated ranks in tests): the library's send / recv
+    pointers lie inside tensors registered here (the step's workspaces), which the callback
+    views and hands to ``coll.all_gather_into`` (or dist.all_gather_into_tensor)."""
+
+    def __init__(self, rank: int, world: int, group: Optional[dist.ProcessGroup] = None,
+                 gather=None) -> None:
+        self.rank, self.world, self.group = rank, world, group
+        self._gather = gather
+        self._bufs = []
+        self._fn = _lib.ALLGATHER_FN(self._callback)
+        self.error: Optional[BaseException] = None
+
+    def register(self, t: torch.Tensor) -> None:
+        self._bufs.append(t)
+
+    def _view(self, p: int, nbytes: int) -> torch.Tensor:
+        for t in self._bufs:
+            base = t.data_ptr()
+            size = t.numel() * t.element_size()
+            if base <= p and p + nbytes <= base + size:
+                return t.view(torch.uint8).view(-1)[p - base:p - base + nbytes]
+        raise EbertError(f"all-gather buffer {p:#x} (+{nbytes}) is not in a registered tensor")
+
+    def _callback(self, ctx, send, recv, nbytes, stream) -> int:
+        try:
+            import contextlib
+            s = self._view(send, nbytes)
+            r = self._view(recv, nbytes * self.world)
+            # the library's stream (NULL -- ctypes None -- is the device's default stream)
+            ctx = (torch.cuda.stream(torch.cuda.ExternalStream(stream, device=s.device))
+                   if stream else contextlib.nullcontext())
+            with ctx:
+                if self._gather is not None:
+                    self._gather(r, s)
+                else:
+                    dist.all_gather_into_tensor(r, s, group=self.group)
+            return 0
+        except BaseException as e:  # noqa: BLE001 -- surfaces as EBT_EHIP, kept for the caller
+            self.error = e
+            return -1
+
+    def comm(self, n_global: int) -> "_lib.EbtComm":
+        return _lib.EbtComm(self.rank, self.world, n_global, self._fn, None)
+
+    def close(self) -> None:
+        self._bufs = []
+
+
+class ShardedTopk:
+    """ebt_cosine_topk_sharded_submit / _finish / _wait (include/ebert.h) over one rank's shard:
+    the whole row-sharded step inside libebert, batches in flight. ``slots`` workspaces (each
+    with its host buffer, pending record and outputs) cycle; with the default 3 a caller runs
+    per step submit(i), finish(i-1), wait(i-2) (``run``). comm: RcclComm or TorchGatherComm.
+    Reference: /root/reference/src/backend/app/lib.py:51-55 per shard, merged across shards."""
+
+    def __init__(self, catalog: Catalog, k: int, B: int, comm, slots: int = 3, timer=None,
+                 kprime: Optional[int] = None, fuse: bool = True) -> None:
+        import ctypes
+        self.catalog, self.k, self.B, self.timer = catalog, k, B, timer
+        self._comm_owner = comm
+        self.comm = comm.comm(catalog.n_global)
+        self.opt = _lib.EbtOptions(kprime=int(kprime or 0),
+                                   flags=0 if fuse else _lib.EBT_FLAG_NO_FUSE, chunk_rows=0)
+        lib = _lib.load()
+        need = lib.ebt_sharded_workspace_bytes(ctypes.byref(catalog.cstruct),
+                                               ctypes.byref(self.comm), B, k,
+                                               ctypes.byref(self.opt))
+        if need == 0:
+            raise EbertError(f"ebt_sharded_workspace_bytes: batch {B}, k={k} over this shard "
+                             "is not supported")
+        dev = catalog.device
+        self.ws_bytes = int(need)
+        self.ws = [torch.empty(need, dtype=torch.uint8, device=dev) for _ in range(slots)]
+        self.host = [torch.zeros(B + 2, dtype=torch.int32, pin_memory=True) for _ in range(slots)]
+        self.pend = [_lib.EbtShardedPending() for _ in range(slots)]
+        self.out = [(torch.empty((B, k), dtype=torch.float64, device=dev),
+                     torch.empty((B, k), dtype=torch.int64, device=dev)) for _ in range(slots)]
+        self.keep = [None] * slots
+        if isinstance(comm, TorchGatherComm):
+            for w in self.ws:
+                comm.register(w)
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != 0:
+            err = getattr(self._comm_owner, "error", None)
+            msg = _lib.load().ebt_last_error().decode(errors="replace")
+            raise EbertError(f"ebt_cosine_topk_sharded_{what} failed with status {rc}: {msg}"
+                             + (f" (all-gather: {err!r})" if err is not None else ""))
+
+    def submit(self, slot: int, queries: Optional[torch.Tensor] = None, liked=None,
+               exclude=None) -> None:
+        """Enqueue one batch into workspace `slot` (free: its previous batch waited)."""
+        import ctypes
+        dev = self.catalog.device
+        q_ptr, q_dt, ldq, lo, lr = None, 0, 0, None, None
+        if queries is not None:
+            require = queries.is_cuda and queries.dim() == 2 and queries.shape[0] == self.B
+            if not require or queries.stride(1) != 1:
+                raise EbertError(f"queries must be a contiguous-row [B={self.B}, d] GPU tensor")
+            q_ptr, q_dt, ldq = ptr(queries), _lib.DTYPE_CODE[queries.dtype], queries.stride(0)
+        else:
+            lo, lr = liked if isinstance(liked, tuple) else csr_from_lists(liked, dev)
+        eo = er = None
+        if exclude is not None:
+            eo, er = exclude if isinstance(exclude, tuple) else csr_from_lists(exclude, dev)
+        self.keep[slot] = (queries, lo, lr, eo, er)
+        s, r = self.out[slot]
+        rc = _lib.load().ebt_cosine_topk_sharded_submit(
+            ctypes.byref(self.catalog.cstruct), ctypes.byref(self.comm), q_ptr, q_dt, self.B, ldq,
+            ptr(lo), ptr(lr), self.k, ptr(eo), ptr(er), ctypes.byref(self.opt), ptr(self.ws[slot]),
+            self.ws_bytes, ptr(s), ptr(r), ptr(self.host[slot]), ctypes.byref(self.pend[slot]),
+            self.timer.handle if self.timer is not None else None, stream_of(dev))
+        self._check(rc, "submit")
+
+    def finish(self, slot: int) -> None:
+        import ctypes
+        self._check(_lib.load().ebt_cosine_topk_sharded_finish(ctypes.byref(self.pend[slot])),
+                    "finish")
+
+    def wait(self, slot: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        import ctypes
+        self._check(_lib.load().ebt_cosine_topk_sharded_wait(ctypes.byref(self.pend[slot])),
+                    "wait")
+        self.keep[slot] = None
+        return self.out[slot]
+
+    def __call__(self, queries=None, liked=None, exclude=None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """One batch, blocking (slot 0)."""
+        self.submit(0, queries=queries, liked=liked, exclude=exclude)
+        self.finish(0)
+        return self.wait(0)
+
+    def run(self, n: int, queries: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """n batches of `queries`, three in flight: per step submit(i), finish(i-1), wait(i-2).
+        Returns the last batch's (scores, rows), final."""
+        S = len(self.ws)
+        if S < 3:
+            raise EbertError("run() needs 3 slots (a batch's buffers live until its wait)")
+        out = None
+        for i in range(n + 2):
+            if i < n:
+                self.submit(i % S, queries=queries)
+            if 1 <= i <= n:
+                self.finish((i - 1) % S)
+            if i >= 2:
+                out = self.wait((i - 2) % S)
+        return out

@@ -514,6 +514,7 @@ def score_topk_stages(catalog: Catalog, k: int, queries: Optional[torch.Tensor] 
     kp = kprime or default_kprime(catalog, k_eff)
     kp = max(_round_up(k_eff, 4), min(_round_up(kp, 4), n_cap, KPRIME_MAX))
     flags = 0 if fuse else _lib.EBT_FLAG_NO_FUSE
+    t_floor = None
     if t_floor_hook is None:
         yield
         s, r, cert = run_pipeline(catalog, qb, k_eff, kp, exclude, chunk_rows, timer, flags=flags)
@@ -525,7 +526,7 @@ def score_topk_stages(catalog: Catalog, k: int, queries: Optional[torch.Tensor] 
         yield
         next(cut)
         yield
-        s, r, cert = next(cut)
+        s, r, cert, t_floor = next(cut)
     # the certificates travel to pinned host memory right behind this batch's kernels, so
     # finishing it waits for this batch only, not for batches submitted after it
     cert_host = torch.empty(cert.shape, dtype=cert.dtype, pin_memory=True)
@@ -533,7 +534,7 @@ def score_topk_stages(catalog: Catalog, k: int, queries: Optional[torch.Tensor] 
     ready = torch.cuda.Event()
     ready.record(torch.cuda.current_stream(dev))
     yield PendingTopk(catalog, qb, k, k_eff, kp, exclude, chunk_rows, timer, flags, n_cap,
-                      s, r, cert, cert_host, ready)
+                      s, r, cert, cert_host, ready, t_floor)
 
 
 def score_topk_finish(p) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -624,6 +625,7 @@ class PendingTopk:
     cert: torch.Tensor
     cert_host: torch.Tensor          # pinned copy of cert, valid once `ready` has completed
     ready: torch.cuda.Event
+    t_floor: Optional[torch.Tensor] = None   # the catalog-wide floor (t_floor_hook), f64 [B]
 
 
 def union_floor_gathered(g: torch.Tensor, k: int) -> torch.Tensor:
@@ -653,13 +655,13 @@ def _screen_global_cut(catalog: Catalog, qb: QueryBatch, k: int, k_req: int, kpr
                            t_floor_hook, theta_hook)
     next(g)
     next(g)
-    return next(g)
+    return next(g)[:3]
 
 
 def _global_cut_stages(catalog: Catalog, qb: QueryBatch, k: int, k_req: int, kprime: int,
                        exclude, chunk_rows, timer, flags, t_floor_hook, theta_hook=None):
     """_screen_global_cut as a generator: yields after the theta hook and after the floor hook,
-    then yields (scores, rows, cert)."""
+    then yields (scores, rows, cert, t_floor)."""
     dev = catalog.device
     B = qb.B
     # the hook is a collective: called on every shard whether or not this one uses its result
@@ -697,7 +699,7 @@ def _global_cut_stages(catalog: Catalog, qb: QueryBatch, k: int, k_req: int, kpr
     with region(timer, "small", dev):
         call("ebt_certify_cut", ptr(cert), ptr(ovf), ptr(th[0]) if use_theta else None,
              ptr(t_floor), ptr(eps), B, stream_of(dev))
-    yield out_s, out_r, cert
+    yield out_s, out_r, cert, t_floor
 
 
 def merge_topk(scores: torch.Tensor, rows: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:

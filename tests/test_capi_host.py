@@ -24,7 +24,7 @@ def test_header_symbols_exported():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_lib._SIGNATURES), set(syms) ^ set(_lib._SIGNATURES)
-    assert lib.ebt_version() >= 100
+    assert lib.ebt_version() >= 200
     assert isinstance(lib.ebt_last_error(), bytes)
 
 

@@ -29,6 +29,23 @@ class Comm(ctypes.Structure):   # struct ebt_comm
                 ("ctx", VP)]
 
 
+class Options(ctypes.Structure):   # struct ebt_options
+    _fields_ = [("kprime", I32), ("flags", I32), ("chunk_rows", I64)]
+
+
+class Pending(ctypes.Structure):   # struct ebt_pending
+    _fields_ = [("cat", VP), ("opt", Options), ("B", I64), ("B_pad", I64), ("chunk", I64),
+                ("k", I32), ("k_eff", I32), ("kprime", I32), ("flags", I32), ("excl_off", VP),
+                ("excl_rows", VP), ("ws", VP), ("ws_bytes", SZ), ("out_scores", VP),
+                ("out_rows", VP), ("cert_host", VP), ("event", VP), ("timer", VP),
+                ("stream", VP)]
+
+
+class ShardedPending(ctypes.Structure):   # struct ebt_sharded_pending
+    _fields_ = [("local", Pending), ("comm", Comm), ("out_scores", VP), ("out_rows", VP),
+                ("host", VP), ("event", VP), ("stage", I32)]
+
+
 @pytest.fixture(scope="module")
 def lib():
     h = ctypes.CDLL(LIB)
@@ -47,6 +64,11 @@ def lib():
     h.ebt_cosine_topk_sharded.argtypes = [ctypes.POINTER(Catalog), ctypes.POINTER(Comm), VP,
                                           ctypes.c_int, I64, I64, VP, VP, I32, VP, VP, VP, VP, SZ,
                                           VP, VP, VP, VP]
+    h.ebt_cosine_topk_sharded_submit.argtypes = [
+        ctypes.POINTER(Catalog), ctypes.POINTER(Comm), VP, ctypes.c_int, I64, I64, VP, VP, I32,
+        VP, VP, VP, VP, SZ, VP, VP, VP, ctypes.POINTER(ShardedPending), VP, VP]
+    h.ebt_cosine_topk_sharded_finish.argtypes = [ctypes.POINTER(ShardedPending)]
+    h.ebt_cosine_topk_sharded_wait.argtypes = [ctypes.POINTER(ShardedPending)]
     return h
 
 
@@ -150,7 +172,7 @@ def test_sharded_capi_shared_threshold_exclusions(cuda_device, lib, hip):
     q = torch.from_numpy(qv.astype(np.float32)).to(cuda_device)
     ex = csr(excl, cuda_device)
     res, calls = run_ranks(lib, hip, full, world, k, q=q, excl=ex)
-    assert calls == [4] * world          # threshold, floor, scores, rows
+    assert calls == [3] * world          # threshold, floor, packed results
     s1, r1 = check_equal_single(lib, full, res, k, q=q, excl=ex)
     sample = [0, 150, 299]
     s_ref, r_ref = R.cosine_topk(qv[sample].astype(np.float32).astype(np.float64),
@@ -169,7 +191,7 @@ def test_sharded_capi_large_k_block_merge(cuda_device, lib, hip):
     full = torch.from_numpy(c).to(cuda_device).to(torch.bfloat16)
     q = torch.from_numpy(qv).to(cuda_device).to(torch.bfloat16)
     res, calls = run_ranks(lib, hip, full, world, k, q=q)
-    assert calls == [3] * world          # floor, scores, rows
+    assert calls == [2] * world          # floor, packed results
     s1, r1 = check_equal_single(lib, full, res, k, q=q)
     c64 = full[:].double().cpu().numpy()
     q64 = q.double().cpu().numpy()
@@ -188,7 +210,7 @@ def test_sharded_capi_liked_users(cuda_device, lib, hip):
     full = torch.from_numpy(c).to(cuda_device)
     lk, ex = csr(liked, cuda_device), csr(rated, cuda_device)
     res, calls = run_ranks(lib, hip, full, world, k, liked=lk, excl=ex)
-    assert calls == [4] * world          # partial sums, floor, scores, rows
+    assert calls == [3] * world          # partial sums, floor, packed results
     s1, r1 = check_equal_single(lib, full, res, k, liked=lk, excl=ex)
     want_s, want_r = R.liked_topk(c, liked, k, rated)
     np.testing.assert_array_equal(r1, want_r)
@@ -210,3 +232,146 @@ def test_sharded_capi_collective_failure(cuda_device, lib, hip):
     res, _ = run_ranks(lib, hip, full, world, k, q=q, fail_rank=1)
     for rc, msg, _, _ in res:
         assert rc == -2 and "all_gather returned" in msg
+
+
+def run_ranks_pipelined(lib, hip, full, world, k, batches, n_ws=3):
+    """ebt_cosine_topk_sharded_submit / _finish / _wait on `world` thread ranks with batches in
+    flight: per step submit(i), finish(i-1), wait(i-2) (the order include/ebert.h suggests),
+    `n_ws` workspaces cycled. Returns per rank the list of (scores, rows) per batch and the
+    all-gather calls per rank."""
+    dev = full.device
+    n = full.shape[0]
+    cuts = shard_cuts(n, world)
+    shared = {"slots": [None] * world, "barrier": threading.Barrier(world, timeout=120),
+              "calls": [0] * world}
+    cats = []
+    for r in range(world):
+        cat, state = make_catalog(lib, full[cuts[r]:cuts[r + 1]])
+        cat.row_offset = cuts[r]
+        cats.append((cat, state))
+    out = [None] * world
+    errs = []
+
+    def body(rank):
+        try:
+            def gather(ctx, send, recv, nbytes, stream):
+                try:
+                    shared["calls"][rank] += 1
+                    hip.hipStreamSynchronize(stream)
+                    shared["slots"][rank] = send
+                    shared["barrier"].wait()
+                    for src in range(world):
+                        if hip.hipMemcpy(recv + src * nbytes, shared["slots"][src], nbytes, 3):
+                            return -1
+                    shared["barrier"].wait()
+                    return 0
+                except threading.BrokenBarrierError:
+                    return -9
+            cb = GATHER(gather)
+            comm = Comm(rank, world, n, cb, None)
+            cat = cats[rank][0]
+            B = batches[0].shape[0]
+            need = lib.ebt_sharded_workspace_bytes(ctypes.byref(cat), ctypes.byref(comm), B, k,
+                                                   None)
+            assert need > 0
+            wss = [torch.empty(need, dtype=torch.uint8, device=dev) for _ in range(n_ws)]
+            hosts = [torch.zeros(B + 2, dtype=torch.int32).pin_memory() for _ in range(n_ws)]
+            pend = [ShardedPending() for _ in range(n_ws)]
+            res = [(torch.empty((B, k), dtype=torch.float64, device=dev),
+                    torch.empty((B, k), dtype=torch.int64, device=dev)) for _ in batches]
+            st = torch.cuda.current_stream(dev).cuda_stream
+
+            def check(rc, what):
+                if rc:
+                    raise AssertionError(f"rank {rank} {what}: {lib.ebt_last_error().decode()}")
+            nb = len(batches)
+            for i in range(nb + 2):
+                if i < nb:
+                    q, w = batches[i], i % n_ws
+                    check(lib.ebt_cosine_topk_sharded_submit(
+                        ctypes.byref(cat), ctypes.byref(comm), P(q), CODE[q.dtype], B, q.stride(0),
+                        None, None, k, None, None, None, P(wss[w]), need, P(res[i][0]),
+                        P(res[i][1]), P(hosts[w]), ctypes.byref(pend[w]), None, st), "submit")
+                if 1 <= i <= nb:
+                    check(lib.ebt_cosine_topk_sharded_finish(ctypes.byref(pend[(i - 1) % n_ws])),
+                          "finish")
+                if 2 <= i:
+                    check(lib.ebt_cosine_topk_sharded_wait(ctypes.byref(pend[(i - 2) % n_ws])),
+                          "wait")
+            torch.cuda.synchronize(dev)
+            out[rank] = [(s.cpu().numpy(), r.cpu().numpy()) for s, r in res]
+        except Exception as e:  # noqa: BLE001 -- reported after the join
+            errs.append(e)
+            shared["barrier"].abort()
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(300)
+    assert not errs, errs
+    assert all(o is not None for o in out), "a rank did not finish"
+    return out, shared["calls"]
+
+
+def test_sharded_capi_pipelined_eight_ranks(cuda_device, lib, hip):
+    """Eight thread ranks, four batches in flight through submit / finish / wait (three
+    workspaces): every rank's answer for every batch equals ONE ebt_cosine_topk over the whole
+    catalog, and the step issues three all-gathers (threshold, floor, packed results)."""
+    n, d, B, k, world = 800_000, 128, 512, 100, 8
+    c = gaussian(241, n, d, "f32")
+    full = torch.from_numpy(c.astype(np.float32)).to(cuda_device)
+    batches = [torch.from_numpy(gaussian(242 + i, B, d, "f32").astype(np.float32)).to(cuda_device)
+               for i in range(4)]
+    res, calls = run_ranks_pipelined(lib, hip, full, world, k, batches)
+    assert calls == [3 * len(batches)] * world
+    cat, state = make_catalog(lib, full)
+    for i, q in enumerate(batches):
+        rc, s1, r1 = topk(lib, cat, k, cuda_device, q=q)
+        assert rc == 0, lib.ebt_last_error()
+        for rank in range(world):
+            s, r = res[rank][i]
+            np.testing.assert_array_equal(r, r1)
+            np.testing.assert_array_equal(s, s1)
+    s_ref, r_ref = R.cosine_topk(gaussian(242, B, d, "f32")[[0, 511]].astype(np.float32)
+                                 .astype(np.float64), c.astype(np.float32).astype(np.float64), k)
+    rc, s1, r1 = topk(lib, cat, k, cuda_device, q=batches[0])
+    np.testing.assert_array_equal(r1[[0, 511]], r_ref)
+
+
+def test_sharded_capi_packed_overflow_falls_back(cuda_device, lib, hip):
+    """Skewed data: every query's whole top 50 lives on shard 0 (noisy copies of the queries),
+    so shard 0's entries above the floor exceed its packed capacity (ceil(1.5 k / R) + 8 per
+    query on average): the merge flags the batch incomplete and _wait re-merges from the full
+    lists (two more all-gathers on every rank) -- the answer stays exact."""
+    n, d, B, k, world = 80_000, 64, 128, 50, 4
+    rng = np.random.default_rng(251)
+    qv = rng.standard_normal((B, d))
+    c = rng.standard_normal((n, d))
+    near = np.repeat(qv, 156, axis=0) + 0.3 * rng.standard_normal((156 * B, d))
+    c[:156 * B] = near                    # inside shard 0 = rows [0, 20000)
+    full = torch.from_numpy(c.astype(np.float32)).to(cuda_device)
+    q = torch.from_numpy(qv.astype(np.float32)).to(cuda_device)
+    res, calls = run_ranks(lib, hip, full, world, k, q=q)
+    assert calls == [4] * world           # floor, packed, then scores + rows
+    s1, r1 = check_equal_single(lib, full, res, k, q=q)
+    assert np.all(r1[:, :k] < 20_000)
+    s_ref, r_ref = R.cosine_topk(qv[[0, 77]].astype(np.float32).astype(np.float64),
+                                 c.astype(np.float32).astype(np.float64), k)
+    np.testing.assert_array_equal(r1[[0, 77]], r_ref)
+
+
+def test_sharded_capi_unsorted_liked(cuda_device, lib, hip):
+    """Liked rows listed out of order (include/ebert.h: the shards' partial sums are then added
+    in another order than the single-GPU sum): the same rows, scores within float64 round-off."""
+    n, d, k, world = 30_000, 64, 40, 3
+    c = gaussian(261, n, d, "f64")
+    liked = [[29_999, 1, 2], [20_002, 10_000, 5], [12_000, 6_000, 29_995, 3]]
+    full = torch.from_numpy(c).to(cuda_device)
+    off = torch.tensor([0, 3, 6, 10], dtype=torch.int64, device=cuda_device)
+    rows = torch.tensor(sum(liked, []), dtype=torch.int64, device=cuda_device)
+    res, calls = run_ranks(lib, hip, full, world, k, liked=(off, rows))
+    want_s, want_r = R.liked_topk(c, liked, k, [[] for _ in liked])
+    for rc, msg, s, r in res:
+        assert rc == 0, msg
+        np.testing.assert_array_equal(r, want_r)
+        np.testing.assert_allclose(s, want_s, rtol=0, atol=1e-12)

@@ -217,7 +217,10 @@ def check_partitioned(gv, gi, ref_v, ref_r, k, kp):
 
 @pytest.mark.parametrize("kp,k,hits,groups,shuffle", [
     (40, 20, 30, 7, False), (200, 100, 500, 300, True), (200, 1, 0, 10, False),
-    (200, 200, 500, 300, False), (600, 100, 300, 50, True), (40, 40, 30, 7, True)])
+    (200, 200, 500, 300, False), (600, 100, 300, 50, True), (40, 40, 30, 7, True),
+    # C5's k' with more groups than one block merge's LDS indexes (16383 at k' = 1256): merged
+    # in parts (select_topk.hip merge_segment)
+    (1256, 1000, 3000, 20000, False), (1256, 1000, 3000, 40000, True)])
 def test_merge_hits_vs_numpy(cuda_device, kp, k, hits, groups, shuffle):
     """ebt_merge_hits: the k' best of (partitioned list + slot hits), exclusions dropped,
     partitioned at k -- ties included -- against numpy on the same composites."""

@@ -63,10 +63,12 @@ def _log(msg):
     print(f"[scale {time.strftime('%H:%M:%S')}] {msg}", flush=True)
 
 
-def _sharded_at_scale(cuda_device, cfg, n_sample, excl_per_query=0, check_plan=None):
+def _sharded_at_scale(cuda_device, cfg, n_sample, excl_per_query=0, check_plan=None,
+                      path="python", slots=2):
     import bench
     import robot_ebert_amd as ebt
-    from robot_ebert_amd.distributed import run_sharded_steps, score_topk_sharded_local_stages
+    from robot_ebert_amd.distributed import (ShardedTopk, TorchGatherComm, run_sharded_steps,
+                                             score_topk_sharded_local_stages)
     n, k, B = cfg["n"], cfg["k"], cfg["b"]
     full = bench.make_catalog_shard(cfg, 0, n, cuda_device)
     qs = [bench.make_queries(cfg, cuda_device), _queries(cfg, 12345, cuda_device)]
@@ -87,11 +89,29 @@ def _sharded_at_scale(cuda_device, cfg, n_sample, excl_per_query=0, check_plan=N
                                                         exclude=excl, collectives=coll), m))
         torch.cuda.synchronize(cuda_device)
         return outs
-    _log(f"{n} x {cfg['d']} {cfg['dtype']}, B={B}, k={k}: {WORLD} thread ranks")
-    res = _run_sharded(full, WORLD, body)
+
+    def body_c(rank, cat, coll):
+        # the C ABI's step (ebt_cosine_topk_sharded_submit / _finish / _wait) over the same
+        # thread exchange: batch 0 alone, then batches 0 and 1 in flight (returns batch 1)
+        def gather(recv, send):
+            recv.copy_(coll.all_gather(send).reshape(-1))
+        eng = ShardedTopk(cat, k, B, TorchGatherComm(rank, WORLD, gather=gather), slots=slots)
+        outs = [tuple(t.clone() for t in eng(queries=qs[0], exclude=excl))]
+        if slots >= 2:
+            eng.submit(0, queries=qs[0], exclude=excl)
+            eng.submit(1, queries=qs[1], exclude=excl)
+            eng.finish(0)
+            eng.finish(1)
+            eng.wait(0)
+            outs.append(tuple(t.clone() for t in eng.wait(1)))
+        torch.cuda.synchronize(cuda_device)
+        return outs
+    _log(f"{n} x {cfg['d']} {cfg['dtype']}, B={B}, k={k}: {WORLD} thread ranks, {path} path")
+    res = _run_sharded(full, WORLD, body if path == "python" else body_c)
+    torch.cuda.empty_cache()
     _log("sharded batches done; single-GPU reference")
     whole = ebt.Catalog(full)
-    for i, q in enumerate(qs):
+    for i, q in enumerate(qs[:len(res[0])]):
         s_ref, r_ref = ebt.score_topk(whole, k, queries=q, exclude=excl)
         for rank in range(WORLD):
             s, r = res[rank][i]
@@ -111,8 +131,10 @@ def _sharded_at_scale(cuda_device, cfg, n_sample, excl_per_query=0, check_plan=N
     np.testing.assert_allclose(s.cpu().numpy()[idx], s_o, rtol=0, atol=SCORE_ATOL)
 
 
-def test_c3_eight_ranks_shared_threshold(cuda_device):
-    """C3 on 8 ranks: 125K-row shards, the shared screening threshold, exclusions."""
+@pytest.mark.parametrize("path", ["python", "capi"])
+def test_c3_eight_ranks_shared_threshold(cuda_device, path):
+    """C3 on 8 ranks: 125K-row shards, the shared screening threshold, exclusions; the Python
+    pipeline and the C ABI's step."""
     import bench
     from robot_ebert_amd.distributed import shard_range, shared_sample_tiles
     from robot_ebert_amd.search import pad_batch
@@ -121,10 +143,11 @@ def test_c3_eight_ranks_shared_threshold(cuda_device):
         assert shared_sample_tiles(n, WORLD, pad_batch(B)) > 0
         assert shard_range(n, WORLD - 1, WORLD)[1] == n
     _sharded_at_scale(cuda_device, dict(bench.CONFIGS["C3"]), 32, excl_per_query=128,
-                      check_plan=plan)
+                      check_plan=plan, path=path)
 
 
-def test_c4_whole_catalog_eight_ranks(cuda_device):
+@pytest.mark.parametrize("path", ["python", "capi"])
+def test_c4_whole_catalog_eight_ranks(cuda_device, path):
     """C4: the whole 10M x 768 bf16 catalog as 8 shards of 1.25M rows, 8192 queries, top-100."""
     import bench
     from robot_ebert_amd.distributed import shared_sample_tiles
@@ -132,10 +155,11 @@ def test_c4_whole_catalog_eight_ranks(cuda_device):
 
     def plan(n, B):
         assert shared_sample_tiles(n, WORLD, pad_batch(B)) == 0   # per-shard screens
-    _sharded_at_scale(cuda_device, dict(bench.CONFIGS["C4"]), 32, check_plan=plan)
+    _sharded_at_scale(cuda_device, dict(bench.CONFIGS["C4"]), 32, check_plan=plan, path=path)
 
 
-def test_c5_batch_and_k_eight_ranks(cuda_device):
+@pytest.mark.parametrize("path", ["python", "capi"])
+def test_c5_batch_and_k_eight_ranks(cuda_device, path):
     """C5's batch and k (16384 queries, top-1000: k' = 1256, the floor-only branch with the
     block merge) on 8 shards of 1M x 1536 f16."""
     import bench
@@ -147,4 +171,5 @@ def test_c5_batch_and_k_eight_ranks(cuda_device):
         shard = ebt.Catalog(torch.zeros((256, cfg["d"]), dtype=torch.float16,
                                         device=cuda_device))
         assert default_kprime(shard, cfg["k"]) > MERGE_WAVE_KMAX
-    _sharded_at_scale(cuda_device, cfg, 32, check_plan=plan)
+    # the C path with one batch (8 ranks x a 16384-query workspace of ~8 GB each)
+    _sharded_at_scale(cuda_device, cfg, 32, check_plan=plan, path=path, slots=1)

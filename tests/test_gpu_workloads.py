@@ -84,11 +84,11 @@ def device_f64_topk(emb: torch.Tensor, q: torch.Tensor, k: int, excl=None, qbloc
 
 
 def run_workload(cuda_device, config: str, rank: int = 0, world: int = 1, n_sample: int = 64,
-                 excl_per_query: int = 0, full_device_check: bool = True):
+                 excl_per_query: int = 0, full_device_check: bool = True, **override):
     import robot_ebert_amd as ebt
     from robot_ebert_amd.distributed import shard_range
     bench = _bench()
-    cfg = dict(bench.CONFIGS[config])
+    cfg = dict(bench.CONFIGS[config], **override)
     begin, end = shard_range(cfg["n"], rank, world)
     emb = bench.make_catalog_shard(cfg, begin, end, cuda_device)
     q = bench.make_queries(cfg, cuda_device)
@@ -152,3 +152,11 @@ def test_c5_per_rank_shard(cuda_device):
     """C5 per-rank work: rank 5 of 8 of the 50M x 1536 f16 catalog (6.25M rows), 16384 queries,
     top-1000."""
     run_workload(cuda_device, "C5", rank=5, world=8, n_sample=32)
+
+
+def test_c5_small_batch_many_groups(cuda_device):
+    """C5's k (top-1000, k' = 1256) with a small batch (1024 queries) over 4.5M rows: the
+    speculative screen's segment then spans more 256-row groups than one block merge's LDS
+    indexes (16383 at k' = 1256, select_topk.hip merge_block_max_groups); the segment is
+    clamped / merged in parts instead of failing."""
+    run_workload(cuda_device, "C5", n_sample=16, n=4_500_000, b=1024, full_device_check=False)
