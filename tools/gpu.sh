@@ -8,6 +8,10 @@
 #   prof   OUT CONFIG [STEPS]  rocprofv3 kernel-trace + stats, then FETCH_SIZE and WRITE_SIZE
 #                              PMC passes (one counter block each) on the screening GEMM
 #   py     OUT SCRIPT [ARGS..] python SCRIPT ARGS > OUT/out.jsonl (tools/*.py experiments)
+#   trace  OUT CMD...          rocprofv3 --kernel-trace --stats of CMD (a kernel timeline)
+#   pmc    OUT REGEX CMD...    a trace pass, then one PMC counter group per rocprofv3 run
+#                              (occupancy / waits, FETCH_SIZE, LDS, instruction mix) over the
+#                              kernels matching REGEX; summarise with tools/pmc_summary.py
 export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 MODE=$1
@@ -70,8 +74,33 @@ EOF
       { tail -20 "$O/err.log"; exit 1; }
     tail -20 "$O/out.jsonl"
     ;;
+  trace)
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O" -o run \
+      -- "$@" > "$O/out.log" 2>&1
+    rc=$?
+    echo "trace rc=$rc"
+    exit $rc
+    ;;
+  pmc)
+    RX=$1
+    shift
+    P="--kernel-include-regex $RX --output-format csv"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o run \
+      -- "$@" > "$O/trace.log" 2>&1 &&
+    timeout -s KILL 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+      SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES SQ_VALU_MFMA_BUSY_CYCLES $P \
+      -d "$O/p1" -o run -- "$@" > "$O/p1.log" 2>&1 &&
+    timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE $P -d "$O/p2" -o run -- "$@" > "$O/p2.log" 2>&1 &&
+    timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT \
+      SQ_WAIT_INST_LDS $P -d "$O/p3" -o run -- "$@" > "$O/p3.log" 2>&1 &&
+    timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VMEM SQ_INST_CYCLES_VMEM SQ_INSTS_SALU \
+      SQ_INSTS_VALU SQ_INSTS_SMEM SQ_INSTS_MFMA $P -d "$O/p4" -o run -- "$@" > "$O/p4.log" 2>&1
+    rc=$?
+    echo "pmc rc=$rc"
+    exit $rc
+    ;;
   *)
-    echo "usage: tools/gpu.sh suite|tests|bench|prof|py OUT ..." >&2
+    echo "usage: tools/gpu.sh suite|tests|bench|prof|py|trace|pmc OUT ..." >&2
     exit 2
     ;;
 esac
