@@ -19,17 +19,26 @@ from . import lib
 from .models import Recommendation
 
 router = APIRouter()
+# a batcher.RecBatcher installed by app(batcher=...): the handler's scoring step is then
+# coalesced with the other worker threads' requests; None = one call per request
+_batcher = None
 
 
 @router.get("/users/{user_id}/recommendations/")
 def get_user_recommendations(user_id: str, k: int = 10) -> List[Recommendation]:
     """get unconditional movie recommendations for an existing user by ID"""
+    if _batcher is not None:
+        return lib.get_user_recs_batched(_batcher, user_id=user_id, k=k)
     user_recommendations = lib.get_user_recs(user_id=user_id, k=k)
     return user_recommendations
 
 
-def app() -> FastAPI:
-    """FastAPI app with the users router (main.py:11-12); configure ``lib`` first."""
+def app(batcher=None) -> FastAPI:
+    """FastAPI app with the users router (main.py:11-12); configure ``lib`` first. With a
+    ``batcher.RecBatcher`` over ``lib.movies_collab_catalog`` the route's requests share GPU
+    batches (same answers, same errors)."""
+    global _batcher
+    _batcher = batcher
     a = FastAPI()
     a.include_router(router, tags=["Users"])
     return a

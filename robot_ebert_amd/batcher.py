@@ -5,10 +5,20 @@ The reference serves one user per call: FastAPI runs the sync handler ``get_user
 (``src/backend/app/api/users.py:150-155``) on up to 40 anyio worker threads, each calling
 ``lib.get_user_recs`` (``lib.py:32-63``) with B = 1. On MI355X a 1-query screen wastes the chip, so
 request threads hand their (liked rows, rated rows, k) to ONE dispatcher thread that waits at
-most ``max_wait_ms`` for company, runs a single ``score_topk`` over up to ``max_batch`` users and
+most ``max_wait_ms`` for company, runs a single batched search over up to ``max_batch`` users and
 hands each caller its own slice. The dispatcher is the only thread that touches the GPU (and, for a
 sharded catalog, the process group: RCCL communicators must not be used concurrently, SURVEY §8b
 "Threading").
+
+* k classes: a batch runs at the largest k among its requests, so requests are grouped by k class
+  (``K_CLASSES``: the screen's k' and merge path change with k) and a large-k request does not pull
+  small-k users onto the large-k path.
+* Pipelining (default scoring): a batch is submitted (``search.score_topk_submit``: its kernels
+  enqueued) and the dispatcher goes on collecting the next requests; the batch is finished and its
+  callers answered as soon as its GPU work is done (an event polled between collection waits), so
+  collection and GPU work overlap. With an injected ``score_fn`` the batch runs synchronously.
+* Bounded statistics: ``batches`` keeps the sizes of the last ``history`` batches; ``stats()``
+  gives totals and a power-of-two batch-size histogram.
 
 Per-request semantics are those of ``lib.get_user_recs``: a request without liked rows fails
 with sklearn's ValueError (alone -- the rest of its batch is unaffected), results are
@@ -16,34 +26,51 @@ with sklearn's ValueError (alone -- the rest of its batch is unaffected), result
 """
 from __future__ import annotations
 
+import collections
 import queue
 import threading
 import time
 from concurrent.futures import Future
-from typing import Callable, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
 _SENTINEL = object()
+# requests with k in (K_CLASSES[i-1], K_CLASSES[i]] share a batch; the last class is unbounded
+K_CLASSES = (32, 128, 512, 4096)
+POLL_S = 2e-4   # how often a waiting dispatcher checks its in-flight batches
+
+
+def k_class(k: int) -> int:
+    for i, hi in enumerate(K_CLASSES):
+        if k <= hi:
+            return i
+    return len(K_CLASSES)
 
 
 class RecBatcher:
     def __init__(self, catalog, max_batch: int = 4096, max_wait_ms: float = 2.0,
-                 score_fn: Optional[Callable] = None) -> None:
+                 score_fn: Optional[Callable] = None, history: int = 1024,
+                 max_inflight: int = 2) -> None:
         """catalog: the ``Catalog`` every request scores against. score_fn(catalog, k, liked=,
-        exclude=) -> (scores [B, k], rows [B, k]) defaults to ``search.score_topk``."""
+        exclude=) -> (scores [B, k], rows [B, k]); default: ``search.score_topk_submit`` /
+        ``score_topk_finish`` with up to ``max_inflight`` batches on the GPU."""
         if max_batch < 1:
             raise ValueError("max_batch must be >= 1")
-        if score_fn is None:
-            from .search import score_topk as score_fn
         self.catalog = catalog
         self.max_batch = int(max_batch)
         self.max_wait = float(max_wait_ms) / 1e3
         self._score = score_fn
+        self._pipelined = score_fn is None
+        self.max_inflight = max(1, int(max_inflight))
         self._q: "queue.Queue" = queue.Queue()
         self._closed = False
         self._lock = threading.Lock()  # orders submit()'s check-and-put against close()
-        self.batches: List[int] = []  # sizes of the batches run (observability / tests)
+        self.batches = collections.deque(maxlen=int(history))  # sizes of the last batches
+        self._n_batches = 0
+        self._n_requests = 0
+        self._hist: Dict[int, int] = collections.Counter()
+        self._inflight: collections.deque = collections.deque()
         self._thread = threading.Thread(target=self._run, name="ebert-batcher", daemon=True)
         self._thread.start()
 
@@ -77,18 +104,41 @@ class RecBatcher:
             self._q.put(_SENTINEL)
         self._thread.join(timeout)
 
+    def stats(self) -> dict:
+        """Totals since start and the batch-size histogram (bin b = sizes in [2^b, 2^(b+1)))."""
+        return {"batches": self._n_batches, "requests": self._n_requests,
+                "mean_batch": self._n_requests / max(self._n_batches, 1),
+                "size_hist_pow2": dict(sorted(self._hist.items()))}
+
     # ---- dispatcher thread ---------------------------------------------------------------------
+    def _get(self, timeout: Optional[float]):
+        """The next queued item within `timeout` seconds (None: wait forever), completing
+        in-flight batches whose GPU work is done while waiting; raises queue.Empty."""
+        end = None if timeout is None else time.monotonic() + timeout
+        while True:
+            self._reap(block=False)
+            if not self._inflight:
+                left = None if end is None else end - time.monotonic()
+                if left is not None and left <= 0:
+                    return self._q.get_nowait()
+                return self._q.get(timeout=left)
+            step = POLL_S if end is None else min(POLL_S, max(end - time.monotonic(), 0.0))
+            try:
+                return self._q.get(timeout=step) if step > 0 else self._q.get_nowait()
+            except queue.Empty:
+                if end is not None and time.monotonic() >= end:
+                    raise
+
     def _collect(self) -> Tuple[list, bool]:
-        first = self._q.get()
+        first = self._get(None)
         if first is _SENTINEL:
             return [], True
         reqs = [first]
         deadline = time.monotonic() + self.max_wait
         stop = False
         while len(reqs) < self.max_batch:
-            left = deadline - time.monotonic()
             try:
-                item = self._q.get(timeout=max(left, 0.0)) if left > 0 else self._q.get_nowait()
+                item = self._get(max(deadline - time.monotonic(), 0.0))
             except queue.Empty:
                 break
             if item is _SENTINEL:
@@ -101,28 +151,83 @@ class RecBatcher:
         while True:
             reqs, stop = self._collect()
             if reqs:
-                self._dispatch(reqs)
+                groups: Dict[int, list] = collections.defaultdict(list)
+                for r in reqs:
+                    groups[k_class(r[2])].append(r)
+                for c in sorted(groups):
+                    self._dispatch(groups[c])
             if stop:
                 while True:  # drain what was queued before close()
                     try:
                         item = self._q.get_nowait()
                     except queue.Empty:
-                        return
+                        break
                     if item is not _SENTINEL:
                         self._dispatch([item])
+                while self._inflight:
+                    self._reap(block=True)
+                return
+
+    def _record(self, n: int) -> None:
+        self.batches.append(n)
+        self._n_batches += 1
+        self._n_requests += n
+        self._hist[max(n, 1).bit_length() - 1] += 1
 
     def _dispatch(self, reqs: list) -> None:
         k_max = max(r[2] for r in reqs)
+        liked, excl = [r[0] for r in reqs], [r[1] for r in reqs]
+        if not self._pipelined:
+            try:
+                scores, rows = self._score(self.catalog, k_max, liked=liked, exclude=excl)
+            except BaseException as e:  # the whole batch failed: every caller sees the error
+                for r in reqs:
+                    r[3].set_exception(e)
+                return
+            self._deliver(reqs, scores, rows)
+            return
+        import torch
+        from .search import score_topk_submit
+        while len(self._inflight) >= self.max_inflight:
+            self._reap(block=True)
         try:
-            scores, rows = self._score(self.catalog, k_max, liked=[r[0] for r in reqs],
-                                       exclude=[r[1] for r in reqs])
-            scores = scores.cpu().numpy() if hasattr(scores, "cpu") else np.asarray(scores)
-            rows = rows.cpu().numpy() if hasattr(rows, "cpu") else np.asarray(rows)
-        except BaseException as e:  # the whole batch failed: every caller sees the error
+            p = score_topk_submit(self.catalog, k_max, liked=liked, exclude=excl)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.catalog.device))
+        except BaseException as e:
             for r in reqs:
                 r[3].set_exception(e)
             return
-        self.batches.append(len(reqs))
+        self._inflight.append((p, ev, reqs))
+
+    def _reap(self, block: bool) -> None:
+        """Finish the oldest in-flight batches whose first pass is done (all of them in order,
+        stopping at the first one still running unless `block`)."""
+        from .search import score_topk_finish
+        while self._inflight:
+            p, ev, reqs = self._inflight[0]
+            if not block and not ev.query():
+                return
+            self._inflight.popleft()
+            try:
+                scores, rows = score_topk_finish(p)
+            except BaseException as e:
+                for r in reqs:
+                    r[3].set_exception(e)
+                continue
+            self._deliver(reqs, scores, rows)
+            if block:
+                return
+
+    def _deliver(self, reqs: list, scores, rows) -> None:
+        try:
+            scores = scores.cpu().numpy() if hasattr(scores, "cpu") else np.asarray(scores)
+            rows = rows.cpu().numpy() if hasattr(rows, "cpu") else np.asarray(rows)
+        except BaseException as e:
+            for r in reqs:
+                r[3].set_exception(e)
+            return
+        self._record(len(reqs))
         for i, (_, _, k, fut) in enumerate(reqs):
             s, r = scores[i, :k], rows[i, :k]
             keep = r >= 0

@@ -1050,16 +1050,18 @@ def test_non_finite_catalog_rows_never_candidates(cuda_device, k):
     assert np.all(rn[:, m:] == -1) and np.all(np.isnan(sn[:, m:]))
 
 
-@pytest.mark.parametrize("k", [10, 10000])
-def test_route_recommendations_matches_reference(cuda_device, k):
+@pytest.mark.parametrize("k,batched", [(10, False), (10000, False), (10, True), (10000, True)])
+def test_route_recommendations_matches_reference(cuda_device, k, batched):
     """Row a-1: GET /users/{user_id}/recommendations/?k= (api/users.py:150-155) through FastAPI's
     TestClient returns the reference's golden recommendations as JSON; the user without a liked
     movie gets HTTP 500 (the reference's uncaught sklearn ValueError), the one without ratings
-    an empty list."""
+    an empty list. batched: the route's scoring goes through a RecBatcher (§8f-2)."""
     from fastapi.testclient import TestClient
     from robot_ebert_amd import api
+    from robot_ebert_amd.batcher import RecBatcher
     lib, gold = _collab_setup(cuda_device)
-    client = TestClient(api.app(), raise_server_exceptions=False)
+    b = RecBatcher(lib.movies_collab_catalog, max_batch=64, max_wait_ms=1.0) if batched else None
+    client = TestClient(api.app(batcher=b), raise_server_exceptions=False)
     for uid, rec in gold["users"].items():
         want = rec[f"k{k}"]
         resp = client.get(f"/users/{uid}/recommendations/", params={"k": k})
@@ -1073,6 +1075,9 @@ def test_route_recommendations_matches_reference(cuda_device, k):
                                    atol=SCORE_ATOL)
         if not want:
             assert got == []
+    if b is not None:
+        b.close()
+        api.app()   # the module-level route back to one call per request
 
 
 @pytest.mark.parametrize("dt,d", [("f32", 1536), ("bf16", 768), ("f16", 200), ("f64", 64)])

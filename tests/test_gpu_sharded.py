@@ -414,3 +414,45 @@ def test_union_floor_kernel_matches_torch(cuda_device, R, k, kk):
     want = union_floor(vals, eps, k)                     # CPU tensors: the torch form
     got = union_floor_gathered(torch.cat([vals, eps[:, :, None]], 2).to(cuda_device), k)
     assert torch.equal(got.cpu(), want)
+
+
+def test_rccl_comm_capi_world1(cuda_device):
+    """bench.py's N > 1 C-ABI path on the one group one GPU allows: libebert's own RCCL
+    communicator (ebt_rccl_unique_id broadcast through a torch "nccl" group, ebt_rccl_comm_init,
+    ncclAllGather inside ebt_cosine_topk_sharded_*) driving ShardedTopk with three batches in
+    flight; the answers equal the single-GPU path, and a direct ebt_rccl_all_gather round-trips
+    a buffer."""
+    import socket
+    import torch.distributed as dist
+    import robot_ebert_amd as ebt
+    from robot_ebert_amd import _lib
+    from robot_ebert_amd.distributed import RcclComm, ShardedTopk
+    from test_gpu_parity import _t
+    n, d, B, k = 150_000, 128, 300, 50
+    cat = ebt.Catalog(_t(gaussian(111, n, d, "f32"), "f32", cuda_device))
+    q = _t(gaussian(112, B, d, "f32"), "f32", cuda_device)
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                            world_size=1, device_id=cuda_device)
+    try:
+        rc = RcclComm()
+        try:
+            x = torch.arange(1000, dtype=torch.int32, device=cuda_device)
+            y = torch.zeros_like(x)
+            _lib.call("ebt_rccl_all_gather", rc.handle, _lib.ptr(x), _lib.ptr(y), 4000,
+                      _lib.stream_of(cuda_device))
+            torch.cuda.synchronize()
+            assert torch.equal(x, y)
+            eng = ShardedTopk(cat, k, B, rc)
+            s, r = eng.run(4, q)
+            torch.cuda.synchronize()
+        finally:
+            rc.close()
+    finally:
+        dist.destroy_process_group()
+    s_ref, r_ref = ebt.score_topk(cat, k, queries=q)
+    assert torch.equal(r, r_ref)
+    assert torch.equal(s, s_ref)

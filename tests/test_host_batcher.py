@@ -116,3 +116,37 @@ def test_submit_racing_close_never_hangs():
                 f.result(timeout=10)
             except RuntimeError as e:
                 assert "closed" in str(e)
+
+
+def test_batcher_groups_by_k_class():
+    """A large-k request does not pull small-k users onto the large-k path: every batch holds
+    one k class (batcher.K_CLASSES), and each caller still gets its own k."""
+    from robot_ebert_amd.batcher import k_class
+    rng = np.random.default_rng(5)
+    cat = _Cat(rng.standard_normal((3000, 8)))
+    seen = []
+
+    def score(c, k, liked, exclude):
+        seen.append(k)
+        qs = np.stack([R.mean_cosine_query(c.x[l]) for l in liked])
+        return R.cosine_topk(qs, c.x, k, exclude)
+    b = RecBatcher(cat, max_batch=64, max_wait_ms=100.0, score_fn=score)
+    ks = [5, 2000, 7, 100, 3, 2000, 30, 600]
+    futs = [b.submit([i], [], k) for i, k in enumerate(ks)]
+    res = [f.result(timeout=30) for f in futs]
+    b.close()
+    assert sorted(k_class(k) for k in seen) == sorted(set(k_class(k) for k in ks))
+    assert max(seen) == 2000 and min(seen) == 30   # class 0 ran at its own k_max
+    for (s, r), k in zip(res, ks):
+        assert len(r) == k
+
+
+def test_batcher_stats_are_bounded():
+    cat = _Cat(np.random.default_rng(6).standard_normal((200, 8)))
+    b = RecBatcher(cat, max_batch=4, max_wait_ms=0.0, score_fn=_oracle_score([]), history=4)
+    for i in range(10):
+        b.submit([i], [], 3).result(timeout=10)
+    b.close()
+    st = b.stats()
+    assert len(b.batches) == 4 and st["batches"] == 10 and st["requests"] == 10
+    assert sum(st["size_hist_pow2"].values()) == 10 and st["size_hist_pow2"] == {0: 10}
