@@ -83,7 +83,19 @@ def main():
     print("thread ranks done", file=sys.stderr, flush=True)
     record = shared["record"]
     per_step = len(record) // a.steps
-    recv_bytes = [int(g.numel()) for g in record[:per_step]]
+    sizes = sorted(set(int(g.numel()) for g in record))
+    recv_total = sum(int(g.numel()) for g in record)
+    # the packed results' gathers: every rank's starts[B] = its entries above the floor
+    lib = _lib.load()
+    w = int(lib.ebt_shard_list_width(k, W))
+    cap = int(lib.ebt_shard_pack_cap(B, k, W, cfg["n"]))
+    pb = int(lib.ebt_shard_pack_bytes(B, cap)) if cap else 0
+    counts = []
+    for g in record:
+        if pb and g.numel() == W * pb:
+            v = g.view(W, pb)[:, :4 * (B + 1)].contiguous().view(torch.int32)
+            counts.append(v[:, B].double().cpu())
+    sent = torch.stack(counts) if counts else None
     ref = outs[0]
     cat0 = cats[0]
     del cats[1:]
@@ -140,8 +152,13 @@ def main():
     stages = {n: round(timer.query(n)[0] / a.steps, 4) for n in _lib.STAGES}
     print(json.dumps({
         "config": a.config, "world": W, "shard_rows": cat0.n, "path": "C ABI (ShardedTopk)",
-        "gathers_per_step": per_step, "recv_bytes_per_gather": recv_bytes,
-        "recv_mb_per_step": round(sum(recv_bytes) / 1e6, 3),
+        "gathers_per_step": per_step, "gather_sizes_bytes": sizes,
+        "recv_mb_per_step": round(recv_total / a.steps / 1e6, 3),
+        "floor_width_per_query": w, "packed_cap_per_rank": cap, "packed_bytes_per_rank": pb,
+        "packed_entries_per_query_mean": (round(float(sent.mean()) / B, 2)
+                                          if sent is not None else None),
+        "packed_entries_per_query_max_rank": (round(float(sent.max()) / B, 2)
+                                              if sent is not None else None),
         "wall_ms_per_step": round(wall, 3), "replay_equals_threads": same,
         "host_ms_per_step": round(sum(host_ms.values()), 4), "host_ms_by_call": host_ms,
         "callback_ms_per_step": round(cb_ms, 4),

@@ -41,8 +41,8 @@ SHAPES = {"C1": dict(n=2269, d=32, dtype=torch.float64),
 
 
 def setup(shape, users, liked, rated, seed=0):
+    import tempfile
     from sqlalchemy import create_engine, insert
-    from sqlalchemy.pool import StaticPool
     cfg = SHAPES[shape]
     n, d = cfg["n"], cfg["d"]
     dev = torch.device("cuda:0")
@@ -51,8 +51,11 @@ def setup(shape, users, liked, rated, seed=0):
     ids = [str(100000 + i) for i in range(n)]
     cat = ebt.Catalog(emb, ids=ids)
     rng = np.random.default_rng(seed + 1)
-    engine = create_engine("sqlite://", connect_args={"check_same_thread": False},
-                           poolclass=StaticPool)
+    # a file-backed SQLite database: one connection per request thread (the reference's
+    # Postgres pool serves its 40 worker threads concurrently as well)
+    path = os.path.join(tempfile.mkdtemp(), "ratings.db")
+    engine = create_engine(f"sqlite:///{path}", connect_args={"check_same_thread": False},
+                           pool_size=64, max_overflow=0)
     tables.ratings.create(engine)
     user_rows = {}
     rows = []
@@ -122,7 +125,7 @@ def main():
     out = {"shape": a.shape, "n": cat.n, "d": cat.d, "dtype": str(emb.dtype), "users": a.users,
            "liked_per_user": a.liked, "rated_per_user": a.liked + a.rated, "k": k,
            "threads": a.threads, "max_wait_ms": a.max_wait_ms,
-           "data": "synthetic (seeded Gaussian catalog, random ratings in SQLite in memory)"}
+           "data": "synthetic (seeded Gaussian catalog, random ratings in a file-backed SQLite table)"}
     # warm
     for u in uids[:3]:
         lib.get_user_recs(u, k)
