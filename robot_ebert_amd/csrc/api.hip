@@ -28,6 +28,65 @@ int hip_check(hipError_t e, const char* what) {
 
 int launch_check(const char* what) { return hip_check(hipGetLastError(), what); }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device) and larger size:
+// the launch paths ask before every launch, and the runtime call costs host time per batch
+// (the attribute is a permission, not an allocation: a smaller launch after a larger one is
+// unaffected).
+void set_max_lds(const void* fn, int bytes) {
+  static std::mutex mu;
+  static std::vector<std::pair<std::pair<const void*, int>, int>> seen;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> g(mu);
+  for (auto& e : seen)
+    if (e.first.first == fn && e.first.second == dev) {
+      if (e.second >= bytes) return;
+      if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) ==
+          hipSuccess)
+        e.second = bytes;
+      return;
+    }
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) == hipSuccess)
+    seen.push_back({{fn, dev}, bytes});
+}
+
+// Completion events of submitted batches, recycled (creating and destroying one per batch is
+// host time on every step): per device, a free list under a lock.
+hipEvent_t event_get() {
+  static_assert(sizeof(hipEvent_t) == sizeof(void*), "event handle");
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  {
+    std::lock_guard<std::mutex> g(event_pool_mutex());
+    auto& fl = event_pool()[dev & 63];
+    if (!fl.empty()) {
+      hipEvent_t e = fl.back();
+      fl.pop_back();
+      return e;
+    }
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  return e;
+}
+void event_put(hipEvent_t e) {
+  if (!e) return;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> g(event_pool_mutex());
+  auto& fl = event_pool()[dev & 63];
+  if (fl.size() < 64) fl.push_back(e);
+  else (void)hipEventDestroy(e);
+}
+std::mutex& event_pool_mutex() {
+  static std::mutex m;
+  return m;
+}
+std::vector<hipEvent_t>* event_pool() {
+  static std::vector<hipEvent_t> pools[64];
+  return pools;
+}
+
 // kernels (defined in the other translation units)
 int screen_gemm(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int, const float*,
                 const float*, float*, int64_t, hipStream_t, int64_t cstride = 0);

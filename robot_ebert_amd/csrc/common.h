@@ -6,6 +6,9 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
+#include <mutex>
+#include <vector>
+
 #include "../../include/ebert.h"
 
 namespace ebt {
@@ -21,6 +24,11 @@ typedef uint16_t u16x8_t __attribute__((ext_vector_type(8)));
 void set_error(const char* fmt, ...);
 int hip_check(hipError_t e, const char* what);
 int launch_check(const char* what);
+void set_max_lds(const void* fn, int bytes);
+hipEvent_t event_get();
+void event_put(hipEvent_t e);
+std::mutex& event_pool_mutex();
+std::vector<hipEvent_t>* event_pool();
 
 // ---- element conversion --------------------------------------------------------------------
 __device__ __forceinline__ double bf16_bits_to_f64(uint16_t h) {

@@ -483,12 +483,11 @@ int ebt_cosine_topk_submit(const ebt_catalog* cat, const void* q, int q_dtype, i
   rc = hip_check(hipMemcpyAsync(cert_host, cert, (size_t)(B + 1) * 4, hipMemcpyDeviceToHost, st),
                  "hipMemcpyAsync");
   if (rc) return rc;
-  hipEvent_t ev;
-  rc = hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
-  if (rc) return rc;
+  hipEvent_t ev = event_get();
+  if (!ev) return hip_check(hipErrorOutOfMemory, "hipEventCreate");
   rc = hip_check(hipEventRecord(ev, st), "hipEventRecord");
   if (rc) {
-    (void)hipEventDestroy(ev);
+    event_put(ev);
     return rc;
   }
   ebt_pending P{};
@@ -523,7 +522,7 @@ int ebt_cosine_topk_finish(ebt_pending* p) {
   const ebt_catalog& c = *p->cat;
   hipEvent_t ev = (hipEvent_t)p->event;
   int rc = hip_check(hipEventSynchronize(ev), "hipEventSynchronize");
-  (void)hipEventDestroy(ev);
+  event_put(ev);
   p->event = nullptr;
   if (rc) return rc;
   const int64_t B = p->B;
@@ -1107,12 +1106,11 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
   rc = hip_check(hipMemcpyAsync(host, cert, (size_t)(B + 1) * 4, hipMemcpyDeviceToHost, st),
                  "hipMemcpyAsync");
   if (rc) return rc;
-  hipEvent_t ev;
-  rc = hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
-  if (rc) return rc;
+  hipEvent_t ev = event_get();
+  if (!ev) return hip_check(hipErrorOutOfMemory, "hipEventCreate");
   rc = hip_check(hipEventRecord(ev, st), "hipEventRecord");
   if (rc) {
-    (void)hipEventDestroy(ev);
+    event_put(ev);
     return rc;
   }
   ebt_sharded_pending P{};
@@ -1190,12 +1188,11 @@ int ebt_cosine_topk_sharded_finish(ebt_sharded_pending* p) {
     rc = sh_full_merge(S, p->comm, ws, B, k, p->out_scores, p->out_rows, timer, st);
   }
   if (rc) return rc;
-  hipEvent_t ev;
-  rc = hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
-  if (rc) return rc;
+  hipEvent_t ev = event_get();
+  if (!ev) return hip_check(hipErrorOutOfMemory, "hipEventCreate");
   rc = hip_check(hipEventRecord(ev, st), "hipEventRecord");
   if (rc) {
-    (void)hipEventDestroy(ev);
+    event_put(ev);
     return rc;
   }
   p->event = ev;
@@ -1211,7 +1208,7 @@ int ebt_cosine_topk_sharded_wait(ebt_sharded_pending* p) {
   hipStream_t st = (hipStream_t)lp.stream;
   hipEvent_t ev = (hipEvent_t)p->event;
   int rc = hip_check(hipEventSynchronize(ev), "hipEventSynchronize");
-  (void)hipEventDestroy(ev);
+  event_put(ev);
   p->event = nullptr;
   p->stage = 0;
   if (rc) return rc;

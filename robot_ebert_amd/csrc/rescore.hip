@@ -533,8 +533,7 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
     if (R > 8) {
       const size_t lds2 = rescore_lds_stage_total(d, es, kprime, R);
 #define EBT_RSL(DT)                                                                             \
-  (void)hipFuncSetAttribute((const void*)rescore_lds_kernel<DT>,                                \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);             \
+  set_max_lds((const void*)rescore_lds_kernel<DT>, (int)lds2);                                 \
   hipLaunchKernelGGL((rescore_lds_kernel<DT>), grid, block, lds2, st, q64, d, cat, ld, gnorm,   \
                      row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps, t_floor,    \
                      out_s, out_r, certified, ovf_cnt, ovf_cap, R);
@@ -550,10 +549,8 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
   }
 #endif
 #define EBT_RS(DT)                                                                              \
-  (void)hipFuncSetAttribute((const void*)rescore_kernel<DT, true>,                              \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
-  (void)hipFuncSetAttribute((const void*)rescore_kernel<DT, false>,                             \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
+  set_max_lds((const void*)rescore_kernel<DT, true>, (int)lds);                                \
+  set_max_lds((const void*)rescore_kernel<DT, false>, (int)lds);                               \
   if (vec)                                                                                      \
     hipLaunchKernelGGL((rescore_kernel<DT, true>), grid, block, lds, st, q64, d, cat, ld,       \
                        gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,    \
@@ -928,15 +925,13 @@ int merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, 
   if (R > 1 && R <= MERGE_CORANK_RMAX && n <= MERGE_CORANK_CAP) {
     const int P = next_pow2_h((int)n);
     const size_t lds = merge_corank_lds(R, P);
-    (void)hipFuncSetAttribute((const void*)merge_topk_corank_kernel<DenseSrc>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    set_max_lds((const void*)merge_topk_corank_kernel<DenseSrc>, (int)lds);
     hipLaunchKernelGGL(merge_topk_corank_kernel<DenseSrc>, dim3((unsigned)B), dim3(RTHREADS),
                        lds, st, DenseSrc{scores, rows}, R, B, k, P, out_s, out_r, nullptr);
     return launch_check("merge_topk_corank_kernel");
   }
   const int P = next_pow2_h((int)(n < MERGE_CAP ? n : MERGE_CAP));
-  (void)hipFuncSetAttribute((const void*)merge_topk_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(P * 16));
+  set_max_lds((const void*)merge_topk_kernel, (int)(P * 16));
   hipLaunchKernelGGL(merge_topk_kernel, dim3((unsigned)B), dim3(RTHREADS), (size_t)P * 16, st,
                      scores, rows, R, B, k, P, out_s, out_r);
   return launch_check("merge_topk_kernel");
@@ -1243,10 +1238,8 @@ int rescore_owned(const double* q64, int64_t B, int32_t d, const void* cat, int 
                    (((int64_t)d * es) % 16 == 0);
   dim3 grid((unsigned)B), block(RTHREADS);
 #define EBT_RO(DT)                                                                              \
-  (void)hipFuncSetAttribute((const void*)rescore_owned_kernel<DT, true>,                        \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
-  (void)hipFuncSetAttribute((const void*)rescore_owned_kernel<DT, false>,                       \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
+  set_max_lds((const void*)rescore_owned_kernel<DT, true>, (int)lds);                          \
+  set_max_lds((const void*)rescore_owned_kernel<DT, false>, (int)lds);                         \
   if (vec)                                                                                      \
     hipLaunchKernelGGL((rescore_owned_kernel<DT, true>), grid, block, lds, st, q64, d, cat, ld, \
                        gnorm, row_offset, n_local, cand_vals, cand_rows, kprime, k, eps, exact); \
@@ -1327,8 +1320,7 @@ int finalize_topk(const float* cand_vals, const int64_t* cand_rows, const double
   if (B == 0) return EBT_OK;
   const int kpp = next_pow2_h(kprime);
   const size_t lds = (size_t)kpp * 16;
-  (void)hipFuncSetAttribute((const void*)finalize_topk_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  set_max_lds((const void*)finalize_topk_kernel, (int)lds);
   hipLaunchKernelGGL(finalize_topk_kernel, dim3((unsigned)B), dim3(RTHREADS), lds, st, cand_vals,
                      cand_rows, exact, kprime, kpp, k, n_rows, eps, ovf, out_s, out_r, certified);
   return launch_check("finalize_topk_kernel");
@@ -1580,8 +1572,7 @@ extern "C" int ebt_merge_packed(const void* recv, int32_t R, int64_t B, int32_t 
   }
   const int P = next_pow2_h(R * k);
   const size_t lds = merge_corank_lds(R, P);
-  (void)hipFuncSetAttribute((const void*)merge_topk_corank_kernel<PackedSrc>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  set_max_lds((const void*)merge_topk_corank_kernel<PackedSrc>, (int)lds);
   const PackedSrc src{(const char*)recv, (int64_t)ebt_shard_pack_bytes(B, cap), cap};
   hipLaunchKernelGGL(merge_topk_corank_kernel<PackedSrc>, dim3((unsigned)B), dim3(RTHREADS), lds,
                      (hipStream_t)stream, src, R, B, k, P, out_scores, out_rows, incomplete);

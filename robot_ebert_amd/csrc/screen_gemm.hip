@@ -1093,8 +1093,7 @@ static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_
                                                    : screen_gemm_qp2_kernel<false, EPI, true>)
                           : (img_dtype == EBT_BF16 ? screen_gemm_qp2_kernel<true, EPI, false>
                                                    : screen_gemm_qp2_kernel<false, EPI, false>);
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              QP_LDS_TOTAL);
+    set_max_lds((const void*)k, QP_LDS_TOTAL);
     QpArgs a{};
     a.Q = Q;
     a.C = C;
@@ -1119,7 +1118,7 @@ static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_
   auto k = img_dtype == EBT_BF16 ? screen_gemm_kernel<true, FILTER>
                                  : screen_gemm_kernel<false, FILTER>;
   const int lds = GLDS_BYTES + (FILTER ? GBN * 4 : 0);
-  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  set_max_lds((const void*)k, lds);
   hipLaunchKernelGGL(k, grid, block, lds, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
                      n_ctiles, d_pad / GBK, qscale, cscale, e);
   return launch_check("screen_gemm_kernel");

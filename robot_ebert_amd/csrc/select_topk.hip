@@ -452,8 +452,7 @@ static int select_launch(const float* vals, const int64_t* idx, int64_t ld, int6
   const size_t lds = select_lds_bytes(kprime);
   dim3 grid((unsigned)B, (unsigned)segs), block(STHREADS);
 #define EBT_SEL_LAUNCH(H, V)                                                                  \
-  (void)hipFuncSetAttribute((const void*)select_topk_kernel<H, V, SEL_TPI(H)>,                \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
+  set_max_lds((const void*)select_topk_kernel<H, V, SEL_TPI(H)>, (int)lds);                    \
   hipLaunchKernelGGL((select_topk_kernel<H, V, SEL_TPI(H)>), grid, block, lds, stream, vals, \
                      idx, ld, n, seg_len, idx_base, (int)kprime, out_vals, out_idx, ld_out)
   if (idx) {
@@ -736,9 +735,7 @@ static int merge_segment_part(float* fv, int64_t* fi, int64_t B, int kprime,
     set_error("merge_segment: %lld groups do not fit the LDS", (long long)n_groups);
     return EBT_EINVAL;
   }
-  (void)hipFuncSetAttribute((const void*)merge_segment_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)((size_t)P_max * 8 + gb_bytes));
+  set_max_lds((const void*)merge_segment_kernel, (int)((size_t)P_max * 8 + gb_bytes));
   // with an expected hit count (and an ovf array for the deferral bit): a first pass with room
   // for 3x the expected hits, at 4+ workgroups per CU instead of 1, then the full-size pass for
   // the (rare) queries that did not fit

@@ -72,8 +72,7 @@ def _user_ratings(user_id: str) -> pd.DataFrame:
         raise KeyError("tmdb_id")
     df = pd.DataFrame(rows)
     cat = movies_collab_catalog
-    pos = cat.index_pos
-    return df[df["tmdb_id"].isin(pos.keys())]
+    return df[cat.contains(df["tmdb_id"])]
 
 
 def user_query_lists(user_ratings: pd.DataFrame, catalog: Catalog,
@@ -102,7 +101,9 @@ def _user_request(user_id: str) -> Optional[Tuple[List[int], List[int]]]:
         if not user_ratings:
             return None
     user_ratings = pd.DataFrame(user_ratings)
-    user_ratings = user_ratings[user_ratings["tmdb_id"].isin(cat.index_pos.keys())]  # lib.py:44
+    # lib.py:44's isin over the catalog index, as a per-rating membership test (isin over the
+    # dict's keys rebuilt a 1M-entry hash table per request: ~0.2 s at C3's catalog size)
+    user_ratings = user_ratings[cat.contains(user_ratings["tmdb_id"])]  # lib.py:44
     liked, rated = user_query_lists(user_ratings, cat)  # lib.py:47-48
     if not liked:  # sklearn check_pairwise_arrays on an empty X (lib.py:51)
         raise ValueError(f"Found array with 0 sample(s) (shape=(0, {cat.d})) while a minimum of 1 "

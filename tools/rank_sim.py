@@ -131,6 +131,16 @@ def main():
     run(timer)
     torch.cuda.synchronize()
     stages = {n: round(timer.query(n)[0] / a.steps, 4) for n in _lib.STAGES}
+    out = {"config": a.config, "world": W, "shard_rows": cat0.n,
+           "gathers_recorded": len(record), "gathers_per_step": per_step,
+           "recv_mb_per_step": round(sum(g.numel() * g.element_size() for g in record)
+                                     / a.steps / 1e6, 3),
+           "wall_ms_per_step": round(wall, 3), "replay_equals_threads": same,
+           "stages_ms_per_step_timed_run": stages,
+           "stage_sum_ms": round(sum(stages.values()), 3)}
+    if record[-1].dtype == torch.uint8:   # the packed results exchange (merge_packed)
+        print(json.dumps(out), flush=True)
+        return
     # the post-gather merge alone on the last recorded results (the last two gathers)
     from robot_ebert_amd.search import merge_topk
     gs, gr = record[-2], record[-1]
@@ -154,12 +164,8 @@ def main():
     diag = {"unsorted_lists": unsorted_lists, "lists": W * sc_.shape[1],
             "candidates_mean": round(float(cands.mean()), 1),
             "candidates_max": int(cands.max())}
-    print(json.dumps({"config": a.config, "world": W, "shard_rows": cat0.n,
-                      "gathers_recorded": len(record), "gathers_per_step": per_step,
-                      "wall_ms_per_step": round(wall, 3), "replay_equals_threads": same,
-                      "stages_ms_per_step_timed_run": stages,
-                      "stage_sum_ms": round(sum(stages.values()), 3),
-                      "merge_alone_ms": round(merge_alone, 4), "merge_lists": diag}), flush=True)
+    out.update(merge_alone_ms=round(merge_alone, 4), merge_lists=diag)
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

@@ -3,7 +3,7 @@ reference's concurrency: FastAPI runs the sync handler of
 /root/reference/src/backend/app/api/users.py:150-155 on up to 40 anyio worker threads, one user
 per call (lib.py:32-63). Here 40 request threads drive
 
-  * route:   lib.get_user_recs_batched (the same SQL on an in-memory SQLite ratings table, the
+  * route:   lib.get_user_recs_batched (the same SQL on a file-backed SQLite ratings table, the
              pandas filtering, the scoring coalesced by one batcher.RecBatcher, the hydration);
   * scoring: RecBatcher.submit(liked, rated, k) alone (the GPU path without SQL / hydration);
 
