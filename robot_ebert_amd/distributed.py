@@ -543,10 +543,18 @@ class TorchGatherComm:
 
     def __init__(self, rank: int, world: int, group: Optional[dist.ProcessGroup] = None,
                  gather=None) -> None:
+        import weakref
         self.rank, self.world, self.group = rank, world, group
         self._gather = gather
         self._bufs = []
-        self._fn = _lib.ALLGATHER_FN(self._callback)
+        # the C callback holds only a weak reference: a bound method would make a cycle
+        # (self -> callback -> self) that keeps the registered workspaces alive until a GC pass
+        ref = weakref.ref(self)
+
+        def cb(ctx, send, recv, nbytes, stream):
+            me = ref()
+            return me._callback(ctx, send, recv, nbytes, stream) if me is not None else -1
+        self._fn = _lib.ALLGATHER_FN(cb)
         self.error: Optional[BaseException] = None
 
     def register(self, t: torch.Tensor) -> None:

@@ -100,11 +100,15 @@ def _user_request(user_id: str) -> Optional[Tuple[List[int], List[int]]]:
         user_ratings = cnx.execute(statement).all()
         if not user_ratings:
             return None
-    user_ratings = pd.DataFrame(user_ratings)
-    # lib.py:44's isin over the catalog index, as a per-rating membership test (isin over the
-    # dict's keys rebuilt a 1M-entry hash table per request: ~0.2 s at C3's catalog size)
-    user_ratings = user_ratings[cat.contains(user_ratings["tmdb_id"])]  # lib.py:44
-    liked, rated = user_query_lists(user_ratings, cat)  # lib.py:47-48
+    # lib.py:43-48 on the fetched rows in plain Python (the DataFrame construction and boolean
+    # indexing cost ~2 ms of interpreter time per request, under FastAPI's 40 worker threads
+    # all of it serialised on the GIL): keep the ratings of catalog movies (the isin of :44),
+    # liked = ratings >= LIKED_MOVIE_SCORE in row order (:47), rated = their ids in first-seen
+    # order (:48, pd.unique) -- the lists user_query_lists builds from the DataFrame.
+    pos = cat.index_pos
+    kept = [(r.tmdb_id, r.rating) for r in user_ratings if r.tmdb_id in pos]  # lib.py:44
+    liked = cat.rows_of([t for t, rt in kept if rt >= LIKED_MOVIE_SCORE])     # lib.py:47
+    rated = cat.rows_of(list(dict.fromkeys(t for t, _ in kept)))              # lib.py:48
     if not liked:  # sklearn check_pairwise_arrays on an empty X (lib.py:51)
         raise ValueError(f"Found array with 0 sample(s) (shape=(0, {cat.d})) while a minimum of 1 "
                          "is required by check_pairwise_arrays.")

@@ -108,6 +108,8 @@ def _sharded_at_scale(cuda_device, cfg, n_sample, excl_per_query=0, check_plan=N
         return outs
     _log(f"{n} x {cfg['d']} {cfg['dtype']}, B={B}, k={k}: {WORLD} thread ranks, {path} path")
     res = _run_sharded(full, WORLD, body if path == "python" else body_c)
+    import gc
+    gc.collect()
     torch.cuda.empty_cache()
     _log("sharded batches done; single-GPU reference")
     whole = ebt.Catalog(full)
