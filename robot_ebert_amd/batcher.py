@@ -6,17 +6,19 @@ The reference serves one user per call: FastAPI runs the sync handler ``get_user
 ``lib.get_user_recs`` (``lib.py:32-63``) with B = 1. On MI355X a 1-query screen wastes the chip, so
 request threads hand their (liked rows, rated rows, k) to ONE dispatcher thread that waits at
 most ``max_wait_ms`` for company, runs a single batched search over up to ``max_batch`` users and
-hands each caller its own slice. The dispatcher is the only thread that touches the GPU (and, for a
-sharded catalog, the process group: RCCL communicators must not be used concurrently, SURVEY §8b
-"Threading").
+hands each caller its own slice. Only the batcher's threads touch the GPU; with an injected
+``score_fn`` (e.g. a sharded catalog's step, whose RCCL communicators must not be used
+concurrently, SURVEY §8b "Threading") only the dispatcher does.
 
 * k classes: a batch runs at the largest k among its requests, so requests are grouped by k class
   (``K_CLASSES``: the screen's k' and merge path change with k) and a large-k request does not pull
   small-k users onto the large-k path.
-* Pipelining (default scoring): a batch is submitted (``search.score_topk_submit``: its kernels
-  enqueued) and the dispatcher goes on collecting the next requests; the batch is finished and its
-  callers answered as soon as its GPU work is done (an event polled between collection waits), so
-  collection and GPU work overlap. With an injected ``score_fn`` the batch runs synchronously.
+* Pipelining (default scoring): the dispatcher submits a batch (``search.score_topk_submit``: its
+  kernels enqueued) and goes back to collecting; a completion thread finishes the batches in
+  order (``score_topk_finish``: it waits in the C library, without the GIL) and answers their
+  callers, so collection and GPU work overlap and no thread polls (under FastAPI's 40 request
+  threads every wake-up competes for the GIL). At most ``max_inflight`` batches are submitted and
+  not yet finished. With an injected ``score_fn`` the batch runs synchronously.
 * Bounded statistics: ``batches`` keeps the sizes of the last ``history`` batches; ``stats()``
   gives totals and a power-of-two batch-size histogram.
 
@@ -38,7 +40,6 @@ import numpy as np
 _SENTINEL = object()
 # requests with k in (K_CLASSES[i-1], K_CLASSES[i]] share a batch; the last class is unbounded
 K_CLASSES = (32, 128, 512, 4096)
-POLL_S = 2e-4   # how often a waiting dispatcher checks its in-flight batches
 
 
 def k_class(k: int) -> int:
@@ -70,7 +71,13 @@ class RecBatcher:
         self._n_batches = 0
         self._n_requests = 0
         self._hist: Dict[int, int] = collections.Counter()
-        self._inflight: collections.deque = collections.deque()
+        self._done: "queue.Queue" = queue.Queue()      # submitted batches, in order
+        self._slots = threading.Semaphore(self.max_inflight)
+        self._completer = None
+        if self._pipelined:
+            self._completer = threading.Thread(target=self._complete, name="ebert-batcher-done",
+                                               daemon=True)
+            self._completer.start()
         self._thread = threading.Thread(target=self._run, name="ebert-batcher", daemon=True)
         self._thread.start()
 
@@ -103,6 +110,8 @@ class RecBatcher:
             self._closed = True
             self._q.put(_SENTINEL)
         self._thread.join(timeout)
+        if self._completer is not None:
+            self._completer.join(timeout)
 
     def stats(self) -> dict:
         """Totals since start and the batch-size histogram (bin b = sizes in [2^b, 2^(b+1)))."""
@@ -111,34 +120,17 @@ class RecBatcher:
                 "size_hist_pow2": dict(sorted(self._hist.items()))}
 
     # ---- dispatcher thread ---------------------------------------------------------------------
-    def _get(self, timeout: Optional[float]):
-        """The next queued item within `timeout` seconds (None: wait forever), completing
-        in-flight batches whose GPU work is done while waiting; raises queue.Empty."""
-        end = None if timeout is None else time.monotonic() + timeout
-        while True:
-            self._reap(block=False)
-            if not self._inflight:
-                left = None if end is None else end - time.monotonic()
-                if left is not None and left <= 0:
-                    return self._q.get_nowait()
-                return self._q.get(timeout=left)
-            step = POLL_S if end is None else min(POLL_S, max(end - time.monotonic(), 0.0))
-            try:
-                return self._q.get(timeout=step) if step > 0 else self._q.get_nowait()
-            except queue.Empty:
-                if end is not None and time.monotonic() >= end:
-                    raise
-
     def _collect(self) -> Tuple[list, bool]:
-        first = self._get(None)
+        first = self._q.get()
         if first is _SENTINEL:
             return [], True
         reqs = [first]
         deadline = time.monotonic() + self.max_wait
         stop = False
         while len(reqs) < self.max_batch:
+            left = deadline - time.monotonic()
             try:
-                item = self._get(max(deadline - time.monotonic(), 0.0))
+                item = self._q.get(timeout=left) if left > 0 else self._q.get_nowait()
             except queue.Empty:
                 break
             if item is _SENTINEL:
@@ -164,8 +156,7 @@ class RecBatcher:
                         break
                     if item is not _SENTINEL:
                         self._dispatch([item])
-                while self._inflight:
-                    self._reap(block=True)
+                self._done.put(_SENTINEL)
                 return
 
     def _record(self, n: int) -> None:
@@ -186,38 +177,34 @@ class RecBatcher:
                 return
             self._deliver(reqs, scores, rows)
             return
-        import torch
         from .search import score_topk_submit
-        while len(self._inflight) >= self.max_inflight:
-            self._reap(block=True)
+        self._slots.acquire()            # released by the completion thread
         try:
             p = score_topk_submit(self.catalog, k_max, liked=liked, exclude=excl)
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.catalog.device))
         except BaseException as e:
+            self._slots.release()
             for r in reqs:
                 r[3].set_exception(e)
             return
-        self._inflight.append((p, ev, reqs))
+        self._done.put((p, reqs))
 
-    def _reap(self, block: bool) -> None:
-        """Finish the oldest in-flight batches whose first pass is done (all of them in order,
-        stopping at the first one still running unless `block`)."""
+    def _complete(self) -> None:
+        """Completion thread: finish the submitted batches in order and answer their callers."""
         from .search import score_topk_finish
-        while self._inflight:
-            p, ev, reqs = self._inflight[0]
-            if not block and not ev.query():
+        while True:
+            item = self._done.get()
+            if item is _SENTINEL:
                 return
-            self._inflight.popleft()
+            p, reqs = item
             try:
                 scores, rows = score_topk_finish(p)
             except BaseException as e:
+                self._slots.release()
                 for r in reqs:
                     r[3].set_exception(e)
                 continue
             self._deliver(reqs, scores, rows)
-            if block:
-                return
+            self._slots.release()
 
     def _deliver(self, reqs: list, scores, rows) -> None:
         try:
