@@ -557,7 +557,12 @@ def main() -> None:
         if args.share_gpu:
             comm = TorchGatherComm(rank, world)
         else:
-            rccl = comm = RcclComm()
+            try:
+                rccl = comm = RcclComm()
+            except Exception as e:  # noqa: BLE001 -- same collectives through torch.distributed
+                log(f"rank {rank}: libebert's RCCL communicator failed ({e}); all-gathers go "
+                    "through torch.distributed instead")
+                comm = TorchGatherComm(rank, world)
         eng = ShardedTopk(cat, k, cfg["b"], comm, timer=timer)
 
     def run_steps(n, log_every=0):
@@ -642,6 +647,9 @@ def main() -> None:
             "rccl_world_size": (dist.get_world_size() if dist is not None and not args.share_gpu
                                 else (1 if dist is None else 0)),
             "sharded_path": (args.sharded_path if world > 1 else None),
+            "sharded_allgather": (None if world == 1 else
+                                  "libebert RCCL (ebt_rccl_all_gather)" if rccl is not None else
+                                  "torch.distributed all_gather_into_tensor"),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3),

@@ -516,10 +516,16 @@ class RcclComm:
         lib = _lib.load()
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
         uid = ctypes.create_string_buffer(128)
-        if self.rank == 0:
-            call("ebt_rccl_unique_id", uid, 128)
-        obj = [uid.raw if self.rank == 0 else None]
+        obj = [None]
+        if self.rank == 0:   # a failure here reaches every rank (None), never half of them
+            try:
+                call("ebt_rccl_unique_id", uid, 128)
+                obj = [uid.raw]
+            except EbertError:
+                obj = [None]
         dist.broadcast_object_list(obj, src=0, group=group)
+        if obj[0] is None:
+            raise EbertError("ebt_rccl_unique_id failed on rank 0 (RCCL not loadable?)")
         uid = ctypes.create_string_buffer(obj[0], 128)
         h = ctypes.c_void_p()
         call("ebt_rccl_comm_init", uid, self.rank, self.world, ctypes.byref(h))
