@@ -39,6 +39,32 @@ def test_invalid_args_return_einval_without_gpu():
     assert lib.ebt_merge_topk(None, None, 0, 1, 1, None, None, None) == -1
 
 
+def test_compact_exchange_sizing_and_args_without_gpu():
+    """The compact N > 1 exchange's sizing (ebt_shard_list_width, ebt_shard_pack_cap / _bytes)
+    and argument checks are host code: C3/8 sends 27 entries per query for the floor and packs
+    at most 27 results per query per rank; the compact form is off for one rank, for R k > 8192
+    and for catalogs of 2^31 rows or more."""
+    from robot_ebert_amd import _lib
+    lib = _lib.load()
+    assert lib.ebt_shard_list_width(100, 8) == 27          # ceil(1.5 * 100 / 8) + 8
+    assert lib.ebt_shard_list_width(1000, 8) == 196
+    assert lib.ebt_shard_list_width(7, 2) == 7             # never more than k
+    cap = lib.ebt_shard_pack_cap(4096, 100, 8, 1_000_000)
+    assert cap == 4096 * 27
+    nb = lib.ebt_shard_pack_bytes(4096, cap)
+    assert nb % 256 == 0 and nb >= 4 * (4096 + 1) + 12 * cap
+    assert nb * 8 <= 12 * 2 ** 20                           # the results gather at C3/8 <= 12 MB
+    assert lib.ebt_shard_pack_cap(4096, 100, 1, 1_000_000) == 0
+    assert lib.ebt_shard_pack_cap(16, 2000, 8, 1_000_000) == 0
+    assert lib.ebt_shard_pack_cap(16, 100, 8, 2 ** 31) == 0
+    assert lib.ebt_shard_pack(None, None, 4, 10, None, 40, None, None) == -1
+    assert b"ebt_shard_pack" in lib.ebt_last_error()
+    assert lib.ebt_merge_packed(None, 8, 4, 10, 40, None, None, None, None) == -1
+    assert lib.ebt_floor_pack(None, 10, 4, 10, 3, None, None, None) == -1
+    assert lib.ebt_cosine_topk_sharded_finish(None) == -1
+    assert lib.ebt_cosine_topk_sharded_wait(None) == -1
+
+
 def test_workspace_grows_with_chunks():
     from robot_ebert_amd import _lib
     lib = _lib.load()
