@@ -1041,9 +1041,10 @@ extern "C" int ebt_debug_clock_stamps(unsigned long long* buf) {
 // MI355X ("screening GEMM"): a 4-slot ring with k32 slices, one barrier per phase
 // with two barriers (qp), a persistent one-workgroup-per-CU walk of the same tiles, and a
 // 4-wave 128 x 128-per-wave tile (LDS-DMA issue cost with one wave per SIMD).
-// Compute units of the current device (the persistent grid size), cached per device. The cache
-// is the library's only process-wide state: relaxed atomics (every writer stores the same value,
-// so concurrent first calls from the serving threads race on nothing).
+// Compute units of the current device (the persistent grid size), cached per device: relaxed
+// atomics (every writer stores the same value, so concurrent first calls from the serving
+// threads race on nothing). The library's other process-wide state (api.hip: the LDS-attribute
+// cache and the event pool; rccl_comm.hip: the RCCL entry points) is behind locks.
 static int64_t n_cus() {
   static std::atomic<int64_t> cache[64];
   int dev = 0;
