@@ -396,10 +396,11 @@ int ebt_cosine_topk_finish(ebt_pending* pending);
  * whose row_offset is the shard's first GLOBAL row) and calls ebt_cosine_topk_sharded with the
  * same queries, k and exclusions; every rank returns the same GLOBAL top-k, equal to
  * ebt_cosine_topk over the whole catalog (rows bit-exact, float64 scores). For liked queries
- * that holds when each user's liked rows are listed in ascending order (the order
- * lib.user_query_lists produces): the shards' partial sums are added in rank order, which is
- * then the single-GPU order of additions; an unsorted list gives the same query up to float64
- * round-off of its sum (near-tied rows may then swap). Per batch:
+ * the query is the same up to float64 round-off of its sum: each shard sums its own liked rows
+ * and the partial sums are added in rank order, so the additions are grouped by shard (equal to
+ * the single-GPU sum when no shard after the first holds two of a user's liked rows); rows
+ * within round-off of a tie may then swap -- as they may against the reference itself, which
+ * averages the per-row cosine scores instead of the rows (lib.py:51-52). Per batch:
  *   query prep (liked rows: each shard sums its own, one all-gather of the [B][d] float64
  *   partial sums completes the means); when the shards are small (<= 200K rows, >= 2 ranks, the
  *   fused screen) a catalog-wide screening threshold from every shard's sample maxima (one

@@ -361,13 +361,15 @@ def test_sharded_capi_packed_overflow_falls_back(cuda_device, lib, hip):
 
 
 def test_sharded_capi_unsorted_liked(cuda_device, lib, hip):
-    """Liked rows listed out of order (include/ebert.h: the shards' partial sums are then added
-    in another order than the single-GPU sum): the same rows, scores within float64 round-off."""
+    """Liked rows out of order, or several on a later shard (include/ebert.h: the shards'
+    partial sums group the additions by shard): the reference's rows, scores within float64
+    round-off of the oracle (which averages the per-row cosines, lib.py:51-52)."""
     n, d, k, world = 30_000, 64, 40, 3
     c = gaussian(261, n, d, "f64")
-    liked = [[29_999, 1, 2], [20_002, 10_000, 5], [12_000, 6_000, 29_995, 3]]
+    liked = [[29_999, 1, 2], [20_002, 10_000, 5], [12_000, 6_000, 29_995, 3],
+             [1, 10_001, 10_002, 10_003, 20_004, 20_005]]
     full = torch.from_numpy(c).to(cuda_device)
-    off = torch.tensor([0, 3, 6, 10], dtype=torch.int64, device=cuda_device)
+    off = torch.tensor([0, 3, 6, 10, 16], dtype=torch.int64, device=cuda_device)
     rows = torch.tensor(sum(liked, []), dtype=torch.int64, device=cuda_device)
     res, calls = run_ranks(lib, hip, full, world, k, liked=(off, rows))
     want_s, want_r = R.liked_topk(c, liked, k, [[] for _ in liked])
