@@ -425,21 +425,30 @@ int ebt_cosine_topk_finish(ebt_pending* pending);
  * returns when the results are final. Workspace: ebt_sharded_workspace_bytes (device). */
 typedef int (*ebt_allgather_fn)(void* ctx, const void* send, void* recv, size_t bytes,
                                 void* stream);
+/* Optional: buf[0 .. count) (device float64) <- the sum over ranks of every rank's buf, in place
+ * (RCCL: ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, comm, stream)). The liked path's
+ * partial sums use it when it is set -- about 2 / R of the all-gather's volume; the sum's order
+ * of additions is then the collective's, a float64 round-off-level difference -- else an
+ * all-gather of every rank's partial sums added in rank order. NULL = not provided. */
+typedef int (*ebt_allreduce_f64_fn)(void* ctx, double* buf, size_t count, void* stream);
 typedef struct ebt_comm {
   int32_t rank, world;
   int64_t n_global;           /* rows of the whole catalog: every shard's row_offset + n <= it */
   ebt_allgather_fn all_gather;
   void* ctx;
+  ebt_allreduce_f64_fn all_reduce_f64;  /* optional (NULL), same ctx */
 } ebt_comm;
 /* An RCCL communicator for an ebt_comm: the library opens librccl.so.1 at first use (it does not
  * link it). Rank 0 calls ebt_rccl_unique_id (128 bytes) and hands the id to every rank out of
  * band (e.g. a torch.distributed broadcast); each rank calls ebt_rccl_comm_init with its HIP
- * device current; then comm.all_gather = ebt_rccl_all_gather, comm.ctx = the handle
- * (ncclAllGather of `bytes` int8 on `stream`). EBT_EUNSUPPORTED when RCCL cannot be loaded. */
+ * device current; then comm.all_gather = ebt_rccl_all_gather, comm.all_reduce_f64 =
+ * ebt_rccl_all_reduce_f64, comm.ctx = the handle (ncclAllGather of `bytes` int8, ncclAllReduce
+ * of float64 sums, on `stream`). EBT_EUNSUPPORTED when RCCL cannot be loaded. */
 int ebt_rccl_unique_id(void* id_out, size_t bytes);
 int ebt_rccl_comm_init(const void* id, int32_t rank, int32_t world, void** comm_out);
 int ebt_rccl_comm_destroy(void* comm);
 int ebt_rccl_all_gather(void* comm, const void* send, void* recv, size_t bytes, void* stream);
+int ebt_rccl_all_reduce_f64(void* comm, double* buf, size_t count, void* stream);
 size_t ebt_sharded_workspace_bytes(const ebt_catalog* cat, const ebt_comm* comm, int64_t B,
                                    int32_t k, const ebt_options* opt);
 /* The same in three calls, so that a caller can keep batches in flight (the collectives and

@@ -59,10 +59,15 @@ class EbtPending(ctypes.Structure):
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, _VP, _VP, _VP, _SZ, _VP)
 
 
+ALLREDUCE_F64_FN = ctypes.CFUNCTYPE(ctypes.c_int, _VP, _VP, _SZ, _VP)
+
+
 class EbtComm(ctypes.Structure):
-    """include/ebert.h `ebt_comm`: the caller's all-gather for ebt_cosine_topk_sharded."""
+    """include/ebert.h `ebt_comm`: the caller's all-gather (and optional float64 all-reduce)
+    for ebt_cosine_topk_sharded."""
     _fields_ = [("rank", _I32), ("world", _I32), ("n_global", _I64),
-                ("all_gather", ALLGATHER_FN), ("ctx", _VP)]
+                ("all_gather", ALLGATHER_FN), ("ctx", _VP),
+                ("all_reduce_f64", ALLREDUCE_F64_FN)]
 
 
 class EbtShardedPending(ctypes.Structure):
@@ -98,6 +103,7 @@ _SIGNATURES = {
     "ebt_rccl_comm_init": ([_VP, _I32, _I32, ctypes.POINTER(_VP)], _INT),
     "ebt_rccl_comm_destroy": ([_VP], _INT),
     "ebt_rccl_all_gather": ([_VP, _VP, _VP, _SZ, _VP], _INT),
+    "ebt_rccl_all_reduce_f64": ([_VP, _VP, _SZ, _VP], _INT),
     "ebt_shard_list_width": ([_I32, _I32], _I64),
     "ebt_shard_pack_cap": ([_I64, _I32, _I32, _I64], _I64),
     "ebt_shard_pack_bytes": ([_I64, _I64], _SZ),

@@ -824,7 +824,7 @@ bool shard_layout(const ebt_catalog& c, const ebt_comm& cm, int64_t B, int32_t k
   L.off_scale = o;
   o = al(o + (size_t)B * 8);
   L.off_qrecv = o;
-  o = al(o + (size_t)R * B * c.d * 8);  // the liked path's gathered partial sums
+  if (!cm.all_reduce_f64) o = al(o + (size_t)R * B * c.d * 8);  // the liked path's gathered sums
   L.off_psend = o;
   o = al(o + L.pack_bytes);
   L.off_precv = o;
@@ -921,11 +921,22 @@ int prep_liked_sharded(const ebt_catalog& c, const ebt_comm& cm, const int64_t* 
   double* q64 = (double*)(base + P.q64);
   rc = query_liked_sum(c.data, c.dtype, c.d, c.ld, c.gnorm64, B, off, rows, q64, st,
                        c.row_offset, c.n);
-  if (!rc) rc = sh_gather(cm, q64, qrecv, (size_t)B * c.d * 8, timer, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(sum_ranks_kernel, dim3(grid_for(B * c.d)), dim3(256), 0, st, qrecv,
-                     (int)cm.world, B * c.d, q64);
-  rc = launch_check("sum_ranks_kernel");
+  if (cm.all_reduce_f64) {  // the caller's all-reduce (RCCL: about 2 / R of the gather's bytes)
+    if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_COLLECTIVE, st);
+    const int e = cm.all_reduce_f64(cm.ctx, q64, (size_t)B * c.d, (void*)st);
+    if (timer) (void)ebt_timer_end(timer, EBT_STAGE_COLLECTIVE, st);
+    if (e) {
+      set_error("ebt_cosine_topk_sharded: the caller's all_reduce_f64 returned %d", e);
+      return EBT_EHIP;
+    }
+  } else {
+    rc = sh_gather(cm, q64, qrecv, (size_t)B * c.d * 8, timer, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(sum_ranks_kernel, dim3(grid_for(B * c.d)), dim3(256), 0, st, qrecv,
+                       (int)cm.world, B * c.d, q64);
+    rc = launch_check("sum_ranks_kernel");
+  }
   if (!rc) rc = ebt_scale_rows_f64(q64, B, c.d, d_scale, st);
   if (rc) return rc;
   return ebt_query_image(q64, B, pad_batch(B), c.d, c.img_dtype, nullptr, 0, 0, c.u_cat,

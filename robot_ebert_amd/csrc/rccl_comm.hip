@@ -22,6 +22,7 @@ struct RcclApi {
   decltype(&ncclCommInitRank) comm_init_rank = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
   decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
   bool ok = false;
 };
@@ -37,9 +38,10 @@ const RcclApi* rccl_api() {
     api.comm_init_rank = (decltype(api.comm_init_rank))dlsym(h, "ncclCommInitRank");
     api.comm_destroy = (decltype(api.comm_destroy))dlsym(h, "ncclCommDestroy");
     api.all_gather = (decltype(api.all_gather))dlsym(h, "ncclAllGather");
+    api.all_reduce = (decltype(api.all_reduce))dlsym(h, "ncclAllReduce");
     api.error_string = (decltype(api.error_string))dlsym(h, "ncclGetErrorString");
     api.ok = api.get_unique_id && api.comm_init_rank && api.comm_destroy && api.all_gather &&
-             api.error_string;
+             api.all_reduce && api.error_string;
   });
   return api.ok ? &api : nullptr;
 }
@@ -108,6 +110,18 @@ int ebt_rccl_all_gather(void* comm, const void* send, void* recv, size_t bytes, 
   return rccl_check(a, a->all_gather(send, recv, bytes, ncclInt8, (ncclComm_t)comm,
                                      (hipStream_t)stream),
                     "ncclAllGather");
+}
+
+// ebt_allreduce_f64_fn over the same handle: buf <- the sum over ranks, in place, on `stream`
+int ebt_rccl_all_reduce_f64(void* comm, double* buf, size_t count, void* stream) {
+  const RcclApi* a = rccl_api();
+  if (!a || !comm) {
+    set_error("ebt_rccl_all_reduce_f64: no communicator");
+    return EBT_EINVAL;
+  }
+  return rccl_check(a, a->all_reduce(buf, buf, count, ncclFloat64, ncclSum, (ncclComm_t)comm,
+                                     (hipStream_t)stream),
+                    "ncclAllReduce");
 }
 
 }  // extern "C"

@@ -531,9 +531,10 @@ class RcclComm:
         call("ebt_rccl_comm_init", uid, self.rank, self.world, ctypes.byref(h))
         self.handle = h.value
         self._fn = ctypes.cast(lib.ebt_rccl_all_gather, _lib.ALLGATHER_FN)
+        self._sum = ctypes.cast(lib.ebt_rccl_all_reduce_f64, _lib.ALLREDUCE_F64_FN)
 
     def comm(self, n_global: int) -> "_lib.EbtComm":
-        return _lib.EbtComm(self.rank, self.world, n_global, self._fn, self.handle)
+        return _lib.EbtComm(self.rank, self.world, n_global, self._fn, self.handle, self._sum)
 
     def close(self) -> None:
         if self.handle:

@@ -24,9 +24,9 @@ VP, I32, I64, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_siz
 GATHER = ctypes.CFUNCTYPE(ctypes.c_int, VP, VP, VP, SZ, VP)
 
 
-class Comm(ctypes.Structure):   # struct ebt_comm
+class Comm(ctypes.Structure):   # struct ebt_comm (all_reduce_f64 left NULL: the gather path)
     _fields_ = [("rank", I32), ("world", I32), ("n_global", I64), ("all_gather", GATHER),
-                ("ctx", VP)]
+                ("ctx", VP), ("all_reduce_f64", VP)]
 
 
 class Options(ctypes.Structure):   # struct ebt_options
@@ -88,13 +88,18 @@ def shard_cuts(n, world):
     return cuts
 
 
-def run_ranks(lib, hip, full, world, k, q=None, liked=None, excl=None, fail_rank=-1):
-    """ebt_cosine_topk_sharded on `world` thread ranks; returns per-rank (rc, message, s, r)."""
+REDUCE = ctypes.CFUNCTYPE(ctypes.c_int, VP, VP, SZ, VP)
+
+
+def run_ranks(lib, hip, full, world, k, q=None, liked=None, excl=None, fail_rank=-1,
+              allreduce=False):
+    """ebt_cosine_topk_sharded on `world` thread ranks; returns per-rank (rc, message, s, r).
+    allreduce: the comm also offers all_reduce_f64 (a barrier exchange summing in rank order)."""
     dev = full.device
     n = full.shape[0]
     cuts = shard_cuts(n, world)
     shared = {"slots": [None] * world, "barrier": threading.Barrier(world, timeout=120),
-              "calls": [0] * world}
+              "calls": [0] * world, "rslots": [None] * world, "reduces": [0] * world}
     cats = []
     for r in range(world):
         cat, state = make_catalog(lib, full[cuts[r]:cuts[r + 1]])
@@ -119,8 +124,28 @@ def run_ranks(lib, hip, full, world, k, q=None, liked=None, excl=None, fail_rank
                 return 0
             except threading.BrokenBarrierError:
                 return -9
+        def reduce(ctx, buf, count, stream):
+            try:
+                shared["reduces"][rank] += 1
+                hip.hipStreamSynchronize(stream)
+                mine = torch.empty(count, dtype=torch.float64, device=dev)
+                if hip.hipMemcpy(mine.data_ptr(), buf, count * 8, 3):
+                    return -1
+                shared["rslots"][rank] = mine
+                shared["barrier"].wait()
+                acc = shared["rslots"][0].clone()
+                for src in range(1, world):
+                    acc += shared["rslots"][src]
+                torch.cuda.synchronize(dev)
+                if hip.hipMemcpy(buf, acc.data_ptr(), count * 8, 3):
+                    return -1
+                shared["barrier"].wait()
+                return 0
+            except threading.BrokenBarrierError:
+                return -9
         cb = GATHER(gather)
-        comm = Comm(rank, world, n, cb, None)
+        rcb = REDUCE(reduce)
+        comm = Comm(rank, world, n, cb, None, ctypes.cast(rcb, VP) if allreduce else None)
         cat = cats[rank][0]
         B = q.shape[0] if q is not None else liked[0].numel() - 1
         need = lib.ebt_sharded_workspace_bytes(ctypes.byref(cat), ctypes.byref(comm), B, k, None)
@@ -142,6 +167,8 @@ def run_ranks(lib, hip, full, world, k, q=None, liked=None, excl=None, fail_rank
     for t in ts:
         t.join(300)
     assert all(o is not None for o in out), "a rank did not finish"
+    if allreduce:
+        return out, shared["calls"], shared["reduces"]
     return out, shared["calls"]
 
 
@@ -377,3 +404,27 @@ def test_sharded_capi_unsorted_liked(cuda_device, lib, hip):
         assert rc == 0, msg
         np.testing.assert_array_equal(r, want_r)
         np.testing.assert_allclose(s, want_s, rtol=0, atol=1e-12)
+
+
+def test_sharded_capi_liked_all_reduce(cuda_device, lib, hip):
+    """The liked path over a comm that offers all_reduce_f64 (RCCL's ncclAllReduce on a node):
+    the partial sums go through one all-reduce instead of an all-gather (here a barrier
+    exchange summing in rank order, the gather path's order, so the answer is the gather path's
+    bit for bit) and the workspace drops the gathered-sums buffer."""
+    n, d, k, world = 30_000, 64, 40, 3
+    c = gaussian(221, n, d, "f64")
+    liked = [[1, 2, 29_999], [10_000], [5, 6_000, 12_000, 29_995], [20_001, 20_002]]
+    rated = [sorted(set(x) | {7, 8, 29_980}) for x in liked]
+    full = torch.from_numpy(c).to(cuda_device)
+    lk, ex = csr(liked, cuda_device), csr(rated, cuda_device)
+    res, calls, reduces = run_ranks(lib, hip, full, world, k, liked=lk, excl=ex, allreduce=True)
+    assert calls == [2] * world and reduces == [1] * world   # floor, packed; the partial sums
+    s1, r1 = check_equal_single(lib, full, res, k, liked=lk, excl=ex)
+    want_s, want_r = R.liked_topk(c, liked, k, rated)
+    np.testing.assert_array_equal(r1, want_r)
+    cat, state = make_catalog(lib, full[:10_000])
+    g = Comm(0, world, n, GATHER(lambda *a: 0), None, None)
+    g2 = Comm(0, world, n, GATHER(lambda *a: 0), None, ctypes.cast(REDUCE(lambda *a: 0), VP))
+    need_g = lib.ebt_sharded_workspace_bytes(ctypes.byref(cat), ctypes.byref(g), 4096, k, None)
+    need_r = lib.ebt_sharded_workspace_bytes(ctypes.byref(cat), ctypes.byref(g2), 4096, k, None)
+    assert need_g - need_r >= world * 4096 * d * 8
