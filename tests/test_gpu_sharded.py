@@ -446,6 +446,12 @@ def test_rccl_comm_capi_world1(cuda_device):
                       _lib.stream_of(cuda_device))
             torch.cuda.synchronize()
             assert torch.equal(x, y)
+            z = torch.linspace(-1, 1, 777, dtype=torch.float64, device=cuda_device)
+            z0 = z.clone()
+            _lib.call("ebt_rccl_all_reduce_f64", rc.handle, _lib.ptr(z), 777,
+                      _lib.stream_of(cuda_device))
+            torch.cuda.synchronize()
+            assert torch.equal(z, z0)   # one rank: the sum is its own buffer
             eng = ShardedTopk(cat, k, B, rc)
             s, r = eng.run(4, q)
             torch.cuda.synchronize()
