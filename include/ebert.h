@@ -551,7 +551,8 @@ int ebt_cosine_screen_at(const double* q64, const void* qimg, const float* qscal
 int ebt_union_floor(const float* gathered, int32_t R, int64_t B, int32_t ld, int32_t k,
                     double* t_floor, void* stream);
 /* What a shard sends for that floor: out[b] = (the w largest of list_vals[b*ld + 0 .. n),
- * n = min(k_eff, ld), -inf padded to w; then eps[b]) as [B][w + 1] float32. The list may be
+ * n = min(k_eff, ld), -inf padded to w; then eps[b], or -inf when eps is NULL) as [B][w + 1]
+ * float32. The list may be
  * partitioned (any order): the w largest are selected. w = ebt_shard_list_width(k, world)
  * narrows the gather: the k-th largest over a subset of the shards' values is still a lower
  * bound, and with w >= a shard's share of the global top k it is the same bound. */

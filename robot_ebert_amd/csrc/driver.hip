@@ -739,7 +739,7 @@ int64_t sh_tiles(int64_t n_global, int world, int64_t B_pad) {
 
 struct ShardLayout {
   DriverLayout D;
-  int64_t tiles, G, RG;
+  int64_t tiles, G, RG, J, GJ;  // sample maxima per shard (G), sent per shard (J + 1 of them)
   size_t screen_bytes;
   int64_t fw, cap;  // floor gather width per shard and query; packed results per rank (0: full)
   size_t pack_bytes;
@@ -770,6 +770,17 @@ bool shard_layout(const ebt_catalog& c, const ebt_comm& cm, int64_t B, int32_t k
   L.G = 4 * L.tiles;
   L.RG = R * L.G;
   if (L.RG > 2048) L.tiles = L.G = L.RG = 0;  // ebt_pool_kth's limit (not reached: <= 8 x 32)
+  // theta = the j-th largest of all R G maxima, j <= J (J from the catalog-wide k', rank-
+  // invariant, >= every rank's own j): the j-th of the union of each shard's J largest is the
+  // same value, so each shard sends its J largest (+ a -inf column: ebt_floor_pack's layout)
+  L.J = L.GJ = 0;
+  if (L.tiles) {
+    const double m_total = 256.0 * (double)L.tiles * R;
+    L.J = sh_spec_rank((double)kpg * m_total / (double)cm.n_global);
+    if (L.J > L.RG / 2) L.tiles = L.G = L.RG = L.J = 0;  // the sample would decide nothing
+    L.J = L.J < L.G ? L.J : L.G;
+    L.GJ = L.J + 1;
+  }
   size_t scr = ebt_cosine_topk_workspace(B, D.B_pad, c.n, D.kprime, D.chunk, D.flags);
   if (L.tiles) {
     const size_t t = ebt_cosine_topk_workspace(B, D.B_pad, c.n, D.kprime, D.chunk, EBT_FLAG_THETA);
@@ -786,9 +797,9 @@ bool shard_layout(const ebt_catalog& c, const ebt_comm& cm, int64_t B, int32_t k
   L.off_pool = o;
   o = al(o + (size_t)D.B_pad * L.G * 4);
   L.off_gsamp = o;
-  o = al(o + (size_t)R * B * L.G * 4);
+  o = al(o + (size_t)B * L.GJ * 4 * (R + 1));  // this shard's J largest, then every shard's
   L.off_perm = o;
-  o = al(o + (size_t)B * L.RG * 4);
+  o = al(o + (size_t)B * R * L.GJ * 4);
   L.off_theta = o;
   o = al(o + (size_t)D.B_pad * 4);
   L.off_lv = o;
@@ -1037,18 +1048,24 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
                              c.n, c.d_pad, own, stride, pool, S.G, timer, st);
       if (rc) return rc;
     }
-    rc = sh_gather(cm, pool, gsamp, (size_t)B * S.G * 4, timer, st);
+    float* send = gsamp;                          // [B][J + 1]
+    float* recv = gsamp + (size_t)B * S.GJ;       // [R][B][J + 1]
+    if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
+    rc = ebt_floor_pack(pool, S.G, B, (int32_t)S.G, (int32_t)S.J, nullptr, send, st);
+    if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
+    if (!rc) rc = sh_gather(cm, send, recv, (size_t)B * S.GJ * 4, timer, st);
     if (rc) return rc;
     const double m_total = 256.0 * (double)S.tiles * R;
     const int j = sh_spec_rank((double)L.kprime * m_total / (double)cm.n_global);
-    if (j <= S.RG / 2) {
+    if (j <= S.J) {
       float* perm = (float*)(ws + S.off_perm);
       theta = (float*)(ws + S.off_theta);
+      const int64_t RGJ = (int64_t)R * S.GJ;
       if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
-      hipLaunchKernelGGL(permute_samples_kernel, dim3(grid_for((int64_t)R * B * S.G)), dim3(256),
-                         0, st, gsamp, R, B, (int)S.G, perm);
+      hipLaunchKernelGGL(permute_samples_kernel, dim3(grid_for(RGJ * B)), dim3(256), 0, st, recv,
+                         R, B, (int)S.GJ, perm);
       rc = launch_check("permute_samples_kernel");
-      if (!rc) rc = ebt_pool_kth(perm, S.RG, B, L.B_pad, (int32_t)S.RG, j, theta, st);
+      if (!rc) rc = ebt_pool_kth(perm, RGJ, B, L.B_pad, (int32_t)RGJ, j, theta, st);
       if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
       if (rc) return rc;
       hits = ((double)j + (double)j * j / (2.0 * (double)S.RG)) * (double)c.n / m_total;

@@ -1650,14 +1650,14 @@ __global__ __launch_bounds__(256) void floor_pack_kernel(const float* __restrict
     }
   }
   for (int j = (base < w ? base : w) + lane; j < w; j += 64) dst[j] = -__builtin_inff();
-  if (lane == 0) dst[w] = eps[b];
+  if (lane == 0) dst[w] = eps ? eps[b] : -__builtin_inff();
 }
 }  // namespace ebt
 
 extern "C" int ebt_floor_pack(const float* list_vals, int64_t ld, int64_t B, int32_t k_eff,
                               int32_t w, const float* eps, float* out, void* stream) {
   using namespace ebt;
-  if (!list_vals || !eps || !out || B < 0 || ld < 1 || k_eff < 0 || w < 1 || k_eff > 4096) {
+  if (!list_vals || !out || B < 0 || ld < 1 || k_eff < 0 || w < 1 || k_eff > 4096) {
     set_error("ebt_floor_pack: bad arguments (ld=%lld k_eff=%d w=%d; k_eff <= 4096)",
               (long long)ld, k_eff, w);
     return EBT_EINVAL;

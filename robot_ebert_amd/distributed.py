@@ -225,14 +225,14 @@ def shard_list_width(k: int, world: int) -> int:
     return int(_lib.load().ebt_shard_list_width(k, world))
 
 
-def floor_send(vals: torch.Tensor, eps: torch.Tensor, w: int) -> torch.Tensor:
+def floor_send(vals: torch.Tensor, eps: Optional[torch.Tensor], w: int) -> torch.Tensor:
     """[B, w + 1] f32: the w largest of each row of vals (a partitioned list is fine), -inf
-    padded, then eps (ebt_floor_pack)."""
+    padded, then eps (-inf when None) (ebt_floor_pack)."""
     B, ld = vals.shape
     vals = vals.contiguous()
     out = torch.empty((B, w + 1), dtype=torch.float32, device=vals.device)
-    call("ebt_floor_pack", ptr(vals), ld, B, ld, w, ptr(eps.contiguous()), ptr(out),
-         stream_of(vals.device))
+    call("ebt_floor_pack", ptr(vals), ld, B, ld, w,
+         ptr(eps.contiguous()) if eps is not None else None, ptr(out), stream_of(vals.device))
     return out
 
 
@@ -270,14 +270,32 @@ def shared_sample_tiles(n_global: int, world: int, B_pad: int) -> int:
     return P if P >= 1 and world * P >= 8 else 0
 
 
-def _shared_theta(coll, catalog: Catalog, qb, kprime: int, tiles: int, timer=None):
-    """Catalog-wide screening threshold: every shard's sample maxima (ebt_cosine_sample), ONE
-    all-gather ([R, B, 4 tiles] f32), theta = the j-th largest of all R * 4 tiles maxima
-    (ebt_pool_kth), j from the Poisson bound of spec_params with the k'-th best of the WHOLE
-    catalog as the target. Each shard then keeps ~(its share of) k' j / lambda rows per query
-    instead of ~k' j / lambda of its own, and one filter launch covers it. Returns a future of
-    (theta [B_pad], expected hits per query on this shard) or None (every rank alike)."""
-    wait = _gather_start(coll, local_sample(catalog, qb, tiles, timer))   # [R, B, 4 tiles]
+def sample_send_width(kp_glob: int, tiles: int, world: int, n_global: int) -> int:
+    """J: how many of its 4 * tiles sample maxima per query a shard sends. theta is the j-th
+    largest of all shards' maxima with j <= J (J from the catalog-wide k', the same on every
+    rank), and the j-th largest of the union of each shard's J largest is that same value.
+    0 = no shared threshold (the sample would decide nothing). driver.hip shard_layout."""
+    m_total = 256 * tiles * world
+    J = spec_rank(kp_glob * m_total / max(n_global, 1))
+    if J > world * 4 * tiles // 2:
+        return 0
+    return min(J, 4 * tiles)
+
+
+def _shared_theta(coll, catalog: Catalog, qb, kprime: int, tiles: int, timer=None,
+                  kp_glob: Optional[int] = None):
+    """Catalog-wide screening threshold: every shard's sample maxima (ebt_cosine_sample), its J
+    largest per query (sample_send_width: ebt_floor_pack), ONE all-gather ([R, B, J + 1] f32),
+    theta = the j-th largest of all of them (ebt_pool_kth), j from the Poisson bound of
+    spec_params with the k'-th best of the WHOLE catalog as the target. Each shard then keeps
+    ~(its share of) k' j / lambda rows per query instead of ~k' j / lambda of its own, and one
+    filter launch covers it. Returns a future of (theta [B_pad], expected hits per query on this
+    shard) or None (every rank alike)."""
+    J = sample_send_width(kp_glob or kprime, tiles, coll.world, catalog.n_global)
+    pooled = local_sample(catalog, qb, tiles, timer)                       # [B, 4 tiles]
+    with region(timer, "small", catalog.device):
+        send = floor_send(pooled, None, J) if J else pooled
+    wait = _gather_start(coll, send)                                       # [R, B, J + 1]
 
     def theta():
         with region(timer, "collective_wait", catalog.device):
@@ -304,11 +322,12 @@ def theta_from_samples(g: torch.Tensor, qb, kprime: int, tiles: int, n_global: i
     [R, B, 4 tiles] maxima, or None when the sample is too small to say anything."""
     R, B, G = g.shape
     m_total = 256 * tiles * R
+    RG = R * 4 * tiles
     j = spec_rank(kprime * m_total / max(n_global, 1))
-    if j > R * G // 2:
+    if j > RG // 2 or j > G:
         return None
     theta = pool_kth(g.permute(1, 0, 2).reshape(B, R * G), B, qb.B_pad, j)
-    hits = (j + j * j / (2.0 * R * G)) * n_local / m_total
+    hits = (j + j * j / (2.0 * RG)) * n_local / m_total
     return theta, hits
 
 
@@ -364,7 +383,7 @@ def score_topk_sharded_local_stages(catalog: Catalog, k: int,
     if tiles:
         timer = kw.get("timer")
         kw.setdefault("theta_hook", lambda qb, kp: _shared_theta(coll, catalog, qb, kp, tiles,
-                                                                 timer))
+                                                                 timer, kp_glob))
     g = score_topk_stages(catalog, k, queries=queries, liked=liked_arg, exclude=exclude,
                           liked_counts=counts_t, liked_sum_hook=hook, **kw)
     next(g)
