@@ -1528,8 +1528,10 @@ extern "C" int64_t ebt_shard_list_width(int32_t k, int32_t world) {
 extern "C" int64_t ebt_shard_pack_cap(int64_t B, int32_t k, int32_t world, int64_t n_global) {
   using namespace ebt;
   // the packed merge holds R k entries in LDS; rows travel as int32
+  // (the u32 starts count up to B k entries per rank)
   if (B < 1 || k < 1 || world < 2 || world > MERGE_CORANK_RMAX ||
-      (int64_t)world * k > MERGE_CORANK_CAP || n_global >= (1LL << 31))
+      (int64_t)world * k > MERGE_CORANK_CAP || n_global >= (1LL << 31) ||
+      B * (int64_t)k >= (1LL << 31))
     return 0;
   const int64_t cap = B * shard_list_width(k, world);
   return cap < (1LL << 31) ? cap : 0;
