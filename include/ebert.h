@@ -177,6 +177,18 @@ int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dt
                 const double* t_floor, double* out_scores, int64_t* out_rows, int32_t* certified,
                 void* timer, void* stream);
 
+/* Diagnostics of the rescore's arithmetic (tests, A/B tools; not needed by a caller).
+ * ebt_rescore_form(form): which form of the exact dot products ebt_rescore (and every entry
+ * point that rescores) launches from now on, process-wide: 1 = the lane's query values held in
+ * registers (the default where d fits 512 16-byte chunks), 0 = the query staged in LDS; -1
+ * leaves it. Returns the form in effect before the call. Both forms give bitwise equal scores.
+ * ebt_wave_sum_check: for each of n_waves waves of 64 doubles in[64 w + l], out_a[64 w + l] =
+ * the library's wave sum (cross-lane VALU moves), out_b[...] = the same xor butterfly through
+ * shuffles; the two are expected bitwise equal in every lane. */
+int ebt_rescore_form(int form);
+int ebt_wave_sum_check(const double* in, int64_t n_waves, double* out_a, double* out_b,
+                       void* stream);
+
 /* The fused screen's merge step: query b's candidate list (fv/fi[b*kprime + j], a PARTITIONED
  * list: see below; a sorted list, as ebt_select_topk leaves it, is one) and the hits
  * ebt_screen_filter left in `n_groups` groups of cand/counts (same slots/ld as that call) -> the

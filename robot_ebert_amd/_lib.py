@@ -149,6 +149,8 @@ _SIGNATURES = {
                         _INT),
     "ebt_rescore": ([_VP, _I64, _I32, _VP, _INT, _I64, _VP, _I64, _VP, _VP, _I32, _I32, _I64, _VP,
                      _VP, _VP, _VP, _VP, _VP, _VP], _INT),
+    "ebt_rescore_form": ([_INT], _INT),
+    "ebt_wave_sum_check": ([_VP, _I64, _VP, _VP, _VP], _INT),
     "ebt_sort_exclusions_bytes": ([_I64, _I64], _SZ),
     "ebt_sort_exclusions": ([_VP, _VP, _VP, _I64, _I64, _VP, _SZ, _VP], _INT),
     "ebt_merge_topk": ([_VP, _VP, _I32, _I64, _I32, _VP, _VP, _VP], _INT),

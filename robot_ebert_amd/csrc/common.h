@@ -85,10 +85,99 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // ---- wave reductions -----------------------------------------------------------------------
-__device__ __forceinline__ double wave_sum_f64(double v) {
+// The xor butterfly v += v(lane ^ o), o = 32, 16, 8, 4, 2, 1, through ds_bpermute (LDS pipe,
+// two per level for a double, each waited for). Kept as the reference form of the tree.
+__device__ __forceinline__ double wave_sum_f64_shfl(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
   return v;
+}
+
+__device__ __forceinline__ double f64_from_halves(uint32_t lo, uint32_t hi) {
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const uint32_t hi =
+      (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return f64_from_halves(lo, hi);
+}
+// v(lane ^ 32) / v(lane ^ 16) by the gfx950 half-exchanges of a register with itself
+__device__ __forceinline__ double xor32_f64(double v, int lane) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const auto a = __builtin_amdgcn_permlane32_swap((uint32_t)u, (uint32_t)u, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+  return lane < 32 ? f64_from_halves(a[1], b[1]) : f64_from_halves(a[0], b[0]);
+}
+__device__ __forceinline__ double xor16_f64(double v, int lane) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const auto a = __builtin_amdgcn_permlane16_swap((uint32_t)u, (uint32_t)u, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+  return (lane & 16) ? f64_from_halves(a[0], b[0]) : f64_from_halves(a[1], b[1]);
+}
+
+// One butterfly level of two independent values at once: lanes < 32 (lanes in even 16-lane
+// rows) get x + x(lane ^ 32) (^ 16), the others y + y(lane ^ 32) (^ 16) -- each lane the value
+// its own row's butterfly has there, from one half-exchange per dword.
+__device__ __forceinline__ double pair_sum32_f64(double x, double y) {
+  const uint64_t ux = (uint64_t)__double_as_longlong(x), uy = (uint64_t)__double_as_longlong(y);
+  const auto a = __builtin_amdgcn_permlane32_swap((uint32_t)ux, (uint32_t)uy, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap((uint32_t)(ux >> 32), (uint32_t)(uy >> 32), false, false);
+  return f64_from_halves(a[0], b[0]) + f64_from_halves(a[1], b[1]);
+}
+__device__ __forceinline__ double pair_sum16_f64(double x, double y) {
+  const uint64_t ux = (uint64_t)__double_as_longlong(x), uy = (uint64_t)__double_as_longlong(y);
+  const auto a = __builtin_amdgcn_permlane16_swap((uint32_t)ux, (uint32_t)uy, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap((uint32_t)(ux >> 32), (uint32_t)(uy >> 32), false, false);
+  return f64_from_halves(a[0], b[0]) + f64_from_halves(a[1], b[1]);
+}
+
+// The SAME butterfly (bitwise equal to wave_sum_f64_shfl: every level adds the value of lane ^ o)
+// in VALU cross-lane moves, no LDS traffic: levels 32 and 16 by permlane32/16_swap, 8 by DPP
+// row_ror:8 (= xor 8 inside a 16-lane row), 4 by row_ror:4 (after levels 32..8 the value
+// depends on lane mod 8 only, and lane +- 4 mod 8 = lane ^ 4 mod 8), 2 and 1 by quad_perm.
+// Every lane of the wave must be active (as for the shuffles it replaces).
+__device__ __forceinline__ double wave_sum_f64(double v) {
+  const int lane = (int)(threadIdx.x & (kWave - 1));
+  v += xor32_f64(v, lane);
+  v += xor16_f64(v, lane);
+  v += dpp_f64<0x128>(v);  // row_ror:8
+  v += dpp_f64<0x124>(v);  // row_ror:4
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  return v;
+}
+
+// The butterflies of NR (1, 2 or 4) values at once, each bitwise equal to its own
+// wave_sum_f64: the first log2(NR) levels pair values up (pair_sum32 / pair_sum16), so that
+// from then on each lane carries one value through the remaining levels. Returns, in every lane,
+// the total of value (lane >> 5) (NR = 2) or (lane >> 4) (NR = 4): wave_rows_owner<NR>(lane).
+template <int NR>
+__device__ __forceinline__ double wave_sum_f64_rows(const double (&s)[NR]) {
+  static_assert(NR == 1 || NR == 2 || NR == 4, "NR");
+  const int lane = (int)(threadIdx.x & (kWave - 1));
+  double v;
+  if constexpr (NR == 1) {
+    return wave_sum_f64(s[0]);
+  } else if constexpr (NR == 2) {
+    v = pair_sum32_f64(s[0], s[1]);  // lanes < 32: value 0, lanes >= 32: value 1
+    v += xor16_f64(v, lane);
+  } else {
+    const double t0 = pair_sum32_f64(s[0], s[2]);  // lanes < 32: 0, >= 32: 2
+    const double t1 = pair_sum32_f64(s[1], s[3]);  // lanes < 32: 1, >= 32: 3
+    v = pair_sum16_f64(t0, t1);                    // 16-lane rows: 0, 1, 2, 3
+  }
+  v += dpp_f64<0x128>(v);
+  v += dpp_f64<0x124>(v);
+  v += dpp_f64<0x4E>(v);
+  v += dpp_f64<0xB1>(v);
+  return v;
+}
+template <int NR>
+__device__ __forceinline__ int wave_rows_owner(int lane) {
+  return NR == 1 ? 0 : (NR == 2 ? lane >> 5 : lane >> 4);
 }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }

@@ -9,6 +9,9 @@
 // chosen by (score desc, row asc). The candidate set is PROVABLY a superset of the true top-k
 // when approx[k'-1] < approx[k-1] - 2 eps ("certified-margin rescore");
 // otherwise certified[b] = 0 and the host retries that query with a larger k'.
+#include <atomic>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace ebt {
@@ -94,8 +97,41 @@ __device__ __forceinline__ double chunk_dot(const double* qs, int j0, uint4 raw)
   }
   return s;
 }
+// The same sum with the lane's query values in registers (q[e] = qs[j0 + e]): the same
+// expression, so the same contracted FMA chain and the same bits.
+template <int DT, int PER>
+__device__ __forceinline__ double chunk_dot_reg(const double (&q)[PER], uint4 raw) {
+  double s = 0.0;
+  if constexpr (DT == EBT_F32) {
+    const float* f = (const float*)&raw;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += q[e] * (double)f[e];
+  } else if constexpr (DT == EBT_F64) {
+    const double* f = (const double*)&raw;
+    s += q[0] * f[0] + q[1] * f[1];
+  } else {
+    const uint16_t* h = (const uint16_t*)&raw;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      s += q[e] * (DT == EBT_BF16 ? bf16_bits_to_f64(h[e]) : f16_bits_to_f64(h[e]));
+  }
+  return s;
+}
 
-template <int DT, bool VEC>
+// Rows per wave round trip of the register-query form, by chunks per lane (NU): about eight
+// 16-byte loads per lane in flight (C2 / C4: NU = 2 -> 4 rows; C5: 3 -> 2; C3: 6 -> 2)
+#ifndef EBT_RESCORE_NR_WIDE
+#define EBT_RESCORE_NR_WIDE 2  // rows per trip at 3..6 chunks per lane (build knob for A/B)
+#endif
+template <int NU>
+constexpr int rescore_rows_per_trip() { return NU <= 2 ? 4 : (NU <= 6 ? EBT_RESCORE_NR_WIDE : 1); }
+
+// NU = 0: the query staged in LDS (any d), two rows per wave round trip. NU > 0 (VEC, d / PER
+// <= 64 NU 16-byte chunks): each lane keeps its chunks' query values (chunks lane + 64 u) in
+// registers for every row -- no LDS reads in the dot products, no query staging -- and gathers
+// rescore_rows_per_trip<NU>() rows per round trip from per-pass row lists. Per row the same
+// chunk order, the same per-chunk sums and the same wave butterfly: bitwise the same scores.
+template <int DT, bool VEC, int NU = 0>
 __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     const double* __restrict__ q64, int d, const void* __restrict__ cat, int64_t ld,
     const double* __restrict__ gnorm, int64_t row_offset, const float* __restrict__ cand_vals,
@@ -104,11 +140,12 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     int64_t* __restrict__ out_r, int32_t* __restrict__ certified, const int* __restrict__ ovf_cnt,
     int ovf_cap) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* qs = (double*)smem;                 // d
-  double* sc = qs + ((d + 1) & ~1);           // kpp: approx, then exact
+  double* qs = (double*)smem;                           // d (NU = 0 only)
+  double* sc = qs + (NU > 0 ? 0 : ((d + 1) & ~1));      // kpp: approx, then exact
   int64_t* rw = (int64_t*)(sc + kpp);         // kpp
   int* pl = (int*)(rw + kpp);                 // kpp: list position of each kept row
-  __shared__ int nvalid, corrupt, nkeep, ntop;
+  int* ix = pl + kpp;                         // kpp (NU > 0): the rows of the current pass
+  __shared__ int nvalid, corrupt, nkeep, ntop, nsel;
   __shared__ unsigned long long smin_key;
   constexpr int NW = RTHREADS / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -118,9 +155,29 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     corrupt = 0;
     nkeep = 0;
     ntop = 0;
+    nsel = 0;
     smin_key = ~0ull;
   }
-  stage_f64(qs, q64 + b * d, d);
+  constexpr int ES = (DT == EBT_F64) ? 8 : (DT == EBT_F32 ? 4 : 2);
+  constexpr int PER = 16 / ES;
+  // NU > 0: the lane's query values of chunks lane + 64 u (0 past the row)
+  double qv[NU > 0 ? NU : 1][PER];
+  if constexpr (NU > 0) {
+    const int nch = d / PER;
+    const double* qrow = q64 + b * d;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int ch = lane + 64 * u;
+      const int cc = ch < nch ? ch : 0;  // clamped, so that every load is issued up front
+#pragma unroll
+      for (int e = 0; e < PER; ++e) {
+        const double x = qrow[cc * PER + e];
+        qv[u][e] = ch < nch ? x : 0.0;
+      }
+    }
+  } else {
+    stage_f64(qs, q64 + b * d, d);
+  }
   const int64_t* cr = cand_rows + b * kprime;
   // Candidates whose approx score is below approx[k-1] - 2 eps cannot be in the top k (the k
   // best candidates all have exact >= approx[k-1] - eps > their exact), so their rows are not
@@ -153,11 +210,20 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
       if (kb) base = atomicAdd(&nkeep, __popcll(kb));
     }
     base = __shfl(base, 0, 64);
+    int at = -1;
     if (keep) {
-      const int at = base + __popcll(kb & ((1ull << lane) - 1));
+      at = base + __popcll(kb & ((1ull << lane) - 1));
       rw[at] = row;
       sc[at] = (double)v;
       pl[at] = c;
+    }
+    if constexpr (NU > 0) {  // pass A's rows: the kept ones among the list's first k
+      const bool top = keep && c < k;
+      const uint64_t tb = __ballot(top);
+      int tbase = 0;
+      if (lane == 0 && tb) tbase = atomicAdd(&nsel, __popcll(tb));
+      tbase = __shfl(tbase, 0, 64);
+      if (top) ix[tbase + __popcll(tb & ((1ull << lane) - 1))] = at;
     }
   }
   __syncthreads();
@@ -228,7 +294,51 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     }
     }
   };
-  exact_pass(true, 0.0);
+  // NU > 0: the wave's rows ix[i0 .. i0 + NR) of a pass list, all of their loads issued before
+  // the arithmetic (the last row repeated past the list's end, not stored)
+  auto exact_rows = [&](int n) {
+    if constexpr (NU > 0) {
+      constexpr int NR = rescore_rows_per_trip<NU>();
+      const int nch = d / PER;
+      for (int i0 = wave * NR; i0 < n; i0 += NW * NR) {
+        int64_t r[NR];
+        double g[NR];
+        uint4 x[NR][NU];
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) r[rr] = rw[ix[i0 + rr < n ? i0 + rr : n - 1]];
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) {
+          const char* p = (const char*)cat + r[rr] * ld * ES;
+#pragma unroll
+          for (int u = 0; u < NU; ++u) {
+            const int ch = lane + 64 * u;
+            x[rr][u] = *(const uint4*)(p + (int64_t)(ch < nch ? ch : 0) * 16);
+          }
+          g[rr] = gnorm[r[rr]];
+        }
+        double s[NR];
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) {
+          s[rr] = 0.0;
+#pragma unroll
+          for (int u = 0; u < NU; ++u)
+            if (lane + 64 * u < nch) s[rr] += chunk_dot_reg<DT, PER>(qv[u], x[rr][u]);
+        }
+        // the NR butterflies together; the first lane of each value's lane group stores it
+        const double tot = wave_sum_f64_rows<NR>(s);
+        const int own = wave_rows_owner<NR>(lane);
+        double gown = g[0];
+#pragma unroll
+        for (int rr = 1; rr < NR; ++rr) gown = own == rr ? g[rr] : gown;
+        if ((lane & (64 / NR - 1)) == 0 && i0 + own < n) {
+          const double v = tot / gown;
+          sc[ix[i0 + own]] = (v == v) ? v : -__builtin_inf();
+        }
+      }
+    }
+  };
+  if constexpr (NU > 0) exact_rows(nsel);
+  else exact_pass(true, 0.0);
   __syncthreads();
   // s_min over the k top entries (all k present and valid), as an order-preserving key
   for (int j = tid; j < nk; j += RTHREADS) {
@@ -249,7 +359,26 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
         (long long)((key >> 63) ? (key & 0x7fffffffffffffffull) : ~key));
     if (smin - (double)eps[b] > cut2) cut2 = smin - (double)eps[b];
   }
-  exact_pass(false, cut2);
+  if constexpr (NU > 0) {
+    // pass B's rows: past the list's first k and not below cut2; the others sorted last
+    if (tid == 0) nsel = 0;
+    __syncthreads();
+    for (int j0 = 0; j0 < nk; j0 += RTHREADS) {
+      const int j = j0 + tid;
+      const bool rest = j < nk && pl[j] >= k;
+      const bool sel = rest && !(sc[j] < cut2);
+      if (rest && !sel) sc[j] = -__builtin_inf();
+      const uint64_t sb = __ballot(sel);
+      int sbase = 0;
+      if (lane == 0 && sb) sbase = atomicAdd(&nsel, __popcll(sb));
+      sbase = __shfl(sbase, 0, 64);
+      if (sel) ix[sbase + __popcll(sb & ((1ull << lane) - 1))] = j;
+    }
+    __syncthreads();
+    exact_rows(nsel);
+  } else {
+    exact_pass(false, cut2);
+  }
   // 3. order the kept rows (score desc, row asc); positions past them read NaN / -1
   if (nk <= RESCORE_RANK_MAX) {
     // few rows (C2 / C3: ~120-150): each row's position is the number of rows before it,
@@ -493,6 +622,43 @@ static size_t rescore_lds_stage_total(int d, int es, int kprime, int R) {
          8 * (size_t)R;
 }
 
+// ebt_rescore_form: 1 = register-query form (default; EBT_RESCORE_REG=0 in the environment
+// starts the process with the LDS-query form)
+static std::atomic<int>& rescore_form_flag() {
+  static std::atomic<int> f([] {
+    const char* v = getenv("EBT_RESCORE_REG");
+    return v ? (atoi(v) != 0 ? 1 : 0) : 1;
+  }());
+  return f;
+}
+static bool rescore_form_reg() { return rescore_form_flag().load(std::memory_order_relaxed) != 0; }
+
+__global__ void wave_sum_check_kernel(const double* __restrict__ in, int64_t n_waves,
+                                      double* __restrict__ a, double* __restrict__ b) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= n_waves) return;  // whole waves
+  const double v = in[w * 64 + (threadIdx.x & 63)];
+  a[w * 64 + (threadIdx.x & 63)] = wave_sum_f64(v);
+  b[w * 64 + (threadIdx.x & 63)] = wave_sum_f64_shfl(v);
+}
+
+extern "C" int ebt_rescore_form(int form) {
+  if (form < 0) return rescore_form_flag().load();
+  return rescore_form_flag().exchange(form != 0 ? 1 : 0);
+}
+
+extern "C" int ebt_wave_sum_check(const double* in, int64_t n_waves, double* out_a, double* out_b,
+                                  void* stream) {
+  if (!in || !out_a || !out_b || n_waves < 0) {
+    set_error("ebt_wave_sum_check: bad arguments");
+    return EBT_EINVAL;
+  }
+  if (n_waves == 0) return EBT_OK;
+  hipLaunchKernelGGL(wave_sum_check_kernel, dim3((unsigned)ceil_div(n_waves, 4)), dim3(256), 0,
+                     (hipStream_t)stream, in, n_waves, out_a, out_b);
+  return launch_check("wave_sum_check_kernel");
+}
+
 size_t rescore_lds_bytes(int d, int kprime) {
   const int kpp = next_pow2_h(kprime);
   return 8 * (size_t)((d + 1) & ~1) + 20 * (size_t)kpp;
@@ -548,6 +714,37 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
     }
   }
 #endif
+  // the register-query form (chunks per lane NU, rounded up to an instantiated count) unless
+  // the form is 0 (the LDS-query form, kept for A/B and for d beyond 512 chunks)
+  const int nch = d * es / 16;
+  const int nu_need = (nch + 63) / 64;
+  const int nu = nu_need <= 4 ? nu_need : (nu_need <= 6 ? 6 : (nu_need <= 8 ? 8 : 0));
+  if (vec && rescore_form_reg() && nu > 0) {
+    const size_t lds_r = 24 * (size_t)kpp;
+#define EBT_RSR(DT, NU)                                                                         \
+  set_max_lds((const void*)rescore_kernel<DT, true, NU>, (int)lds_r);                          \
+  hipLaunchKernelGGL((rescore_kernel<DT, true, NU>), grid, block, lds_r, st, q64, d, cat, ld,   \
+                     gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,      \
+                     t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap);
+#define EBT_RSR_NU(DT)                                                                          \
+  switch (nu) {                                                                                 \
+    case 1: EBT_RSR(DT, 1) break;                                                               \
+    case 2: EBT_RSR(DT, 2) break;                                                               \
+    case 3: EBT_RSR(DT, 3) break;                                                               \
+    case 4: EBT_RSR(DT, 4) break;                                                               \
+    case 6: EBT_RSR(DT, 6) break;                                                               \
+    default: EBT_RSR(DT, 8) break;                                                              \
+  }
+    switch (dtype) {
+      case EBT_F32: EBT_RSR_NU(EBT_F32) break;
+      case EBT_BF16: EBT_RSR_NU(EBT_BF16) break;
+      case EBT_F16: EBT_RSR_NU(EBT_F16) break;
+      default: EBT_RSR_NU(EBT_F64) break;
+    }
+#undef EBT_RSR_NU
+#undef EBT_RSR
+    return launch_check("rescore_kernel");
+  }
 #define EBT_RS(DT)                                                                              \
   set_max_lds((const void*)rescore_kernel<DT, true>, (int)lds);                                \
   set_max_lds((const void*)rescore_kernel<DT, false>, (int)lds);                               \
