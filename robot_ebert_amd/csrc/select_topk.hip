@@ -820,15 +820,19 @@ constexpr int WMERGE_K = 512;         // largest k'
 constexpr int WMERGE_Q = STHREADS / 64;
 constexpr int WCNT = 4;               // 16-byte count loads per lane: n_groups <= 64 * 64
 
+// E: the leading entries per lane that can be nonzero (the union fills entry j = c / 64 of
+// lane c % 64 in order, so every entry past ceil(used / 64) is 0 and counts nowhere)
+template <int E>
 __device__ __forceinline__ int wave_count_ge(const uint32_t (&kx)[WTOP_E], uint32_t t) {
   int c = 0;
 #pragma unroll
-  for (int j = 0; j < WTOP_E; ++j) c += __popcll(__ballot(kx[j] >= t));
+  for (int j = 0; j < E; ++j) c += __popcll(__ballot(kx[j] >= t));
   return c;
 }
 
 // The cut c (a composite) with exactly `want` entries of x >= c (1 <= want <= valid entries;
 // composites are unique). lo: a key with count(key >= lo) >= want; hi: the largest key.
+template <int E>
 __device__ __forceinline__ uint64_t wave_cut(const uint64_t (&x)[WTOP_E],
                                              const uint32_t (&kx)[WTOP_E], int want, uint32_t lo,
                                              uint32_t hi) {
@@ -836,13 +840,13 @@ __device__ __forceinline__ uint64_t wave_cut(const uint64_t (&x)[WTOP_E],
   if (l > h) l = h;
   while (l < h) {  // largest t with count(key >= t) >= want
     const uint64_t mid = l + ((h - l + 1) >> 1);
-    if (wave_count_ge(kx, (uint32_t)mid) >= want) l = mid;
+    if (wave_count_ge<E>(kx, (uint32_t)mid) >= want) l = mid;
     else h = mid - 1;
   }
   const uint32_t t = (uint32_t)l;
   int gt = 0, eq = 0;
 #pragma unroll
-  for (int j = 0; j < WTOP_E; ++j) {
+  for (int j = 0; j < E; ++j) {
     gt += __popcll(__ballot(kx[j] > t));
     eq += __popcll(__ballot(kx[j] == t));
   }
@@ -854,7 +858,7 @@ __device__ __forceinline__ uint64_t wave_cut(const uint64_t (&x)[WTOP_E],
       const uint64_t mid = l2 + ((h2 - l2 + 1) >> 1);
       int c = 0;
 #pragma unroll
-      for (int j = 0; j < WTOP_E; ++j)
+      for (int j = 0; j < E; ++j)
         c += __popcll(__ballot(kx[j] == t && (uint32_t)x[j] >= (uint32_t)mid));
       if (c >= need) l2 = mid;
       else h2 = mid - 1;
@@ -865,10 +869,11 @@ __device__ __forceinline__ uint64_t wave_cut(const uint64_t (&x)[WTOP_E],
 }
 
 // smallest nonzero composite >= cut over the wave (uniform result)
+template <int E>
 __device__ __forceinline__ uint64_t wave_min_at_least(const uint64_t (&x)[WTOP_E], uint64_t cut) {
   uint64_t m = ~0ull;
 #pragma unroll
-  for (int j = 0; j < WTOP_E; ++j) m = (x[j] != 0ull && x[j] >= cut && x[j] < m) ? x[j] : m;
+  for (int j = 0; j < E; ++j) m = (x[j] != 0ull && x[j] >= cut && x[j] < m) ? x[j] : m;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const uint64_t v = ((uint64_t)(uint32_t)__shfl_xor((int)(m >> 32), o, 64) << 32) |
@@ -881,6 +886,7 @@ __device__ __forceinline__ uint64_t wave_min_at_least(const uint64_t (&x)[WTOP_E
 // The k' largest of the wave's composites x (0 = empty), written partitioned at k (see above)
 // to ov/oi[0..kprime).
 // Returns the value it wrote to position k-1 (uniform): the k-th best, -inf when fewer than k.
+template <int E>
 __device__ float wave_topk_write(const uint64_t (&x)[WTOP_E], int kprime, int k, float* ov,
                                  int64_t* oi, int lane, uint32_t key_lo) {
   float kth = -__builtin_inff();
@@ -888,7 +894,9 @@ __device__ float wave_topk_write(const uint64_t (&x)[WTOP_E], int kprime, int k,
   int nvalid = 0;
   uint32_t kmax = 0u, kmin = 0xffffffffu;  // over the valid entries
 #pragma unroll
-  for (int j = 0; j < WTOP_E; ++j) {
+  for (int j = E; j < WTOP_E; ++j) kx[j] = 0u;
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
     kx[j] = (uint32_t)(x[j] >> 32);
     nvalid += __popcll(__ballot(x[j] != 0ull));
     kmax = max(kmax, kx[j]);
@@ -907,18 +915,18 @@ __device__ float wave_topk_write(const uint64_t (&x)[WTOP_E], int kprime, int k,
   if (want > 0) {
     // the kept set S = {x >= cw_cut} (want entries), its smallest cw; the top kk = min(k, want)
     // A = {x >= ck_cut}, its smallest ck (the kk-th best)
-    const uint64_t cw_cut = wave_cut(x, kx, want, key_lo > 1u ? key_lo : 1u, kmax);
-    const uint64_t cw = wave_min_at_least(x, cw_cut);
+    const uint64_t cw_cut = wave_cut<E>(x, kx, want, key_lo > 1u ? key_lo : 1u, kmax);
+    const uint64_t cw = wave_min_at_least<E>(x, cw_cut);
     const int kk = k < want ? k : want;
     uint64_t ck = cw;
     if (kk < want) {
-      const uint64_t ck_cut = wave_cut(x, kx, kk, (uint32_t)(cw_cut >> 32), kmax);
-      ck = wave_min_at_least(x, ck_cut);
+      const uint64_t ck_cut = wave_cut<E>(x, kx, kk, (uint32_t)(cw_cut >> 32), kmax);
+      ck = wave_min_at_least<E>(x, ck_cut);
     }
     if (kk == k) kth = key2f((uint32_t)(ck >> 32));
     int na = 0, nb = kk;
 #pragma unroll
-    for (int j = 0; j < WTOP_E; ++j) {
+    for (int j = 0; j < E; ++j) {
       const uint64_t v = x[j];
       const bool inA = v > ck;                                  // the kk-1 best
       const bool inB = v != 0ull && v >= cw && v < ck && v != cw;  // between
@@ -970,7 +978,9 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
   uint64_t x[WTOP_E];
   bool over = false;
   uint32_t key_lo = 1u;  // the new k'-th key is >= the list's k'-th key
+  int used_n = WTOP_N;    // union entries (x[j] of lane l is entry l + 64 j; 0 past them)
   if constexpr (DENSE) {
+    used_n = n_dense < WTOP_N ? n_dense : WTOP_N;
     const float* row = dense + b * ld_dense;
 #pragma unroll
     for (int j = 0; j < WTOP_E; ++j) {
@@ -1085,6 +1095,7 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
       }
     }
     const int used = kprime + m < WTOP_N ? kprime + m : WTOP_N;
+    used_n = used;
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -1095,7 +1106,11 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
-  const float kth = wave_topk_write(x, kprime, k, fv + b * kprime, fi + b * kprime, lane, key_lo);
+  // entries in use per lane (uniform): the selection's counting loops stop there
+  const int ne = (int)((used_n + 63) / 64);
+  const float kth =
+      ne <= 8 ? wave_topk_write<8>(x, kprime, k, fv + b * kprime, fi + b * kprime, lane, key_lo)
+              : wave_topk_write<WTOP_E>(x, kprime, k, fv + b * kprime, fi + b * kprime, lane, key_lo);
   const bool any_over = __ballot(over) != 0ull;
   if (lane == 0) {
     // vspec: the speculative screen's VERIFY on the final list (spec_threshold_kernel,

@@ -32,6 +32,11 @@ def main():
     ap.add_argument("--b", type=int, default=4096)
     ap.add_argument("--d", type=int, default=1536)
     ap.add_argument("--secs", type=float, default=2.5)
+    ap.add_argument("--z", type=float, default=3.0,
+                    help="threshold of the hit mode in sigmas of the cosine (3: C3's ~0.13 %% "
+                         "hits; 2.73: C2's ~313 hits per 100K rows)")
+    ap.add_argument("--img", default="f16", choices=["f16", "bf16"],
+                    help="operand type (bf16: the C2 / C4 native catalogs)")
     ap.add_argument("--lib", default=os.path.join(ROOT, "_abl", "libebert_stamp.so"))
     ap.add_argument("--precision", action="store_true",
                     help="instead: no-hit launches on operands of reduced mantissa width "
@@ -48,9 +53,12 @@ def main():
     B, N, d = a.b, a.n, a.d
     g = torch.Generator(device=dev).manual_seed(0)
     q = torch.randn((B, d), generator=g, device=dev)
-    q = (q / q.norm(dim=1, keepdim=True)).half()
+    q = q / q.norm(dim=1, keepdim=True)
+    q = q.half() if a.img == "f16" else q.to(torch.bfloat16)
     c = torch.randn((N, d), generator=g, device=dev)
-    c = (c / c.norm(dim=1, keepdim=True)).half()
+    c = c / c.norm(dim=1, keepdim=True)
+    c = c.half() if a.img == "f16" else c.to(torch.bfloat16)
+    idt = 2 if a.img == "f16" else 1
     qs = torch.ones(B, device=dev)
     G, slots = 256, 32
     groups = (N + G - 1) // G
@@ -61,9 +69,9 @@ def main():
     st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     zq, zc = torch.zeros_like(q), torch.zeros_like(c)
-    modes = [("random_c3_threshold", q, c, 3.0 / d ** 0.5, 2),
-             ("random_no_hits", q, c, float("inf"), 2),
-             ("zero_no_hits", zq, zc, float("inf"), 2)]
+    modes = [(f"random_z{a.z:g}_threshold", q, c, a.z / d ** 0.5, idt),
+             ("random_no_hits", q, c, float("inf"), idt),
+             ("zero_no_hits", zq, zc, float("inf"), idt)]
     if a.precision:
         def trunc(x, bits, bf16=False):
             """the same values with only `bits` explicit mantissa bits (truncated)"""
