@@ -16,3 +16,4 @@ EBERT_LIB=_abl/libebert_head.so bash tools/gpu.sh bench r4t_c3_head C3 --steps 2
 EBERT_LIB=_abl/libebert_nr1.so bash tools/gpu.sh bench r4t_c3_nr1 C3 --steps 20 --no-cpu-baseline
 bash tools/gpu.sh bench r4t_c2_streams2 C2 --steps 50 --no-cpu-baseline --streams 2
 bash tools/gpu.sh py r4t_stamp tools/clock_stamp.py --n 100000 --b 1024 --d 768 --img bf16 --z 2.73 --secs 1.5
+bash tools/gpu.sh py r4t_stamp_cs tools/clock_stamp.py --n 100000 --b 1024 --d 768 --img bf16 --z 2.73 --secs 1.5 --cscale

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--z", type=float, default=3.0,
                     help="threshold of the hit mode in sigmas of the cosine (3: C3's ~0.13 %% "
                          "hits; 2.73: C2's ~313 hits per 100K rows)")
+    ap.add_argument("--cscale", action="store_true",
+                    help="pass per-row scales (the native-catalog epilogue: C2 / C4), all 1")
     ap.add_argument("--img", default="f16", choices=["f16", "bf16"],
                     help="operand type (bf16: the C2 / C4 native catalogs)")
     ap.add_argument("--lib", default=os.path.join(ROOT, "_abl", "libebert_stamp.so"))
@@ -60,6 +62,7 @@ def main():
     c = c.half() if a.img == "f16" else c.to(torch.bfloat16)
     idt = 2 if a.img == "f16" else 1
     qs = torch.ones(B, device=dev)
+    cs = torch.ones(N, device=dev) if a.cscale else None
     G, slots = 256, 32
     groups = (N + G - 1) // G
     cand = torch.empty((B, groups * slots), dtype=torch.int64, device=dev)
@@ -96,7 +99,8 @@ def main():
         thr = torch.full((B,), t, device=dev)
 
         def launch():
-            rc = f(P(qq), B, P(cc), N, d, d, img_dt, P(qs), None, P(thr), P(cand), groups * slots,
+            rc = f(P(qq), B, P(cc), N, d, d, img_dt, P(qs), P(cs) if cs is not None else None,
+                   P(thr), P(cand), groups * slots,
                    slots, P(counts), groups, P(ovf), 0, st)
             if rc:
                 raise RuntimeError(lib.ebt_last_error().decode())
@@ -128,7 +132,8 @@ def main():
         tf = fl / ms / 1e9
         hits = float(counts.float().sum(1).mean()) if t != float("inf") else 0.0
         print(json.dumps({
-            "mode": name, "shape": [B, N, d], "warm_launches": n_warm,
+            "mode": name, "shape": [B, N, d], "img": a.img, "row_scales": bool(a.cscale),
+            "warm_launches": n_warm,
             "launch_ms": round(ms, 4), "tflops": round(tf, 1), "frac_of_2500": round(tf / 2500, 4),
             "clock_ghz_median": round(med, 3), "clock_ghz_p10": round(clk[len(clk) // 10], 3),
             "clock_ghz_p90": round(clk[9 * len(clk) // 10], 3), "workgroups": len(clk),
