@@ -840,24 +840,8 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
         colm |= (mx * q4[c] >= t4[c] || !(q4[c] >= 0.f) ? 1u : 0u) << c;
       }
     } else {
-      // With row scales s_r > 0: max_r(a_r s_r) <= max_r(a_r) * (that max >= 0 ? max s : min s)
-      // over the lane's 32 rows, so the test runs on the column's plain max (as SIMPLE) times
-      // one of two per-lane scale extremes -- 2 multiplies per column instead of 32. The two
-      // roundings are the ones the per-row form had (fl(a s), then * qs): the same 2^-20 slack
-      // keeps the flags a superset, and step 3 below tests every value exactly, so the hits
-      // are the same. Rows past n_rows may hold any scale: it can only add flags (NaNs drop out
-      // of fmaxf / fminf), and step 3 skips those rows.
       f32x4_t cs[2][4];
       lds_rowscales8(lcs + wa * 64 + 4 * g_, cs);
-      float smax = cs[0][0][0], smin = cs[0][0][0];
-#pragma unroll
-      for (int ah = 0; ah < 2; ++ah)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          smax = fmaxf(smax, max4(cs[ah][i][0], cs[ah][i][1], cs[ah][i][2], cs[ah][i][3]));
-          smin = fminf(smin, fminf(fminf(cs[ah][i][0], cs[ah][i][1]),
-                                   fminf(cs[ah][i][2], cs[ah][i][3])));
-        }
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         float mx = -__builtin_inff();
@@ -866,11 +850,11 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const f32x4_t& a = acc_of(ah, c >> 1)[i][c & 1];
-            mx = fmaxf(mx, max4(a[0], a[1], a[2], a[3]));
+            const f32x4_t& s = cs[ah][i];
+            mx = fmaxf(mx, max4(a[0] * s[0], a[1] * s[1], a[2] * s[2], a[3] * s[3]));
           }
-        const float ub = mx * (mx >= 0.f ? smax : smin);
         const float th_lo = t4[c] - fabsf(t4[c]) * 0x1p-20f - 0x1p-120f;
-        colm |= (ub * q4[c] >= th_lo || !(q4[c] >= 0.f) ? 1u : 0u) << c;
+        colm |= (mx * q4[c] >= th_lo || !(q4[c] >= 0.f) ? 1u : 0u) << c;
       }
     }
     if (__builtin_expect(__ballot(colm != 0u) == 0ull, 1)) return;
