@@ -373,7 +373,13 @@ constexpr int QP_PARAM = 1024 + 3 * QP_TILE * 4;
 constexpr int QP_STG_COLS = 16;
 constexpr int QP_STG_WAVE = QP_STG_COLS * (128 + 16);
 constexpr int QP_STG = 8 * QP_STG_WAVE;
-constexpr int QP_LDS_TOTAL = QP_LDS + QP_PARAM + QP_STG;
+#ifdef EBT_EPI_STAMP
+// diagnostic build: per wave 8 u64 (phase cycle sums, tiles, last stamp) after the staging area
+constexpr int QP_EPI_STAMP = 8 * 8 * 8;
+#else
+constexpr int QP_EPI_STAMP = 0;
+#endif
+constexpr int QP_LDS_TOTAL = QP_LDS + QP_PARAM + QP_STG + QP_EPI_STAMP;
 static_assert(QP_LDS_TOTAL <= 160 * 1024, "LDS budget");
 
 // Epilogue LDS reads in inline asm (each completes before it returns). The compiler treats any
@@ -491,6 +497,33 @@ __device__ __forceinline__ QpArgsK qp_args() {
   return p;
 }
 
+#ifdef EBT_EPI_STAMP
+// Diagnostic build only: where a filter launch's cycles go, per wave. Lane 0 of every wave
+// stamps the shader clock (s_memtime) at phase boundaries and adds the cycles since its previous
+// stamp to that phase's sum in LDS: [0] K-loop (from the end of the previous tile's epilogue),
+// [1] column test, [2] hit staging, [3] hit processing, [4] the rest of the epilogue up to the
+// next tile (the workgroup barrier included: waiting for the slowest wave), [5] tiles, [6] tiles
+// with hits in this wave; [7] the last stamp. Written to g_epi[(block * 8 + wave) * 8 ..] at exit.
+__device__ unsigned long long* g_epi;
+__device__ __forceinline__ void epi_stamp(char* smem, int wave, int phase) {
+  if ((threadIdx.x & 63) == 0) {
+    unsigned long long* e = (unsigned long long*)(smem + QP_LDS + QP_PARAM + QP_STG) + wave * 8;
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    if (phase >= 0) e[phase] += t - e[7];
+    e[7] = t;
+  }
+}
+__device__ __forceinline__ void epi_count(char* smem, int wave, int slot) {
+  if ((threadIdx.x & 63) == 0)
+    ((unsigned long long*)(smem + QP_LDS + QP_PARAM + QP_STG) + wave * 8)[slot] += 1;
+}
+#define EPI_STAMP(ph) epi_stamp(smem, wave, (ph))
+#define EPI_COUNT(sl) epi_count(smem, wave, (sl))
+#else
+#define EPI_STAMP(ph)
+#define EPI_COUNT(sl)
+#endif
+
 #ifdef EBT_CLOCK_STAMP
 // Diagnostic build only (MI355X_MICROARCH.md "DVFS give-back" item 6): lane 0 of each workgroup
 // of a filter-mode launch records the shader-clock and the 100 MHz real-time counters after the
@@ -558,6 +591,11 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
     lcnt[tid] = 0u;
     if (!qp_args()->cscale) lcs[tid] = 1.f;
   }
+#ifdef EBT_EPI_STAMP
+  if (tid < 64) ((unsigned long long*)(smem + QP_LDS + QP_PARAM + QP_STG))[tid] = 0ull;
+  __syncthreads();
+  EPI_STAMP(-1);
+#endif
   // the tile's epilogue parameters by LDS-DMA (one 1 KiB piece per array, waves 0..2): they
   // travel in the operand stream and are retired by its counted waits
   auto issue_params = [&](const QpTile& T) {
@@ -788,6 +826,8 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
       QP2_KTILE(1, fby, fbx, nc, nq, 0, nc, nq, 1, false);
     }
     __builtin_amdgcn_sched_barrier(0);
+    EPI_STAMP(0);
+    EPI_COUNT(5);
     // the epilogue's lane geometry is recomputed from an opaque copy of the lane id, so that
     // none of it is hoisted into registers held through the K-loop
     int lane_e = tid;
@@ -857,7 +897,12 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
         colm |= (mx * q4[c] >= th_lo || !(q4[c] >= 0.f) ? 1u : 0u) << c;
       }
     }
+#ifdef EBT_ABL_HIT_NONE  // ablation builds only: the column test without the hit path
+    if (__ballot(colm != 0u) != 0ull || true) return;
+#endif
+    EPI_STAMP(1);
     if (__builtin_expect(__ballot(colm != 0u) == 0ull, 1)) return;
+    EPI_COUNT(6);
     // 2. compact indices: columns in order, lanes in order within a column (n: uniform)
     int idx[4];
     int n = 0;
@@ -885,15 +930,24 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
           const int jj = c & 1;
           const f32x4_t meta = {__builtin_bit_cast(float, (uint32_t)(ql4[c] | (g_ << 8))), q4[c],
                                 t4[c], 0.f};
+#ifndef EBT_ABL_STAGE_META_ONLY
           lds_put_col(wst + s * 128, ac0[0][jj], ac0[1][jj], ac0[2][jj], ac0[3][jj], ac1[0][jj],
                       ac1[1][jj], ac1[2][jj], ac1[3][jj], wmeta + s * 16, meta);
+#else  // ablation builds only: the staging's record write alone (values left stale)
+          asm volatile("ds_write_b128 %0, %1" : : "v"(wmeta + s * 16), "v"(meta) : "memory");
+#endif
         }
       }
+      EPI_STAMP(2);
       // 3. lane: staged column s, values u * 8 .. u * 8 + 7 = half ah = u >> 1, accumulators
       // i0, i0 + 1 (i0 = (u & 1) * 2), rows il0 .. il0 + 3 and il0 + 16 .. il0 + 19
       const int nr = n - r0 < QP_STG_COLS ? n - r0 : QP_STG_COLS;
       const int s = lane_ >> 2, u = lane_ & 3;
+#ifdef EBT_ABL_HIT_STAGE_ONLY  // ablation builds only: the staging without the processing
+      if (s < 0) {
+#else
       if (s < nr) {
+#endif
         f32x4_t m, v0, v1;
         lds_staged(wmeta + s * 16, wst + s * 128 + u * 32, m, v0, v1);
         const uint32_t mw = __builtin_bit_cast(uint32_t, m[0]);
@@ -923,11 +977,17 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
               // out of the tile loop, and at the K-loop's register peak spills it
               uint32_t key = f2key(v[k]);
               asm volatile("" : "+v"(key));
+#ifndef EBT_ABL_NO_HIT_STORES  // ablation builds only (timing of the epilogue's stores)
               dst[p] = ((uint64_t)key << 32) | (uint64_t)(~row);
+#else
+              (void)dst;
+              (void)row;
+#endif
             }
           }
         }
       }
+      EPI_STAMP(3);
     }
   };
   auto store_quadrant = [&](const QpTile& T, const f32x4_t (&acc)[4][2], int ah, int bh) {
@@ -1003,11 +1063,16 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
       if (tid_ < QP_TILE) {
         const uint32_t c = lcnt[tid_];
         const int64_t q = cur.q0 + tid_;
+#ifndef EBT_ABL_NO_COUNT_STORES
         A->e.counts[q * A->e.ld_counts + cur.ct] = (uint8_t)(c < 255u ? c : 255u);
         if (c > (uint32_t)A->e.slots) A->e.ovf[q] = 1;
+#else
+        (void)q;
+#endif
         lcnt[tid_] = 0u;
       }
     }
+    EPI_STAMP(4);
     if (last) break;
     L += n_x;
     issue_params(tile_at(L));
@@ -1015,6 +1080,14 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
 #undef QP2_KTILE
   // the last tile restaged its own first K-tiles: drain before the LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef EBT_EPI_STAMP
+  if (EPI == EPI_FILTER && (tid & 63) == 0 && g_epi) {
+    const unsigned long long* e =
+        (const unsigned long long*)(smem + QP_LDS + QP_PARAM + QP_STG) + wave * 8;
+    unsigned long long* o = g_epi + ((int64_t)bid * 8 + wave) * 8;
+    for (int i = 0; i < 8; ++i) o[i] = e[i];
+  }
+#endif
 #ifdef EBT_CLOCK_STAMP
   if (EPI == EPI_FILTER && tid == 0 && g_stamps) {
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -1028,6 +1101,11 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
 #endif
 }
 
+#ifdef EBT_EPI_STAMP
+extern "C" int ebt_debug_epi_stamps(unsigned long long* buf) {
+  return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_epi), &buf, sizeof(buf)), "hipMemcpyToSymbol");
+}
+#endif
 #ifdef EBT_CLOCK_STAMP
 extern "C" int ebt_debug_clock_stamps(unsigned long long* buf) {
   return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf)),
