@@ -427,6 +427,16 @@ __device__ __forceinline__ void lds_rowscales8(const float* p, f32x4_t (&c)[2][4
       : "v"((uint32_t)(uintptr_t)p)
       : "memory");
 }
+// Per-lane select by a lane mask (bit l: lane l takes t): v_cndmask_b32 on an SGPR pair.
+__device__ __forceinline__ float vsel(uint64_t m, float t, float f) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+  return r;
+}
+__device__ __forceinline__ f32x4_t vsel4(uint64_t m, const f32x4_t& t, const f32x4_t& f) {
+  return f32x4_t{vsel(m, t[0], f[0]), vsel(m, t[1], f[1]), vsel(m, t[2], f[2]),
+                 vsel(m, t[3], f[3])};
+}
 // Staging writes (in asm: a plain LDS store would get the same vmcnt(0) as a plain read).
 __device__ __forceinline__ void lds_put_col(uint32_t dst, const f32x4_t& a0, const f32x4_t& a1,
                                             const f32x4_t& a2, const f32x4_t& a3,
@@ -903,6 +913,61 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
     EPI_STAMP(1);
     if (__builtin_expect(__ballot(colm != 0u) == 0ull, 1)) return;
     EPI_COUNT(6);
+#ifndef EBT_HIT_STAGE_BY_COLUMN
+    // 2. compact indices by BLOCK b = (bh, p): the lane's flagged columns of query half bh, one
+    //    per pass p (p = 0: its first, jj = 0 if flagged else 1; p = 1: jj = 1 when both are);
+    //    blocks in order, lanes in order within a block (n: uniform). A round writes one
+    //    9-instruction block per (bh, p) it holds -- usually the two p = 0 blocks, where the
+    //    per-column form wrote one per column c with a flagged lane (up to four): the staging is
+    //    bound by those ds_write_b128 (profiles/r4/ab/epilogue_phases.jsonl). The jj choice is a
+    //    lane-mask v_cndmask per value (a C select of two array elements would become a
+    //    dynamically indexed array in scratch).
+    int idx[4];
+    bool inb[4];
+    int n = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const bool f0 = (colm >> ((b >> 1) * 2)) & 1u, f1 = (colm >> ((b >> 1) * 2 + 1)) & 1u;
+      inb[b] = (b & 1) ? (f0 && f1) : (f0 || f1);
+      const uint64_t bc = __ballot(inb[b]);
+      idx[b] = n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bc >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bc, 0u));
+      n += __popcll(bc);
+    }
+    const uint32_t wst = (uint32_t)(uintptr_t)(smem + QP_LDS + QP_PARAM + wave * QP_STG_WAVE);
+    const uint32_t wmeta = wst + QP_STG_COLS * 128;
+    uint64_t* cand = A->e.cand;
+    const int64_t ld_cand = A->e.ld_cand;
+    const int slots = A->e.slots;
+    const int64_t rbase = A->e.idx_base + T.c0;
+#pragma unroll 1
+    for (int r0 = 0; r0 < n; r0 += QP_STG_COLS) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int s = idx[b] - r0;
+        if (inb[b] && s >= 0 && s < QP_STG_COLS) {
+          const int bh = b >> 1;
+          const f32x4_t(&ac0)[4][2] = acc_of(0, bh);
+          const f32x4_t(&ac1)[4][2] = acc_of(1, bh);
+          // jj = 1 for lanes whose first flagged column of this half is its second (or p = 1)
+          const bool j1 = (b & 1) || !((colm >> (bh * 2)) & 1u);
+          const uint64_t jm = __ballot(j1);
+          const int ql = bh * 128 + wb * 32 + (j1 ? 16 : 0) + fr_;
+          const float qs = vsel(jm, q4[bh * 2 + 1], q4[bh * 2]);
+          const float th = vsel(jm, t4[bh * 2 + 1], t4[bh * 2]);
+          const f32x4_t meta = {__builtin_bit_cast(float, (uint32_t)(ql | (g_ << 8))), qs, th, 0.f};
+#ifndef EBT_ABL_STAGE_META_ONLY
+          lds_put_col(wst + s * 128, vsel4(jm, ac0[0][1], ac0[0][0]), vsel4(jm, ac0[1][1], ac0[1][0]),
+                      vsel4(jm, ac0[2][1], ac0[2][0]), vsel4(jm, ac0[3][1], ac0[3][0]),
+                      vsel4(jm, ac1[0][1], ac1[0][0]), vsel4(jm, ac1[1][1], ac1[1][0]),
+                      vsel4(jm, ac1[2][1], ac1[2][0]), vsel4(jm, ac1[3][1], ac1[3][0]),
+                      wmeta + s * 16, meta);
+#else  // ablation builds only: the staging's record write alone (values left stale)
+          asm volatile("ds_write_b128 %0, %1" : : "v"(wmeta + s * 16), "v"(meta) : "memory");
+#endif
+        }
+      }
+#else
     // 2. compact indices: columns in order, lanes in order within a column (n: uniform)
     int idx[4];
     int n = 0;
@@ -938,6 +1003,7 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
 #endif
         }
       }
+#endif
       EPI_STAMP(2);
       // 3. lane: staged column s, values u * 8 .. u * 8 + 7 = half ah = u >> 1, accumulators
       // i0, i0 + 1 (i0 = (u & 1) * 2), rows il0 .. il0 + 3 and il0 + 16 .. il0 + 19
