@@ -294,7 +294,7 @@ constexpr int QP_THREADS = 512;
 constexpr int QP_HALF = 128 * 128;            // 16 KiB: 128 rows x 64 k x 2 B
 constexpr int QP_BUF = 4 * QP_HALF;           // one K-tile
 constexpr int QP_LDS = 2 * QP_BUF;            // 128 KiB
-constexpr int QP_GROUP_C = 4;
+constexpr int QP_GROUP_C = 4;  // (tile_at's whole-group fast path shifts by 2)
 constexpr int QP_TILE = 256;
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -497,7 +497,8 @@ struct QpArgs {
   const float* qscale;
   const float* cscale;
   int64_t cstride;
-  int n_qtiles, n_ctiles, ktiles, pad_;
+  int n_qtiles, n_ctiles, ktiles;
+  int pg_log2;  // log2(QP_GROUP_C * n_qtiles) when that is a power of two, else -1
   EpiArgs e;
 };
 typedef const __attribute__((address_space(4))) QpArgs* QpArgsK;
@@ -565,11 +566,21 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
     const QpArgsK A = qp_args();
     const int per_group = QP_GROUP_C * A->n_qtiles, n_ctiles = A->n_ctiles;
     QpTile T;
-    const int g = Lt / per_group, w = Lt - g * per_group;
+    // the walk's divisions are by launch constants: shifts when they are powers of two (every
+    // BASELINE batch: 4..64 query tiles) and the group is whole (uniform branches), so the tile
+    // boundary does not wait on scalar division sequences
+    const int pl = A->pg_log2;
+    const int g = pl >= 0 ? Lt >> pl : Lt / per_group, w = Lt - g * per_group;
     const int gc_rem = n_ctiles - g * QP_GROUP_C;
     const int gc = gc_rem < QP_GROUP_C ? gc_rem : QP_GROUP_C;
-    T.ct = g * QP_GROUP_C + w % gc;
-    const int qt = w / gc;
+    int qt;
+    if (gc == QP_GROUP_C) {
+      T.ct = g * QP_GROUP_C + (w & (QP_GROUP_C - 1));
+      qt = w >> 2;
+    } else {
+      T.ct = g * QP_GROUP_C + w % gc;
+      qt = w / gc;
+    }
     T.c0 = T.ct * QP_TILE;
     // catalog row of the tile's first row: c0, or ct * cstride for a strided sample of full
     // tiles (store / pool mode; n_rows then counts the sample's rows and the scores stay dense)
@@ -1250,6 +1261,8 @@ static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_
     a.n_qtiles = n_qtiles;
     a.n_ctiles = (int)n_ctiles;
     a.ktiles = ktiles;
+    const int per_group = QP_GROUP_C * n_qtiles;
+    a.pg_log2 = (per_group & (per_group - 1)) == 0 ? __builtin_ctz((unsigned)per_group) : -1;
     a.e = e;
     hipLaunchKernelGGL(k, grid, block, QP_LDS_TOTAL, stream, a);
     return launch_check("screen_gemm_qp2_kernel");
