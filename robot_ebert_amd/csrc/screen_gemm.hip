@@ -427,6 +427,15 @@ __device__ __forceinline__ void lds_rowscales8(const float* p, f32x4_t (&c)[2][4
       : "v"((uint32_t)(uintptr_t)p)
       : "memory");
 }
+// f2key (common.h) as selects instead of nested branches: one store block per hit value in the
+// filter epilogue runs it under a divergent mask, where each branch level cost an exec save /
+// skip pair.
+__device__ __forceinline__ uint32_t f2key_select(float f) {
+  const uint32_t u = __float_as_uint(f);
+  uint32_t k = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  k = f == 0.f ? 0x80000000u : k;
+  return (f == f && f != -__builtin_inff()) ? k : 0u;
+}
 // Per-lane select by a lane mask (bit l: lane l takes t): v_cndmask_b32 on an SGPR pair.
 __device__ __forceinline__ float vsel(uint64_t m, float t, float f) {
   float r;
@@ -1052,7 +1061,7 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
               const uint32_t row = (uint32_t)(rbase + il0 + (k < 4 ? k : 12 + k));
               // opaque key: otherwise the compiler hoists a 64-bit constant of f2key's zero case
               // out of the tile loop, and at the K-loop's register peak spills it
-              uint32_t key = f2key(v[k]);
+              uint32_t key = f2key_select(v[k]);
               asm volatile("" : "+v"(key));
 #ifndef EBT_ABL_NO_HIT_STORES  // ablation builds only (timing of the epilogue's stores)
               dst[p] = ((uint64_t)key << 32) | (uint64_t)(~row);
