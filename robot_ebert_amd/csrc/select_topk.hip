@@ -962,6 +962,18 @@ __device__ __forceinline__ float kth_minus_2eps_down(float kth, float eps) {
   return f;
 }
 
+#ifdef EBT_MERGE_STAMP
+// Diagnostic build only: the shader cycles of each phase of a query's wave merge (hit mode):
+// [0] list + counts loaded, [1] slot indices of the hits (LDS), [2] hits gathered, [3] the
+// selection and the list written; g_mstamp[4 b ..] (vector stores; nothing else reads them).
+__device__ unsigned long long* g_mstamp;
+extern "C" int ebt_debug_merge_stamps(unsigned long long* buf) {
+  return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_mstamp), &buf, sizeof(buf)), "hipMemcpyToSymbol");
+}
+#define MST(i) ms[i] = __builtin_amdgcn_s_memtime()
+#else
+#define MST(i)
+#endif
 template <bool DENSE>
 __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
     float* __restrict__ fv, int64_t* __restrict__ fi, int64_t B, int kprime, int k,
@@ -975,6 +987,10 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
   const int64_t b = (int64_t)blockIdx.x * WMERGE_Q + w;
   if (b >= B) return;
   uint64_t* U = stage[w];
+#ifdef EBT_MERGE_STAMP
+  unsigned long long ms[5] = {0, 0, 0, 0, 0};
+  MST(4);
+#endif
   uint64_t x[WTOP_E];
   bool over = false;
   uint32_t key_lo = 1u;  // the new k'-th key is >= the list's k'-th key
@@ -1052,6 +1068,7 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
         mine += c < slots ? c : slots;
       }
     }
+    MST(0);
     int incl = mine;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1077,6 +1094,7 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
         }
       }
     }
+    MST(1);
     const int mh = kprime + m < WTOP_N ? m : WTOP_N - kprime;
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1094,6 +1112,7 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
           U[kprime + h] = (ehi > elo && excluded(comp[u])) ? 0ull : comp[u];
       }
     }
+    MST(2);
     const int used = kprime + m < WTOP_N ? kprime + m : WTOP_N;
     used_n = used;
     __builtin_amdgcn_wave_barrier();
@@ -1112,6 +1131,15 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
       ne <= 8 ? wave_topk_write<8>(x, kprime, k, fv + b * kprime, fi + b * kprime, lane, key_lo)
               : wave_topk_write<WTOP_E>(x, kprime, k, fv + b * kprime, fi + b * kprime, lane, key_lo);
   const bool any_over = __ballot(over) != 0ull;
+#ifdef EBT_MERGE_STAMP
+  MST(3);
+  if (!DENSE && lane == 0 && g_mstamp) {
+    g_mstamp[4 * b + 0] = ms[0] - ms[4];
+    g_mstamp[4 * b + 1] = ms[1] - ms[0];
+    g_mstamp[4 * b + 2] = ms[2] - ms[1];
+    g_mstamp[4 * b + 3] = ms[3] - ms[2];
+  }
+#endif
   if (lane == 0) {
     // vspec: the speculative screen's VERIFY on the final list (spec_threshold_kernel,
     // SPEC_VERIFY) fused into the last merge: theta_spec > the k-th - 2 eps (rounded down), a
