@@ -370,8 +370,15 @@ enum { EPI_STORE = 0, EPI_FILTER = 1, EPI_POOL = 2 };
 // flagged (lane, query column) pairs per round, each its 32 raw accumulators (128 B) and a
 // 16-byte record {local query | row group << 8, query scale, threshold, -}.
 constexpr int QP_PARAM = 1024 + 3 * QP_TILE * 4;
+#ifndef EBT_HIT_STAGE_WHOLE
+// half columns: 16 raw accumulators (64 B) + a 16-byte record per slot, 32 slots per wave
+constexpr int QP_STG_COLS = 32;
+constexpr int QP_STG_VAL = 64;
+#else
 constexpr int QP_STG_COLS = 16;
-constexpr int QP_STG_WAVE = QP_STG_COLS * (128 + 16);
+constexpr int QP_STG_VAL = 128;
+#endif
+constexpr int QP_STG_WAVE = QP_STG_COLS * (QP_STG_VAL + 16);
 constexpr int QP_STG = 8 * QP_STG_WAVE;
 #ifdef EBT_EPI_STAMP
 // diagnostic build: per wave 8 u64 (phase cycle sums, tiles, last stamp) after the staging area
@@ -462,6 +469,10 @@ __device__ __forceinline__ void lds_put_col(uint32_t dst, const f32x4_t& a0, con
       : "v"(dst), "v"(meta_dst), "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5), "v"(a6),
         "v"(a7), "v"(meta)
       : "memory");
+}
+// One 16-byte staging write (in asm, as lds_put_col).
+__device__ __forceinline__ void lds_put_vec(uint32_t dst, const f32x4_t& v) {
+  asm volatile("ds_write_b128 %0, %1" : : "v"(dst), "v"(v) : "memory");
 }
 // A staged column's record and 8 of its values (one wait).
 __device__ __forceinline__ void lds_staged(uint32_t meta, uint32_t vals, f32x4_t& m, f32x4_t& v0,
@@ -895,6 +906,45 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
     float q4[4], t4[4];
     lds_qs_th4(lqs, lth, ql4, q4, t4);
     auto max4 = [](float a, float b, float c, float d) { return fmaxf(fmaxf(a, b), fmaxf(c, d)); };
+#ifndef EBT_HIT_STAGE_WHOLE
+    // the test per HALF column (c, ah), 16 values: bit c * 2 + ah of colm8; colm = per column
+    uint32_t colm8 = 0;
+    if constexpr (SIMPLE) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int ah = 0; ah < 2; ++ah) {
+          float mx = -__builtin_inff();
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const f32x4_t& a = acc_of(ah, c >> 1)[i][c & 1];
+            mx = fmaxf(mx, max4(a[0], a[1], a[2], a[3]));
+          }
+          colm8 |= (mx * q4[c] >= t4[c] || !(q4[c] >= 0.f) ? 1u : 0u) << (c * 2 + ah);
+        }
+    } else {
+      f32x4_t cs[2][4];
+      lds_rowscales8(lcs + wa * 64 + 4 * g_, cs);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float th_lo = t4[c] - fabsf(t4[c]) * 0x1p-20f - 0x1p-120f;
+#pragma unroll
+        for (int ah = 0; ah < 2; ++ah) {
+          float mx = -__builtin_inff();
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const f32x4_t& a = acc_of(ah, c >> 1)[i][c & 1];
+            const f32x4_t& s = cs[ah][i];
+            mx = fmaxf(mx, max4(a[0] * s[0], a[1] * s[1], a[2] * s[2], a[3] * s[3]));
+          }
+          colm8 |= (mx * q4[c] >= th_lo || !(q4[c] >= 0.f) ? 1u : 0u) << (c * 2 + ah);
+        }
+      }
+    }
+    uint32_t colm = 0;  // per column c: either half flagged
+#pragma unroll
+    for (int c = 0; c < 4; ++c) colm |= (((colm8 >> (2 * c)) & 3u) != 0u ? 1u : 0u) << c;
+#else
     uint32_t colm = 0;
     if constexpr (SIMPLE) {
 #pragma unroll
@@ -927,13 +977,117 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
         colm |= (mx * q4[c] >= th_lo || !(q4[c] >= 0.f) ? 1u : 0u) << c;
       }
     }
+#endif
 #ifdef EBT_ABL_HIT_NONE  // ablation builds only: the column test without the hit path
     if (__ballot(colm != 0u) != 0ull || true) return;
 #endif
     EPI_STAMP(1);
     if (__builtin_expect(__ballot(colm != 0u) == 0ull, 1)) return;
     EPI_COUNT(6);
-#ifndef EBT_HIT_STAGE_BY_COLUMN
+#ifndef EBT_HIT_STAGE_WHOLE
+    // 2. HALF columns (16 values, the half ah of a column with its own flag), by block b = (bh, p):
+    //    the lane's p-th flagged half column of query half bh (combo k = jj * 2 + ah, in order);
+    //    blocks in order, lanes in order within a block (n: uniform). A half is staged in 5
+    //    writes (4 value vectors + the record) instead of a column's 9, only where its own max
+    //    passes the test (a hit usually sits in one half), and 32 of them fit a round (the same
+    //    LDS as 16 columns), so C2's waves stage theirs in one round instead of two. The (jj, ah)
+    //    choice is a lane-mask v_cndmask per value, as for whole columns below.
+    const uint32_t wst = (uint32_t)(uintptr_t)(smem + QP_LDS + QP_PARAM + wave * QP_STG_WAVE);
+    const uint32_t wmeta = wst + QP_STG_COLS * QP_STG_VAL;
+    uint64_t* cand = A->e.cand;
+    const int64_t ld_cand = A->e.ld_cand;
+    const int slots = A->e.slots;
+    const int64_t rbase = A->e.idx_base + T.c0;
+    // the lane's flagged halves not staged yet, per query half bh (bit jj * 2 + ah)
+    uint32_t pend0 = colm8 & 0xFu, pend1 = (colm8 >> 4) & 0xFu;
+#pragma unroll 1
+    while (__ballot((pend0 | pend1) != 0u) != 0ull) {  // rounds (uniform)
+      int nr = 0;  // slots filled in this round (uniform)
+#pragma unroll
+      for (int bh = 0; bh < 2; ++bh) {
+        uint32_t& pend = bh ? pend1 : pend0;
+#pragma unroll 1
+        while (nr < QP_STG_COLS) {  // passes: each lane's next pending half of this bh
+          const bool in = pend != 0u;
+          const uint64_t bc = __ballot(in);
+          if (bc == 0ull) break;
+          const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bc >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bc, 0u));
+          if (in && nr + pos < QP_STG_COLS) {
+            const int s = nr + pos;
+            const int k = __builtin_ctz(pend);  // jj * 2 + ah
+            pend &= pend - 1u;
+            const bool j1 = (k >> 1) != 0, a1 = (k & 1) != 0;
+            const uint64_t jm = __ballot(j1), am = __ballot(a1);
+            const f32x4_t(&ac0)[4][2] = acc_of(0, bh);
+            const f32x4_t(&ac1)[4][2] = acc_of(1, bh);
+            const int ql = bh * 128 + wb * 32 + (j1 ? 16 : 0) + fr_;
+            const float qs = vsel(jm, q4[bh * 2 + 1], q4[bh * 2]);
+            const float th = vsel(jm, t4[bh * 2 + 1], t4[bh * 2]);
+            const f32x4_t meta = {
+                __builtin_bit_cast(float, (uint32_t)(ql | (g_ << 8) | ((a1 ? 1 : 0) << 12))), qs,
+                th, 0.f};
+            // one vector at a time (selected, then written): fewer registers live at once
+            const uint32_t dst = wst + s * QP_STG_VAL;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              lds_put_vec(dst + i * 16, vsel4(am, vsel4(jm, ac1[i][1], ac1[i][0]),
+                                              vsel4(jm, ac0[i][1], ac0[i][0])));
+            lds_put_vec(wmeta + s * 16, meta);
+          }
+          const int cnt = __popcll(bc);
+          nr = nr + cnt < QP_STG_COLS ? nr + cnt : QP_STG_COLS;
+        }
+      }
+      EPI_STAMP(2);
+      // 3. lane: staged half s, values u * 8 .. u * 8 + 7 = accumulators i0, i0 + 1 (i0 = 2 u)
+      // of half ah (the record), rows il0 .. il0 + 3 and il0 + 16 .. il0 + 19
+      const int s = lane_ >> 1, u = lane_ & 1;
+#ifdef EBT_ABL_HIT_STAGE_ONLY  // ablation builds only: the staging without the processing
+      if (s < 0) {
+#else
+      if (s < nr) {
+#endif
+        f32x4_t m, v0, v1;
+        lds_staged(wmeta + s * 16, wst + s * QP_STG_VAL + u * 32, m, v0, v1);
+        const uint32_t mw = __builtin_bit_cast(uint32_t, m[0]);
+        const int ql = (int)(mw & 255u), g = (int)((mw >> 8) & 15u), ah = (int)(mw >> 12);
+        const float qs = m[1], th = m[2];
+        const int il0 = ah * 128 + wa * 64 + u * 32 + 4 * g;
+        f32x4_t c0 = {1.f, 1.f, 1.f, 1.f}, c1 = c0;
+        if constexpr (!SIMPLE) lds_f32x4x2(lcs + il0, c0, c1);
+        float v[8];
+        uint32_t hb = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float a = k < 4 ? v0[k] : v1[k - 4];
+          v[k] = SIMPLE ? a * qs : a * qs * (k < 4 ? c0[k] : c1[k - 4]);
+          const int il = il0 + (k < 4 ? k : 12 + k);
+          hb |= (v[k] >= th && (full || T.c0 + il < n_rows) ? 1u : 0u) << k;
+        }
+        if (hb) {
+          const uint32_t base = lds_add_rtn(lcnt + ql, (uint32_t)__popc(hb));
+          uint64_t* dst = cand + (T.q0 + ql) * ld_cand + T.ct * slots;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t pp = base + (uint32_t)__popc(hb & ((1u << k) - 1u));
+            if (((hb >> k) & 1u) && pp < (uint32_t)slots) {
+              const uint32_t row = (uint32_t)(rbase + il0 + (k < 4 ? k : 12 + k));
+              uint32_t key = f2key_select(v[k]);
+              asm volatile("" : "+v"(key));
+#ifndef EBT_ABL_NO_HIT_STORES  // ablation builds only (timing of the epilogue's stores)
+              dst[pp] = ((uint64_t)key << 32) | (uint64_t)(~row);
+#else
+              (void)dst;
+              (void)row;
+#endif
+            }
+          }
+        }
+      }
+      EPI_STAMP(3);
+    }
+#else
     // 2. compact indices by BLOCK b = (bh, p): the lane's flagged columns of query half bh, one
     //    per pass p (p = 0: its first, jj = 0 if flagged else 1; p = 1: jj = 1 when both are);
     //    blocks in order, lanes in order within a block (n: uniform). A round writes one
@@ -987,43 +1141,6 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
 #endif
         }
       }
-#else
-    // 2. compact indices: columns in order, lanes in order within a column (n: uniform)
-    int idx[4];
-    int n = 0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const uint64_t bc = __ballot((colm >> c) & 1u);
-      idx[c] = n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bc >> 32),
-                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bc, 0u));
-      n += __popcll(bc);
-    }
-    const uint32_t wst = (uint32_t)(uintptr_t)(smem + QP_LDS + QP_PARAM + wave * QP_STG_WAVE);
-    const uint32_t wmeta = wst + QP_STG_COLS * 128;
-    uint64_t* cand = A->e.cand;
-    const int64_t ld_cand = A->e.ld_cand;
-    const int slots = A->e.slots;
-    const int64_t rbase = A->e.idx_base + T.c0;
-#pragma unroll 1
-    for (int r0 = 0; r0 < n; r0 += QP_STG_COLS) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int s = idx[c] - r0;
-        if (((colm >> c) & 1u) && s >= 0 && s < QP_STG_COLS) {
-          const f32x4_t(&ac0)[4][2] = acc_of(0, c >> 1);
-          const f32x4_t(&ac1)[4][2] = acc_of(1, c >> 1);
-          const int jj = c & 1;
-          const f32x4_t meta = {__builtin_bit_cast(float, (uint32_t)(ql4[c] | (g_ << 8))), q4[c],
-                                t4[c], 0.f};
-#ifndef EBT_ABL_STAGE_META_ONLY
-          lds_put_col(wst + s * 128, ac0[0][jj], ac0[1][jj], ac0[2][jj], ac0[3][jj], ac1[0][jj],
-                      ac1[1][jj], ac1[2][jj], ac1[3][jj], wmeta + s * 16, meta);
-#else  // ablation builds only: the staging's record write alone (values left stale)
-          asm volatile("ds_write_b128 %0, %1" : : "v"(wmeta + s * 16), "v"(meta) : "memory");
-#endif
-        }
-      }
-#endif
       EPI_STAMP(2);
       // 3. lane: staged column s, values u * 8 .. u * 8 + 7 = half ah = u >> 1, accumulators
       // i0, i0 + 1 (i0 = (u & 1) * 2), rows il0 .. il0 + 3 and il0 + 16 .. il0 + 19
@@ -1075,6 +1192,7 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
       }
       EPI_STAMP(3);
     }
+#endif
   };
   auto store_quadrant = [&](const QpTile& T, const f32x4_t (&acc)[4][2], int ah, int bh) {
 #pragma unroll
