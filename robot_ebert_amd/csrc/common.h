@@ -180,6 +180,38 @@ __device__ __forceinline__ int wave_rows_owner(int lane) {
   return NR == 1 ? 0 : (NR == 2 ? lane >> 5 : lane >> 4);
 }
 
+// Inclusive wave scans of a 32-bit value in DPP moves (no LDS): Hillis-Steele steps row_shr 1, 2,
+// 4, 8 inside each 16-lane row, then row_bcast:15 (rows 1, 3 take lane 15 of the row before) and
+// row_bcast:31 (rows 2, 3 take lane 31). Lanes a move has no source for read 0, the identity of
+// both ops. Every lane of the wave must be active.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_u32_or0(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_scan_add_u32(uint32_t v) {
+  v += dpp_u32_or0<0x111, 0xF>(v);
+  v += dpp_u32_or0<0x112, 0xF>(v);
+  v += dpp_u32_or0<0x114, 0xF>(v);
+  v += dpp_u32_or0<0x118, 0xF>(v);
+  v += dpp_u32_or0<0x142, 0xA>(v);
+  v += dpp_u32_or0<0x143, 0xC>(v);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_scan_max_u32(uint32_t v) {
+  v = max(v, dpp_u32_or0<0x111, 0xF>(v));
+  v = max(v, dpp_u32_or0<0x112, 0xF>(v));
+  v = max(v, dpp_u32_or0<0x114, 0xF>(v));
+  v = max(v, dpp_u32_or0<0x118, 0xF>(v));
+  v = max(v, dpp_u32_or0<0x142, 0xA>(v));
+  v = max(v, dpp_u32_or0<0x143, 0xC>(v));
+  return v;
+}
+// wave-wide max / min (uniform): the scan's last lane
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_max_u32(v), 63);
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) { return ~wave_max_u32(~v); }
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 
 // Guarded norm: sklearn _handle_zeros_in_scale (preprocessing/_data.py:118-123).

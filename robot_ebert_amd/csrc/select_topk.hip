@@ -836,14 +836,14 @@ template <int E>
 __device__ __forceinline__ uint64_t wave_cut(const uint64_t (&x)[WTOP_E],
                                              const uint32_t (&kx)[WTOP_E], int want, uint32_t lo,
                                              uint32_t hi) {
-  uint64_t l = __builtin_amdgcn_readfirstlane(lo), h = __builtin_amdgcn_readfirstlane(hi);
+  uint32_t l = __builtin_amdgcn_readfirstlane(lo), h = __builtin_amdgcn_readfirstlane(hi);
   if (l > h) l = h;
   while (l < h) {  // largest t with count(key >= t) >= want
-    const uint64_t mid = l + ((h - l + 1) >> 1);
-    if (wave_count_ge<E>(kx, (uint32_t)mid) >= want) l = mid;
+    const uint32_t mid = l + ((h - l) >> 1) + ((h - l) & 1u);  // l + ceil((h - l) / 2)
+    if (wave_count_ge<E>(kx, mid) >= want) l = mid;
     else h = mid - 1;
   }
-  const uint32_t t = (uint32_t)l;
+  const uint32_t t = l;
   int gt = 0, eq = 0;
 #pragma unroll
   for (int j = 0; j < E; ++j) {
@@ -874,6 +874,7 @@ __device__ __forceinline__ uint64_t wave_min_at_least(const uint64_t (&x)[WTOP_E
   uint64_t m = ~0ull;
 #pragma unroll
   for (int j = 0; j < E; ++j) m = (x[j] != 0ull && x[j] >= cut && x[j] < m) ? x[j] : m;
+#ifdef EBT_MERGE_SHFL_RED
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const uint64_t v = ((uint64_t)(uint32_t)__shfl_xor((int)(m >> 32), o, 64) << 32) |
@@ -881,6 +882,12 @@ __device__ __forceinline__ uint64_t wave_min_at_least(const uint64_t (&x)[WTOP_E
     m = v < m ? v : m;
   }
   return m;
+#else
+  // the smallest high half, then the smallest low half among the lanes holding it
+  const uint32_t mh = wave_min_u32((uint32_t)(m >> 32));
+  const uint32_t ml = wave_min_u32((uint32_t)(m >> 32) == mh ? (uint32_t)m : 0xffffffffu);
+  return ((uint64_t)mh << 32) | ml;
+#endif
 }
 
 // The k' largest of the wave's composites x (0 = empty), written partitioned at k (see above)
@@ -902,11 +909,16 @@ __device__ float wave_topk_write(const uint64_t (&x)[WTOP_E], int kprime, int k,
     kmax = max(kmax, kx[j]);
     if (x[j] != 0ull) kmin = min(kmin, kx[j]);
   }
+#ifdef EBT_MERGE_SHFL_RED
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
     kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o, 64));
   }
+#else
+  kmax = wave_max_u32(kmax);
+  kmin = wave_min_u32(kmin);
+#endif
   // every valid entry has key >= kmin, so count(key >= kmin) = nvalid >= want: a valid lower
   // end for the first bisection, ~8 steps shorter than 1 when the list started empty
   key_lo = key_lo > kmin ? key_lo : kmin;
@@ -931,11 +943,10 @@ __device__ float wave_topk_write(const uint64_t (&x)[WTOP_E], int kprime, int k,
       const bool inA = v > ck;                                  // the kk-1 best
       const bool inB = v != 0ull && v >= cw && v < ck && v != cw;  // between
       const uint64_t ma = __ballot(inA), mb = __ballot(inB);
-      int pos = -1;
-      if (inA) pos = na + __popcll(ma & below);
-      else if (inB) pos = nb + __popcll(mb & below);
-      else if (v == ck && v != 0ull) pos = kk - 1;
-      else if (v == cw && v != 0ull) pos = want - 1;
+      // (selects, not branches: the same precedence as an if / else chain)
+      const int pa = na + __popcll(ma & below), pb = nb + __popcll(mb & below);
+      const int pc = (v == ck && v != 0ull) ? kk - 1 : ((v == cw && v != 0ull) ? want - 1 : -1);
+      const int pos = inA ? pa : (inB ? pb : pc);
       if (pos >= 0) {
         ov[pos] = key2f((uint32_t)(v >> 32));
         oi[pos] = (int64_t)(~(uint32_t)v);
@@ -1069,6 +1080,7 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
       }
     }
     MST(0);
+#ifdef EBT_MERGE_SLOT_LOOP
     int incl = mine;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1076,7 +1088,66 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
       if (lane >= o) incl += v;
     }
     const int m = __shfl(incl, 63, 64);
+#else
+    const int incl = (int)wave_scan_add_u32((uint32_t)mine);
+    const int m = __builtin_amdgcn_readlane(incl, 63);
+#endif
     if (kprime + m > WTOP_N) over = true;
+#ifndef EBT_MERGE_SLOT_LOOP
+    // the hits without a per-lane loop over them: each group with hits marks its first hit's
+    // position h0 (relative to kprime) with ((g + 1) << 16) | h0 -- increasing with h0 -- so that
+    // an inclusive max scan over the positions gives every hit position h its group g and its
+    // slot h - h0; the wave scans 64 positions at a time and issues each hit's load at once.
+    // The same slots in the same order as the per-group loop below.
+    const int mh = kprime + m < WTOP_N ? m : WTOP_N - kprime;
+    uint32_t* M = (uint32_t*)(U + kprime);  // markers, in the hits' own LDS (rewritten below)
+#pragma unroll
+    for (int u = 0; u < WTOP_E; ++u) {
+      const int h = u * 64 + lane;
+      if (u * 64 < mh && h < mh) M[h] = 0u;
+    }
+    {
+      int r = incl - mine;
+#pragma unroll
+      for (int v = 0; v < WCNT; ++v) {
+        if (v >= nv) break;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          int c = cnt_at(v, e);
+          c = c < slots ? c : slots;
+          if (c > 0 && r < mh) M[r] = ((uint32_t)(g0 + 16 * v + e + 1) << 16) | (uint32_t)r;
+          r += c;
+        }
+      }
+    }
+    MST(1);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    {
+      uint64_t comp[WTOP_E];
+      uint32_t carry = 0u;
+#pragma unroll
+      for (int u = 0; u < WTOP_E; ++u) {
+        const int h = u * 64 + lane;
+        if (u * 64 < mh) {  // uniform
+          uint32_t mk = h < mh ? M[h] : 0u;
+          mk = max(wave_scan_max_u32(mk), carry);
+          carry = __builtin_amdgcn_readlane(mk, 63);
+          const int64_t g = (int64_t)(mk >> 16) - 1;
+          const int p = h - (int)(mk & 0xffffu);
+          comp[u] = h < mh ? cb[g * slots + p] : 0ull;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < WTOP_E; ++u) {
+        const int h = u * 64 + lane;
+        if (u * 64 < mh && h < mh)
+          U[kprime + h] = (ehi > elo && excluded(comp[u])) ? 0ull : comp[u];
+      }
+    }
+#else
     // the hits, in two passes: each lane writes the slot index of its hits (LDS only, so the
     // divergent per-group loop costs no memory latency), then the wave loads 64 hits at a time
     int pos = kprime + incl - mine;
@@ -1112,6 +1183,7 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
           U[kprime + h] = (ehi > elo && excluded(comp[u])) ? 0ull : comp[u];
       }
     }
+#endif
     MST(2);
     const int used = kprime + m < WTOP_N ? kprime + m : WTOP_N;
     used_n = used;
