@@ -131,6 +131,18 @@ constexpr int rescore_rows_per_trip() { return NU <= 2 ? 4 : (NU <= 6 ? EBT_RESC
 // registers for every row -- no LDS reads in the dot products, no query staging -- and gathers
 // rescore_rows_per_trip<NU>() rows per round trip from per-pass row lists. Per row the same
 // chunk order, the same per-chunk sums and the same wave butterfly: bitwise the same scores.
+#ifdef EBT_RESCORE_STAMP
+// Diagnostic build only: shader cycles of each phase of a query's rescore workgroup (wave 0's
+// view): [0] query + list + compaction, [1] pass A, [2] s_min + pass B's list, [3] pass B,
+// [4] order + write; g_rstamp[5 b ..] (vector stores; nothing else reads them).
+__device__ unsigned long long* g_rstamp;
+extern "C" int ebt_debug_rescore_stamps(unsigned long long* buf) {
+  return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_rstamp), &buf, sizeof(buf)), "hipMemcpyToSymbol");
+}
+#define RST(i) rs[i] = __builtin_amdgcn_s_memtime()
+#else
+#define RST(i)
+#endif
 template <int DT, bool VEC, int NU = 0>
 __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     const double* __restrict__ q64, int d, const void* __restrict__ cat, int64_t ld,
@@ -150,6 +162,10 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
   constexpr int NW = RTHREADS / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
+#ifdef EBT_RESCORE_STAMP
+  unsigned long long rs[6] = {0, 0, 0, 0, 0, 0};
+#endif
+  RST(0);
   if (tid == 0) {
     nvalid = 0;
     corrupt = 0;
@@ -227,6 +243,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     }
   }
   __syncthreads();
+  RST(1);
   const int nk = nkeep;
   // 2. exact scores in two passes. The list's first k positions hold its k best approx (a
   //    partitioned or sorted list): pass A scores those; their smallest exact score s_min
@@ -340,14 +357,27 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
   if constexpr (NU > 0) exact_rows(nsel);
   else exact_pass(true, 0.0);
   __syncthreads();
-  // s_min over the k top entries (all k present and valid), as an order-preserving key
-  for (int j = tid; j < nk; j += RTHREADS) {
-    if (pl[j] < k) {
-      atomicAdd(&ntop, 1);
+  RST(2);
+  // pass B's row count restarts (every thread read pass A's before the barrier above)
+  if (NU > 0 && tid == 0) nsel = 0;
+  // s_min over the k top entries (all k present and valid), as an order-preserving key: a wave
+  // count and a wave minimum (DPP), then one LDS atomic per wave instead of one per entry
+  for (int j0 = 0; j0 < nk; j0 += RTHREADS) {
+    const int j = j0 + tid;
+    const bool top = j < nk && pl[j] < k;
+    unsigned long long key = ~0ull;  // no valid key is all ones
+    if (top) {
       const double x = sc[j];
-      unsigned long long key = (unsigned long long)__double_as_longlong(x);
-      key = (key >> 63) ? ~key : (key | 0x8000000000000000ull);
-      if (x == x) atomicMin(&smin_key, key);
+      const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+      if (x == x) key = (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+    }
+    const uint64_t tb = __ballot(top);
+    const uint32_t kh = wave_min_u32((uint32_t)(key >> 32));
+    const uint32_t kl = wave_min_u32((uint32_t)(key >> 32) == kh ? (uint32_t)key : 0xffffffffu);
+    const unsigned long long wk = ((unsigned long long)kh << 32) | kl;
+    if (lane == 0) {
+      if (tb) atomicAdd(&ntop, (int)__popcll(tb));
+      if (wk != ~0ull) atomicMin(&smin_key, wk);
     }
   }
   __syncthreads();
@@ -361,8 +391,6 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
   }
   if constexpr (NU > 0) {
     // pass B's rows: past the list's first k and not below cut2; the others sorted last
-    if (tid == 0) nsel = 0;
-    __syncthreads();
     for (int j0 = 0; j0 < nk; j0 += RTHREADS) {
       const int j = j0 + tid;
       const bool rest = j < nk && pl[j] >= k;
@@ -375,28 +403,65 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
       if (sel) ix[sbase + __popcll(sb & ((1ull << lane) - 1))] = j;
     }
     __syncthreads();
+    RST(3);
     exact_rows(nsel);
   } else {
+    RST(3);
     exact_pass(false, cut2);
   }
+  RST(4);
   // 3. order the kept rows (score desc, row asc); positions past them read NaN / -1
   if (nk <= RESCORE_RANK_MAX) {
     // few rows (C2 / C3: ~120-150): each row's position is the number of rows before it,
-    // counted over LDS broadcast reads -- one barrier instead of a bitonic network's ~36
-    __syncthreads();
-    for (int j = tid; j < nk; j += RTHREADS) {
-      const double s = sc[j];
-      const int64_t r = rw[j];
+    // counted over LDS broadcast reads -- one barrier instead of a bitonic network's ~36. The
+    // reads go 8 rows at a time, all issued before the first compare (one LDS latency per 8
+    // rows, not per row), and up to RTHREADS / 2 rows take two threads each, one per half of
+    // the list (the upper half's count handed over in LDS): the same counts.
+    __shared__ int part[RTHREADS / 2];
+    auto count_before = [&](double s, int64_t r, int j, int lo, int hi) {
       int pos = 0;
-      for (int i = 0; i < nk; ++i) {
-        const double si = sc[i];
-        const int64_t ri = rw[i];
-        pos += (pair_before(si, ri, s, r) || (si == s && ri == r && i < j)) ? 1 : 0;
+      for (int i0 = lo; i0 < hi; i0 += 8) {
+        double si[8];
+        int64_t ri[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + u < hi ? i0 + u : hi - 1;
+          si[u] = sc[i];
+          ri[u] = rw[i];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + u;
+          pos += (i < hi && (pair_before(si[u], ri[u], s, r) ||
+                             (si[u] == s && ri[u] == r && i < j))) ? 1 : 0;
+        }
       }
+      return pos;
+    };
+    auto put = [&](double s, int64_t r, int pos) {
       if (pos < k) {
         out_s[b * k + pos] = s;
         out_r[b * k + pos] = r + row_offset;
       }
+    };
+    __syncthreads();
+    if (nk <= RTHREADS / 2) {
+      const int j = tid & (RTHREADS / 2 - 1);
+      const bool upper = tid >= RTHREADS / 2;
+      const int m = nk >> 1;
+      double s = 0.0;
+      int64_t r = 0;
+      int pos = 0;
+      if (j < nk) {
+        s = sc[j];
+        r = rw[j];
+        pos = upper ? count_before(s, r, j, m, nk) : count_before(s, r, j, 0, m);
+        if (upper) part[j] = pos;
+      }
+      __syncthreads();
+      if (!upper && j < nk) put(s, r, pos + part[j]);
+    } else {
+      for (int j = tid; j < nk; j += RTHREADS) put(sc[j], rw[j], count_before(sc[j], rw[j], j, 0, nk));
     }
     for (int j = nk + tid; j < k; j += RTHREADS) {
       out_s[b * k + j] = __builtin_nan("");
@@ -434,6 +499,13 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     if (corrupt) ok = -2;                           // internal error: row out of range
     certified[b] = ok;
   }
+#ifdef EBT_RESCORE_STAMP
+  RST(5);
+  if (tid == 0 && g_rstamp) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) g_rstamp[5 * b + i] = rs[i + 1] - rs[i];
+  }
+#endif
 }
 
 // The same rescore with the candidate rows gathered into LDS by LDS-DMA
