@@ -225,6 +225,56 @@ def pmc_traffic(config: str, world: int):
         return None, why
 
 
+def measure_topk(run_steps, timer, dev, steps: int, kprime: int, cfg: dict, es: int) -> dict:
+    """north_star's second roofline: the top-K stage that moves bytes on the fused path is the
+    exact rescore (rescore_kernel: candidate rows gathered from the resident catalog, float64
+    dot products, the (score desc, row asc) order, the certificate). Measured over `steps` extra
+    batches AFTER the timed region (its hipEvents would add stream gaps to `value`), on the
+    launch stream, with the rows each launch gathers counted inside the kernel
+    (ebt_timer_count_rows: one atomic per query). Algorithmic bytes per launch = gathered rows x
+    (d x element size + 8 for the row's float64 norm) + B x (k' x 12 list bytes + d x 8 query +
+    k x 16 results + 8 eps / certificate)."""
+    B, d, k = cfg["b"], cfg["d"], cfg["k"]
+    timer.count_rows(True)
+    timer.only("rescore")
+    timer.reset()
+    run_steps(steps)
+    torch.cuda.synchronize(dev)
+    ms, n = timer.query("rescore")
+    rows = timer.rows()
+    timer.count_rows(False)
+    if n == 0 or ms <= 0:
+        return {"kernel": "rescore_kernel", "launches": 0, "note": "no rescore launch recorded"}
+    per_rows = rows / n
+    byts = per_rows * (d * es + 8) + B * (kprime * 12 + d * 8 + k * 16 + 8)
+    avg_ms = ms / n
+    gbs = byts / (avg_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": "rescore_kernel", "achieved": round(gbs, 1),
+            "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
+            "launches": n, "avg_ms": round(avg_ms, 4), "rows_per_launch": round(per_rows, 1),
+            "rows_per_query": round(per_rows / B, 2), "bytes_per_launch": round(byts),
+            "bytes_formula": "rows x (d x es + 8) + B x (k' x 12 + d x 8 + k x 16 + 8); rows "
+                             "counted in the kernel",
+            "steps": steps,
+            "note": "hipEvents around every rescore launch over extra steps after the timed "
+                    "region; rows gathered are random 16-byte-vector row reads over the catalog"}
+
+
+def pmc_kernel_traffic(config: str, world: int, pattern: str):
+    """(HBM bytes per launch, kernel key) of the first kernel whose name contains `pattern` in
+    the committed PMC summary of this config / N (tools/prof_summary.py), or (None, None)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}_n{world}.json")
+    try:
+        with open(path) as f:
+            ks = json.load(f).get("kernels", {})
+    except (OSError, ValueError):
+        return None, None
+    for name, v in ks.items():
+        if pattern in name:
+            return v.get("hbm_bytes_per_launch"), name
+    return None, None
+
+
 def device_f64_check(emb: torch.Tensor, q: torch.Tensor, s, r, nq: int, chunk: int = 1 << 18):
     """Parity at full size without the host oracle (which would need the catalog in float64 on
     the host): nq evenly spaced queries against torch float64 on the device -- the catalog
@@ -610,6 +660,12 @@ def main() -> None:
         elapsed = float(t.item())
 
     dom_ms, dom_n = timer.query(dom_stage)
+    topk = measure_topk(run_steps, timer, dev, max(1, min(args.steps, 10)), pl["kprime"], cfg,
+                        emb.element_size())
+    topk["traffic"], tk = pmc_kernel_traffic(args.config, world, "rescore_kernel")
+    topk["traffic_note"] = (f"profiles/pmc_{args.config}_n{world}.json ({tk}): FETCH_SIZE x 2 + "
+                            "WRITE_SIZE per launch, separate --pmc passes" if tk else
+                            "no rescore entry in this config's PMC summary")
     timer.reset()
     timer.only()
     run_steps(1)
@@ -684,6 +740,7 @@ def main() -> None:
                          "(n_local rows); traffic from the committed PMC summary for this "
                          "config and N (profiles/pmc_<config>_n<N>.json), null when none",
             },
+            "roofline_topk": topk,
             "plan": pl,
             "stage_ms_per_step": {name: round(v[0], 4) for name, v in st.items()},
             "stage_breakdown": stage_breakdown(st, pl_ms, world),

@@ -55,7 +55,10 @@ extern "C" {
 #define EBT_F16 2
 #define EBT_F64 3
 
-/* Library version (major*10000 + minor*100 + patch). */
+/* Library version (major*10000 + minor*100 + patch).
+ * 0.2.0: ebt_rescore gained `timer`; ebt_comm gained the trailing `all_reduce_f64` pointer (the
+ *        library calls it whenever it is non-NULL: zero-initialise every ebt_comm).
+ * 0.3.0: ebt_timer_count_rows / ebt_timer_rows (additive). */
 int ebt_version(void);
 
 /* Message for the last non-zero return on this thread ("" if none). */
@@ -443,6 +446,8 @@ typedef int (*ebt_allgather_fn)(void* ctx, const void* send, void* recv, size_t 
  * of additions is then the collective's, a float64 round-off-level difference -- else an
  * all-gather of every rank's partial sums added in rank order. NULL = not provided. */
 typedef int (*ebt_allreduce_f64_fn)(void* ctx, double* buf, size_t count, void* stream);
+/* Zero-initialise (`ebt_comm c = {0};`, or memset) before filling it in: a field a caller built
+ * against an older layout does not set must read NULL (see ebt_version). */
 typedef struct ebt_comm {
   int32_t rank, world;
   int64_t n_global;           /* rows of the whole catalog: every shard's row_offset + n <= it */
@@ -626,6 +631,13 @@ int ebt_timer_set_mask(void* timer, uint32_t stage_mask);
 int ebt_timer_query(void* timer, int stage, double* total_ms, int64_t* launches);
 int ebt_timer_begin(void* timer, int stage, void* stream);
 int ebt_timer_end(void* timer, int stage, void* stream);
+/* Row accounting for the top-K roofline (bench.py `roofline_topk`): with on != 0 the timer owns
+ * one device counter (allocated on the current device) to which every rescore kernel recorded
+ * under EBT_STAGE_RESCORE adds the candidate rows it gathered (one atomic per query);
+ * ebt_timer_reset zeroes it, ebt_timer_rows reads it (synchronise the launch streams first).
+ * on = 0 frees it. Costs nothing when off. */
+int ebt_timer_count_rows(void* timer, int on);
+int ebt_timer_rows(void* timer, int64_t* rows);
 
 #ifdef __cplusplus
 }

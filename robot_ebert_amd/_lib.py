@@ -174,6 +174,8 @@ _SIGNATURES = {
     "ebt_timer_query": ([_VP, _INT, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64)], _INT),
     "ebt_timer_begin": ([_VP, _INT, _VP], _INT),
     "ebt_timer_end": ([_VP, _INT, _VP], _INT),
+    "ebt_timer_count_rows": ([_VP, _INT], _INT),
+    "ebt_timer_rows": ([_VP, ctypes.POINTER(_I64)], _INT),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -250,6 +252,16 @@ class Timer:
         n = ctypes.c_int64(0)
         call("ebt_timer_query", self._h, STAGES[stage], ctypes.byref(tot), ctypes.byref(n))
         return tot.value, n.value
+
+    def count_rows(self, on: bool = True) -> None:
+        """Count the candidate rows the rescore gathers (top-K roofline bytes; ebt_timer_rows)."""
+        call("ebt_timer_count_rows", self._h, 1 if on else 0)
+
+    def rows(self) -> int:
+        """Candidate rows gathered by the recorded rescores since the last reset."""
+        n = ctypes.c_int64(0)
+        call("ebt_timer_rows", self._h, ctypes.byref(n))
+        return n.value
 
     def region(self, stage: str, device=None):
         """Context manager: the work enqueued on the current stream inside the block is one

@@ -42,6 +42,20 @@ _SENTINEL = object()
 K_CLASSES = (32, 128, 512, 4096)
 
 
+def _answer(fut: Future, result=None, exc: Optional[BaseException] = None) -> None:
+    """Resolve a caller's Future unless it is already done (cancelled by its caller, or answered):
+    one abandoned request must never stop the thread that answers the others."""
+    if fut.done():
+        return
+    try:
+        if exc is not None:
+            fut.set_exception(exc)
+        else:
+            fut.set_result(result)
+    except Exception:  # noqa: BLE001 -- InvalidStateError: cancelled in between
+        pass
+
+
 def k_class(k: int) -> int:
     for i, hi in enumerate(K_CLASSES):
         if k <= hi:
@@ -140,6 +154,8 @@ class RecBatcher:
         return reqs, stop
 
     def _run(self) -> None:
+        if self._pipelined:
+            self._bind_device()
         while True:
             reqs, stop = self._collect()
             if reqs:
@@ -173,7 +189,7 @@ class RecBatcher:
                 scores, rows = self._score(self.catalog, k_max, liked=liked, exclude=excl)
             except BaseException as e:  # the whole batch failed: every caller sees the error
                 for r in reqs:
-                    r[3].set_exception(e)
+                    _answer(r[3], exc=e)
                 return
             self._deliver(reqs, scores, rows)
             return
@@ -184,27 +200,39 @@ class RecBatcher:
         except BaseException as e:
             self._slots.release()
             for r in reqs:
-                r[3].set_exception(e)
+                _answer(r[3], exc=e)
             return
         self._done.put((p, reqs))
 
     def _complete(self) -> None:
         """Completion thread: finish the submitted batches in order and answer their callers."""
         from .search import score_topk_finish
+        self._bind_device()
         while True:
             item = self._done.get()
             if item is _SENTINEL:
                 return
             p, reqs = item
-            try:
-                scores, rows = score_topk_finish(p)
-            except BaseException as e:
+            try:   # the slot is released whatever happens to this batch's callers
+                try:
+                    scores, rows = score_topk_finish(p)
+                except BaseException as e:  # noqa: BLE001
+                    for r in reqs:
+                        _answer(r[3], exc=e)
+                    continue
+                self._deliver(reqs, scores, rows)
+            except BaseException:  # noqa: BLE001 -- never let one batch stop the thread
+                pass
+            finally:
                 self._slots.release()
-                for r in reqs:
-                    r[3].set_exception(e)
-                continue
-            self._deliver(reqs, scores, rows)
-            self._slots.release()
+
+    def _bind_device(self) -> None:
+        """Both batcher threads run on the catalog's device: libebert's per-device event pools
+        key on the calling thread's current HIP device."""
+        dev = getattr(self.catalog, "device", None)
+        if dev is not None and getattr(dev, "type", None) == "cuda":
+            import torch
+            torch.cuda.set_device(dev)
 
     def _deliver(self, reqs: list, scores, rows) -> None:
         try:
@@ -212,10 +240,10 @@ class RecBatcher:
             rows = rows.cpu().numpy() if hasattr(rows, "cpu") else np.asarray(rows)
         except BaseException as e:
             for r in reqs:
-                r[3].set_exception(e)
+                _answer(r[3], exc=e)
             return
         self._record(len(reqs))
         for i, (_, _, k, fut) in enumerate(reqs):
             s, r = scores[i, :k], rows[i, :k]
             keep = r >= 0
-            fut.set_result((s[keep], r[keep]))
+            _answer(fut, (s[keep], r[keep]))

@@ -52,10 +52,20 @@ void set_max_lds(const void* fn, int bytes) {
 
 // Completion events of submitted batches, recycled (creating and destroying one per batch is
 // host time on every step): per device, a free list under a lock.
-hipEvent_t event_get() {
-  static_assert(sizeof(hipEvent_t) == sizeof(void*), "event handle");
+// The pool is keyed by the STREAM's device (a batch may be submitted and finished from threads
+// whose current device differs from it: ADVICE r4), and an event is created under that device.
+static int stream_device(hipStream_t st) {
   int dev = 0;
   (void)hipGetDevice(&dev);
+  if (st) {
+    hipDevice_t d = 0;
+    if (hipStreamGetDevice(st, &d) == hipSuccess) dev = (int)d;
+  }
+  return dev;
+}
+hipEvent_t event_get(hipStream_t st) {
+  static_assert(sizeof(hipEvent_t) == sizeof(void*), "event handle");
+  const int dev = stream_device(st);
   {
     std::lock_guard<std::mutex> g(event_pool_mutex());
     auto& fl = event_pool()[dev & 63];
@@ -65,14 +75,17 @@ hipEvent_t event_get() {
       return e;
     }
   }
+  int cur = dev;
+  (void)hipGetDevice(&cur);
+  if (cur != dev) (void)hipSetDevice(dev);
   hipEvent_t e = nullptr;
-  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+  if (cur != dev) (void)hipSetDevice(cur);
   return e;
 }
-void event_put(hipEvent_t e) {
+void event_put(hipEvent_t e, hipStream_t st) {
   if (!e) return;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
+  const int dev = stream_device(st);
   std::lock_guard<std::mutex> g(event_pool_mutex());
   auto& fl = event_pool()[dev & 63];
   if (fl.size() < 64) fl.push_back(e);
@@ -108,7 +121,7 @@ int mask_excluded(float*, int64_t, int64_t, int64_t, int64_t, const int64_t*, co
                   hipStream_t);
 int rescore(const double*, int64_t, int32_t, const void*, int, int64_t, const double*, int64_t,
             const float*, const int64_t*, int32_t, int32_t, int64_t, const float*, const double*,
-            double*, int64_t*, int32_t*, hipStream_t, const int*, int);
+            double*, int64_t*, int32_t*, hipStream_t, const int*, int, unsigned long long*);
 int screen_gemm_filter(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
                        const float*, const float*, const float*, uint64_t*, int64_t, int,
                        uint8_t*, int64_t, int*, int64_t, hipStream_t);
@@ -173,6 +186,10 @@ struct Timer {
   std::mutex mu;
   uint32_t mask = 0xffffffffu;  // stages recorded (ebt_timer_set_mask)
   std::vector<std::pair<int, hipEvent_t>> open;  // ebt_timer_begin without its _end yet
+  // ebt_timer_count_rows: the rescore kernels add the candidate rows they gather here (device
+  // memory of the device current at that call; one u64), for the top-K roofline's bytes
+  unsigned long long* d_rows = nullptr;
+  int rows_dev = -1;
 
   hipEvent_t get() {
     if (used == pool.size()) {
@@ -187,8 +204,16 @@ struct Timer {
   }
   ~Timer() {
     for (auto e : pool) (void)hipEventDestroy(e);
+    if (d_rows) (void)hipFree(d_rows);
   }
 };
+
+// The row counter the rescore adds to, when counting is on and the rescore stage is recorded
+static unsigned long long* timer_rows(void* timer) {
+  Timer* t = (Timer*)timer;
+  if (!t || !t->d_rows || !((t->mask >> EBT_STAGE_RESCORE) & 1u)) return nullptr;
+  return t->d_rows;
+}
 
 struct StageScope {
   Timer* t;
@@ -488,7 +513,7 @@ using namespace ebt;
 
 extern "C" {
 
-int ebt_version(void) { return 200; }  // 0.2.0: ebt_rescore gained `timer` (ABI break)
+int ebt_version(void) { return 300; }  // 0.3.0: ebt_timer_count_rows / _rows (see ebert.h)
 
 const char* ebt_last_error(void) { return g_err; }
 
@@ -575,7 +600,7 @@ int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dt
   StageScope sc(timer, EBT_STAGE_RESCORE, (hipStream_t)stream);
   return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, cand_vals, cand_rows, kprime, k,
                  n_rows, eps, t_floor, out_scores, out_rows, certified, (hipStream_t)stream,
-                 nullptr, 0);
+                 nullptr, 0, timer_rows(timer));
 }
 
 int ebt_screen_exact(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
@@ -985,7 +1010,8 @@ int ebt_cosine_topk_prepared(const double* q64, const void* qimg, const float* q
   if (rc) return rc;
   StageScope s(timer, EBT_STAGE_RESCORE, st);
   return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, fv, fi, kprime, k, n_rows,
-                 so.eps, nullptr, out_scores, out_rows, certified, st, so.ovf, 0);
+                 so.eps, nullptr, out_scores, out_rows, certified, st, so.ovf, 0,
+                 timer_rows(timer));
 }
 
 int ebt_cosine_screen(const double* q64, const void* qimg, const float* qscale, const float* eps,
@@ -1113,7 +1139,43 @@ int ebt_timer_reset(void* timer) {
   t->recs.clear();
   t->open.clear();
   t->used = 0;
+  if (t->d_rows) {
+    const unsigned long long zero = 0;
+    return hip_check(hipMemcpy(t->d_rows, &zero, sizeof(zero), hipMemcpyHostToDevice),
+                     "hipMemcpy");
+  }
   return EBT_OK;
+}
+
+int ebt_timer_count_rows(void* timer, int on) {
+  if (!timer) return EBT_EINVAL;
+  Timer* t = (Timer*)timer;
+  std::lock_guard<std::mutex> g(t->mu);
+  if (!on) {
+    if (t->d_rows) (void)hipFree(t->d_rows);
+    t->d_rows = nullptr;
+    return EBT_OK;
+  }
+  if (t->d_rows) return EBT_OK;
+  int rc = hip_check(hipMalloc((void**)&t->d_rows, sizeof(unsigned long long)), "hipMalloc");
+  if (rc) return rc;
+  (void)hipGetDevice(&t->rows_dev);
+  const unsigned long long zero = 0;
+  return hip_check(hipMemcpy(t->d_rows, &zero, sizeof(zero), hipMemcpyHostToDevice), "hipMemcpy");
+}
+
+int ebt_timer_rows(void* timer, int64_t* rows) {
+  if (!timer || !rows) return EBT_EINVAL;
+  Timer* t = (Timer*)timer;
+  std::lock_guard<std::mutex> g(t->mu);
+  *rows = 0;
+  if (!t->d_rows) return EBT_OK;
+  unsigned long long v = 0;
+  // hipMemcpy waits for the work before it on the null stream; the caller synchronises the
+  // launch streams first (as for ebt_timer_query)
+  int rc = hip_check(hipMemcpy(&v, t->d_rows, sizeof(v), hipMemcpyDeviceToHost), "hipMemcpy");
+  *rows = (int64_t)v;
+  return rc;
 }
 
 int ebt_timer_begin(void* timer, int stage, void* stream) {

@@ -25,8 +25,8 @@ void set_error(const char* fmt, ...);
 int hip_check(hipError_t e, const char* what);
 int launch_check(const char* what);
 void set_max_lds(const void* fn, int bytes);
-hipEvent_t event_get();
-void event_put(hipEvent_t e);
+hipEvent_t event_get(hipStream_t st);
+void event_put(hipEvent_t e, hipStream_t st);
 std::mutex& event_pool_mutex();
 std::vector<hipEvent_t>* event_pool();
 

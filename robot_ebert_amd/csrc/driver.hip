@@ -483,11 +483,11 @@ int ebt_cosine_topk_submit(const ebt_catalog* cat, const void* q, int q_dtype, i
   rc = hip_check(hipMemcpyAsync(cert_host, cert, (size_t)(B + 1) * 4, hipMemcpyDeviceToHost, st),
                  "hipMemcpyAsync");
   if (rc) return rc;
-  hipEvent_t ev = event_get();
+  hipEvent_t ev = event_get(st);
   if (!ev) return hip_check(hipErrorOutOfMemory, "hipEventCreate");
   rc = hip_check(hipEventRecord(ev, st), "hipEventRecord");
   if (rc) {
-    event_put(ev);
+    event_put(ev, st);
     return rc;
   }
   ebt_pending P{};
@@ -522,7 +522,7 @@ int ebt_cosine_topk_finish(ebt_pending* p) {
   const ebt_catalog& c = *p->cat;
   hipEvent_t ev = (hipEvent_t)p->event;
   int rc = hip_check(hipEventSynchronize(ev), "hipEventSynchronize");
-  event_put(ev);
+  event_put(ev, st);
   p->event = nullptr;
   if (rc) return rc;
   const int64_t B = p->B;
@@ -1057,7 +1057,9 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
     if (rc) return rc;
     const double m_total = 256.0 * (double)S.tiles * R;
     const int j = sh_spec_rank((double)L.kprime * m_total / (double)cm.n_global);
-    if (j <= S.J) {
+    // exact for j <= J; when J was clamped to G every shard sent all of its maxima, and any
+    // j <= RG / 2 is (distributed.theta_from_samples decides alike)
+    if (j <= S.J || (S.J == S.G && j <= S.RG / 2)) {
       float* perm = (float*)(ws + S.off_perm);
       theta = (float*)(ws + S.off_theta);
       const int64_t RGJ = (int64_t)R * S.GJ;
@@ -1134,11 +1136,11 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
   rc = hip_check(hipMemcpyAsync(host, cert, (size_t)(B + 1) * 4, hipMemcpyDeviceToHost, st),
                  "hipMemcpyAsync");
   if (rc) return rc;
-  hipEvent_t ev = event_get();
+  hipEvent_t ev = event_get(st);
   if (!ev) return hip_check(hipErrorOutOfMemory, "hipEventCreate");
   rc = hip_check(hipEventRecord(ev, st), "hipEventRecord");
   if (rc) {
-    event_put(ev);
+    event_put(ev, st);
     return rc;
   }
   ebt_sharded_pending P{};
@@ -1216,11 +1218,11 @@ int ebt_cosine_topk_sharded_finish(ebt_sharded_pending* p) {
     rc = sh_full_merge(S, p->comm, ws, B, k, p->out_scores, p->out_rows, timer, st);
   }
   if (rc) return rc;
-  hipEvent_t ev = event_get();
+  hipEvent_t ev = event_get(st);
   if (!ev) return hip_check(hipErrorOutOfMemory, "hipEventCreate");
   rc = hip_check(hipEventRecord(ev, st), "hipEventRecord");
   if (rc) {
-    event_put(ev);
+    event_put(ev, st);
     return rc;
   }
   p->event = ev;
@@ -1236,7 +1238,7 @@ int ebt_cosine_topk_sharded_wait(ebt_sharded_pending* p) {
   hipStream_t st = (hipStream_t)lp.stream;
   hipEvent_t ev = (hipEvent_t)p->event;
   int rc = hip_check(hipEventSynchronize(ev), "hipEventSynchronize");
-  event_put(ev);
+  event_put(ev, st);
   p->event = nullptr;
   p->stage = 0;
   if (rc) return rc;

@@ -150,14 +150,14 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     const int64_t* __restrict__ cand_rows, int kprime, int kpp, int k, int64_t n_rows,
     const float* __restrict__ eps, const double* __restrict__ t_floor, double* __restrict__ out_s,
     int64_t* __restrict__ out_r, int32_t* __restrict__ certified, const int* __restrict__ ovf_cnt,
-    int ovf_cap) {
+    int ovf_cap, unsigned long long* __restrict__ gathered) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* qs = (double*)smem;                           // d (NU = 0 only)
   double* sc = qs + (NU > 0 ? 0 : ((d + 1) & ~1));      // kpp: approx, then exact
   int64_t* rw = (int64_t*)(sc + kpp);         // kpp
   int* pl = (int*)(rw + kpp);                 // kpp: list position of each kept row
   int* ix = pl + kpp;                         // kpp (NU > 0): the rows of the current pass
-  __shared__ int nvalid, corrupt, nkeep, ntop, nsel;
+  __shared__ int nvalid, corrupt, nkeep, ntop, nsel, ngath;
   __shared__ unsigned long long smin_key;
   constexpr int NW = RTHREADS / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -172,6 +172,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     nkeep = 0;
     ntop = 0;
     nsel = 0;
+    ngath = 0;
     smin_key = ~0ull;
   }
   constexpr int ES = (DT == EBT_F64) ? 8 : (DT == EBT_F32 ? 4 : 2);
@@ -264,6 +265,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     if (!sel_a && !sel_b) continue;
     const int ja = sel_a ? j : jb;          // one selected row goes first
     const bool hb = sel_a && sel_b;         // a second one
+    if (gathered && lane == 0) atomicAdd(&ngath, hb ? 2 : 1);
     const int64_t ra = rw[ja], rb = hb ? rw[jb] : ra;
     const double ga = gnorm[ra], gb = gnorm[rb];
     double sa = 0.0, sb = 0.0;
@@ -359,7 +361,10 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
   __syncthreads();
   RST(2);
   // pass B's row count restarts (every thread read pass A's before the barrier above)
-  if (NU > 0 && tid == 0) nsel = 0;
+  if (NU > 0 && tid == 0) {
+    ngath = nsel;
+    nsel = 0;
+  }
   // s_min over the k top entries (all k present and valid), as an order-preserving key: a wave
   // count and a wave minimum (DPP), then one LDS atomic per wave instead of one per entry
   for (int j0 = 0; j0 < nk; j0 += RTHREADS) {
@@ -498,6 +503,8 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     if (ovf_cnt && ovf_cnt[b] > ovf_cap) ok = -1;  // fused screen dropped candidates
     if (corrupt) ok = -2;                           // internal error: row out of range
     certified[b] = ok;
+    // rows gathered by the two passes (roofline accounting: ebt_timer_count_rows)
+    if (gathered) atomicAdd(gathered, (unsigned long long)(ngath + (NU > 0 ? nsel : 0)));
   }
 #ifdef EBT_RESCORE_STAMP
   RST(5);
@@ -740,7 +747,7 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
             const double* gnorm, int64_t row_offset, const float* cand_vals,
             const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
             const double* t_floor, double* out_s, int64_t* out_r, int32_t* certified,
-            hipStream_t st, const int* ovf_cnt, int ovf_cap) {
+            hipStream_t st, const int* ovf_cnt, int ovf_cap, unsigned long long* gathered) {
   if (!q64 || !cat || !gnorm || !cand_vals || !cand_rows || !eps || !out_s || !out_r ||
       !certified || B < 0 || d <= 0 || ld < d || k < 1 || kprime < k || kprime > 4096 ||
       dtype < 0 || dtype > 3) {
@@ -797,7 +804,7 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
   set_max_lds((const void*)rescore_kernel<DT, true, NU>, (int)lds_r);                          \
   hipLaunchKernelGGL((rescore_kernel<DT, true, NU>), grid, block, lds_r, st, q64, d, cat, ld,   \
                      gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,      \
-                     t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap);
+                     t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap, gathered);
 #define EBT_RSR_NU(DT)                                                                          \
   switch (nu) {                                                                                 \
     case 1: EBT_RSR(DT, 1) break;                                                               \
@@ -823,11 +830,11 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
   if (vec)                                                                                      \
     hipLaunchKernelGGL((rescore_kernel<DT, true>), grid, block, lds, st, q64, d, cat, ld,       \
                        gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,    \
-                       t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap);                     \
+                       t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap, gathered);           \
   else                                                                                          \
     hipLaunchKernelGGL((rescore_kernel<DT, false>), grid, block, lds, st, q64, d, cat, ld,      \
                        gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,    \
-                       t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap);
+                       t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap, gathered);
   switch (dtype) {
     case EBT_F32: EBT_RS(EBT_F32) break;
     case EBT_BF16: EBT_RS(EBT_BF16) break;

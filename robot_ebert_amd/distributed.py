@@ -301,7 +301,8 @@ def _shared_theta(coll, catalog: Catalog, qb, kprime: int, tiles: int, timer=Non
         with region(timer, "collective_wait", catalog.device):
             g = wait()
         with region(timer, "small", catalog.device):
-            return theta_from_samples(g, qb, kprime, tiles, catalog.n_global, catalog.n)
+            return theta_from_samples(g, qb, kprime, tiles, catalog.n_global, catalog.n,
+                                      sent=J or 4 * tiles)
     return theta
 
 
@@ -317,14 +318,20 @@ def local_sample(catalog: Catalog, qb, tiles: int, timer=None) -> torch.Tensor:
 
 
 def theta_from_samples(g: torch.Tensor, qb, kprime: int, tiles: int, n_global: int,
-                       n_local: int):
+                       n_local: int, sent: Optional[int] = None):
     """(theta [B_pad], expected hits per query on an n_local-row shard) from the gathered
-    [R, B, 4 tiles] maxima, or None when the sample is too small to say anything."""
+    [R, B, G] maxima, or None when the sample is too small to say anything. `sent` = how many
+    maxima per query each shard sent (J of sample_send_width; the gathered rows of a packed
+    send carry one extra -inf column, G = J + 1): the j-th largest of the union is exact for
+    j <= sent, and for any j <= RG / 2 when every shard sent all of its 4 * tiles maxima
+    (driver.hip makes the same decision)."""
     R, B, G = g.shape
     m_total = 256 * tiles * R
     RG = R * 4 * tiles
+    if sent is None:
+        sent = G
     j = spec_rank(kprime * m_total / max(n_global, 1))
-    if j > RG // 2 or j > G:
+    if j > RG // 2 or (sent < 4 * tiles and j > sent):
         return None
     theta = pool_kth(g.permute(1, 0, 2).reshape(B, R * G), B, qb.B_pad, j)
     hits = (j + j * j / (2.0 * RG)) * n_local / m_total

@@ -150,3 +150,33 @@ def test_batcher_stats_are_bounded():
     st = b.stats()
     assert len(b.batches) == 4 and st["batches"] == 10 and st["requests"] == 10
     assert sum(st["size_hist_pow2"].values()) == 10 and st["size_hist_pow2"] == {0: 10}
+
+
+def test_pipelined_cancelled_request_does_not_wedge(monkeypatch):
+    """in pipelined mode a caller that cancels its Future while its batch is
+    on the GPU must not stop the completion thread (which would keep the in-flight slot and hang
+    every later request). The GPU submit / finish pair is replaced by the float64 oracle here."""
+    import robot_ebert_amd.search as S
+    x = np.random.default_rng(11).standard_normal((400, 8))
+    cat = _Cat(x)
+    gate = threading.Event()
+
+    def submit(c, k, liked, exclude):
+        qs = np.stack([R.mean_cosine_query(c.x[l]) for l in liked])
+        return R.cosine_topk(qs, c.x, k, exclude)
+
+    def finish(p):
+        gate.wait(10)
+        return p
+    monkeypatch.setattr(S, "score_topk_submit", submit)
+    monkeypatch.setattr(S, "score_topk_finish", finish)
+    b = RecBatcher(cat, max_batch=8, max_wait_ms=0.0, max_inflight=1)
+    first = b.submit([1, 2], [3], 5)
+    assert first.cancel()          # still pending: its batch waits in finish()
+    gate.set()
+    for i in range(6):             # one slot: every later batch needs the first one's release
+        s, r = b.submit([i], [], 4).result(timeout=10)
+        ws, wr = _direct(cat, [i], [], 4)
+        np.testing.assert_array_equal(r, wr)
+    b.close()
+    assert b.stats()["requests"] >= 6

@@ -6,12 +6,23 @@
 #   tests  OUT EXPR [FILES..]  pytest -m gpu -k EXPR over FILES (default tests/)
 #   bench  OUT CONFIG [ARGS..] bench.py --config CONFIG ARGS -> OUT/bench_CONFIG.json (+ .log)
 #   prof   OUT CONFIG [STEPS]  rocprofv3 kernel-trace + stats, then FETCH_SIZE and WRITE_SIZE
-#                              PMC passes (one counter block each) on the screening GEMM
+#                              PMC passes (one counter block each) on the screening GEMM and the
+#                              rescore (the top-K roofline's kernel)
 #   py     OUT SCRIPT [ARGS..] python SCRIPT ARGS > OUT/out.jsonl (tools/*.py experiments)
 #   trace  OUT CMD...          rocprofv3 --kernel-trace --stats of CMD (a kernel timeline)
 #   pmc    OUT REGEX CMD...    a trace pass, then one PMC counter group per rocprofv3 run
 #                              (occupancy / waits, FETCH_SIZE, LDS, instruction mix) over the
 #                              kernels matching REGEX; summarise with tools/pmc_summary.py
+#   ab     OUT ALT CFGS [N]    interleaved A/B bench lines (no CPU baseline), N rounds (2) of
+#                              every config in CFGS (comma list): the current build, then ALT --
+#                              a library (EBERT_LIB=ALT, e.g. _abl/libebert_prev.so from
+#                              tools/abl_build.sh) or an environment setting VAR=VALUE
+#   epi    OUT LIB...          per-phase filter-epilogue cycles (tools/epi_stamp.py) of C2- and
+#                              C3-shaped segments, per -DEBT_EPI_STAMP build _abl/libebert_LIB.so
+#   stamp  OUT LIB...          clock-stamp launches (tools/clock_stamp.py) of C2- and C3-shaped
+#                              filter segments per -DEBT_CLOCK_STAMP build _abl/libebert_LIB.so
+#   recipe NAME                a named evidence run of the table at the end of this file (the
+#                              round-4 A/B runs and closing passes, profiles/r4/README.md)
 export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 MODE=$1
@@ -59,9 +70,9 @@ EOF
     B="python3 bench.py --config $CFG --steps $STEPS --warmup 1 --no-cpu-baseline"
     timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o run \
       -- $B > "$O/trace.json" 2> "$O/trace.log" &&
-    timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex screen_gemm \
+    timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'screen_gemm|rescore_kernel' \
       --output-format csv -d "$O/fetch" -o run -- $B > "$O/fetch.json" 2> "$O/fetch.log" &&
-    timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex screen_gemm \
+    timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'screen_gemm|rescore_kernel' \
       --output-format csv -d "$O/write" -o run -- $B > "$O/write.json" 2> "$O/write.log"
     rc=$?
     echo "prof $CFG rc=$rc"
@@ -99,8 +110,73 @@ EOF
     echo "pmc rc=$rc"
     exit $rc
     ;;
+  ab)
+    ALT=$1
+    CFGS=$2
+    N=${3:-2}
+    for i in $(seq "$N"); do
+      for c in ${CFGS//,/ }; do
+        case $c in C2) A="--steps 50" ;; C3) A="--steps 20" ;; *) A="--steps 5 --warmup 1" ;; esac
+        bash "$0" bench "${O#gpurun_out/}/${c}_new$i" "$c" $A --no-cpu-baseline || exit 1
+        if [[ $ALT == *=* ]]; then
+          env "$ALT" bash "$0" bench "${O#gpurun_out/}/${c}_alt$i" "$c" $A --no-cpu-baseline || exit 1
+        else
+          EBERT_LIB=$ALT bash "$0" bench "${O#gpurun_out/}/${c}_alt$i" "$c" $A --no-cpu-baseline ||
+            exit 1
+        fi
+      done
+    done
+    ;;
+  epi)
+    for v in "$@"; do
+      bash "$0" py "${O#gpurun_out/}/c2_$v" tools/epi_stamp.py --lib "_abl/libebert_$v.so" \
+        --n 100000 --b 1024 --d 768 --img bf16 --z 2.73 --cscale || exit 1
+      bash "$0" py "${O#gpurun_out/}/c3_$v" tools/epi_stamp.py --lib "_abl/libebert_$v.so" || exit 1
+    done
+    ;;
+  stamp)
+    for v in "$@"; do
+      bash "$0" py "${O#gpurun_out/}/c2_$v" tools/clock_stamp.py --lib "_abl/libebert_$v.so" \
+        --n 100000 --b 1024 --d 768 --img bf16 --z 2.73 --cscale --secs 1.5 || exit 1
+      bash "$0" py "${O#gpurun_out/}/c3_$v" tools/clock_stamp.py --lib "_abl/libebert_$v.so" \
+        --secs 1.5 || exit 1
+    done
+    ;;
+  recipe)
+    set -e
+    G="bash $0"
+    N=${O#gpurun_out/}
+    case $N in
+      # round 4 (profiles/r4/README.md names each run's output directory)
+      r4_walk)     $G suite r4w; $G epi r4w_epi epi_prev epi; $G ab r4w _abl/libebert_prev.so C3,C2 ;;
+      r4_evfence)  $G suite r4v; $G ab r4v _abl/libebert_prev.so C2,C3
+                   $G trace r4v_trace python3 bench.py --config C2 --steps 10 --warmup 1 --no-cpu-baseline ;;
+      r4_f2key)    $G suite r4k2; $G ab r4k2 _abl/libebert_prev.so C3,C2
+                   $G bench r4k2_c2_b512 C2 --steps 50 --no-cpu-baseline --b 512
+                   $G bench r4k2_c2_b2048 C2 --steps 50 --no-cpu-baseline --b 2048 ;;
+      r4_halfblock) $G suite r4b; $G epi r4b_epi epi_bycol epi; $G ab r4b _abl/libebert_bycol.so C2,C3 ;;
+      r4_halfcol)  $G suite r4h2; $G epi r4h2_epi epi_whole epi; $G ab r4h2 _abl/libebert_whole.so C2,C3 ;;
+      r4_hitpath)  $G stamp r4h stamp stamp_stageonly stamp_hitnone stamp ;;
+      r4_inplace)  $G suite r4i; $G epi r4i_epi epi_staged epi; $G ab r4i _abl/libebert_staged.so C2,C3 ;;
+      r4_mred|r4_mslot|r4_rorder)
+                   $G suite "$N"; $G ab "$N" _abl/libebert_prev.so C2,C3 ;;
+      r4_r4t)      $G suite r4t; $G ab r4t _abl/libebert_head.so C2,C3; $G ab r4t_ldsq EBT_RESCORE_REG=0 C2
+                   $G ab r4t_nr1 _abl/libebert_nr1.so C3 1
+                   $G bench r4t_c2_streams2 C2 --steps 50 --no-cpu-baseline --streams 2
+                   $G stamp r4t_stamp stamp ;;
+      r4_sample)   $G ab r4s_d40 _abl/libebert_div40.so C3,C4; $G ab r4s_d30 _abl/libebert_div30.so C3 ;;
+      r4_stage)    $G suite r4g; $G epi r4g_epi epi_old epi; $G ab r4g _abl/libebert_head.so C2,C3 ;;
+      r4_stores)   $G stamp r4s stamp stamp_nohit stamp_nocnt stamp_none ;;
+      r4_final)    $G suite r4f; $G bench r4f C3 --steps 20; $G bench r4f C2 --steps 50
+                   $G prof r4f_prof C3 5
+                   $G bench r4f C4 --steps 5 --warmup 1 --parity 32
+                   $G bench r4f C5 --steps 3 --warmup 1 --parity 32 ;;
+      r4_prof_c45) $G prof r4p_c4 C4 3; $G prof r4p_c5 C5 2 ;;
+      *) echo "unknown recipe $N" >&2; exit 2 ;;
+    esac
+    ;;
   *)
-    echo "usage: tools/gpu.sh suite|tests|bench|prof|py|trace|pmc OUT ..." >&2
+    echo "usage: tools/gpu.sh suite|tests|bench|prof|py|trace|pmc|ab|epi|stamp|recipe OUT ..." >&2
     exit 2
     ;;
 esac
