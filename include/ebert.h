@@ -205,6 +205,11 @@ int ebt_merge_hits(float* fv, int64_t* fi, int64_t B, int32_t kprime, int32_t k,
                    const uint64_t* cand, int64_t ld_cand, int32_t slots, const uint8_t* counts,
                    int64_t ld_counts, int64_t n_groups, int64_t row_offset,
                    const int64_t* excl_off, const int64_t* excl_rows, int32_t* ovf, void* stream);
+/* Groups one block merge (k' > 512) indexes at once: its LDS holds the list + hit entries and a
+ * u16 position per group; ebt_merge_hits merges more groups in consecutive parts of this many
+ * (rounded down to 16). Host call, no device work after the first (reads the kernel's static
+ * LDS size). */
+int64_t ebt_merge_block_max_groups(int32_t kprime);
 
 /* Exclusion CSR order: the search entry points binary-search each exclusion segment and take
  * it sorted ascending. ebt_sort_exclusions sorts every segment of a caller's CSR on the device:

@@ -568,6 +568,10 @@ int ebt_screen_scores(const void* qimg, int64_t B_pad, const void* cimg, int64_t
 
 int64_t ebt_filter_group_rows(int64_t B_pad) { return filter_group_rows(B_pad); }
 
+int64_t ebt_merge_block_max_groups(int32_t kprime) {
+  return kprime < 1 || kprime > 4096 ? -1 : merge_block_max_groups(kprime);
+}
+
 int ebt_screen_filter(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
                       int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
                       const float* cscale, const float* thr, uint64_t* cand, int64_t ld_cand,

@@ -220,11 +220,18 @@ def check_partitioned(gv, gi, ref_v, ref_r, k, kp):
     (200, 200, 500, 300, False), (600, 100, 300, 50, True), (40, 40, 30, 7, True),
     # C5's k' with more groups than one block merge's LDS indexes (16383 at k' = 1256): merged
     # in parts (select_topk.hip merge_segment)
-    (1256, 1000, 3000, 20000, False), (1256, 1000, 3000, 40000, True)])
+    (1256, 1000, 3000, 20000, False), (1256, 1000, 3000, 40000, True),
+    # exactly one block merge's group limit at C5's k', and one group more (the first group of
+    # a second part): the boundary of the round-4 r4c fault (block merge)
+    (1256, 1000, 3000, "max", False), (1256, 1000, 3000, "max+1", True)])
 def test_merge_hits_vs_numpy(cuda_device, kp, k, hits, groups, shuffle):
     """ebt_merge_hits: the k' best of (partitioned list + slot hits), exclusions dropped,
     partitioned at k -- ties included -- against numpy on the same composites."""
     ebt, L = _ebt()
+    if isinstance(groups, str):
+        gmax = int(L.load().ebt_merge_block_max_groups(kp))
+        assert gmax > 1000
+        groups = gmax + (1 if groups == "max+1" else 0)
     rng = np.random.default_rng(kp + hits + k)
     B, slots = 9, 16
     vals = np.round(rng.standard_normal((B, kp)) * 8) / 8          # ties
