@@ -208,7 +208,9 @@ struct Timer {
   }
 };
 
-// The row counter the rescore adds to, when counting is on and the rescore stage is recorded
+// 64 row counters 128 bytes apart (the rescore's workgroup b adds to counter b % 64)
+constexpr size_t TIMER_ROW_BYTES = 64 * 128;
+// The row counters the rescore adds to, when counting is on and the rescore stage is recorded
 static unsigned long long* timer_rows(void* timer) {
   Timer* t = (Timer*)timer;
   if (!t || !t->d_rows || !((t->mask >> EBT_STAGE_RESCORE) & 1u)) return nullptr;
@@ -1143,11 +1145,7 @@ int ebt_timer_reset(void* timer) {
   t->recs.clear();
   t->open.clear();
   t->used = 0;
-  if (t->d_rows) {
-    const unsigned long long zero = 0;
-    return hip_check(hipMemcpy(t->d_rows, &zero, sizeof(zero), hipMemcpyHostToDevice),
-                     "hipMemcpy");
-  }
+  if (t->d_rows) return hip_check(hipMemset(t->d_rows, 0, TIMER_ROW_BYTES), "hipMemset");
   return EBT_OK;
 }
 
@@ -1161,11 +1159,10 @@ int ebt_timer_count_rows(void* timer, int on) {
     return EBT_OK;
   }
   if (t->d_rows) return EBT_OK;
-  int rc = hip_check(hipMalloc((void**)&t->d_rows, sizeof(unsigned long long)), "hipMalloc");
+  int rc = hip_check(hipMalloc((void**)&t->d_rows, TIMER_ROW_BYTES), "hipMalloc");
   if (rc) return rc;
   (void)hipGetDevice(&t->rows_dev);
-  const unsigned long long zero = 0;
-  return hip_check(hipMemcpy(t->d_rows, &zero, sizeof(zero), hipMemcpyHostToDevice), "hipMemcpy");
+  return hip_check(hipMemset(t->d_rows, 0, TIMER_ROW_BYTES), "hipMemset");
 }
 
 int ebt_timer_rows(void* timer, int64_t* rows) {
@@ -1174,11 +1171,13 @@ int ebt_timer_rows(void* timer, int64_t* rows) {
   std::lock_guard<std::mutex> g(t->mu);
   *rows = 0;
   if (!t->d_rows) return EBT_OK;
-  unsigned long long v = 0;
+  unsigned long long v[TIMER_ROW_BYTES / 8];
   // hipMemcpy waits for the work before it on the null stream; the caller synchronises the
   // launch streams first (as for ebt_timer_query)
-  int rc = hip_check(hipMemcpy(&v, t->d_rows, sizeof(v), hipMemcpyDeviceToHost), "hipMemcpy");
-  *rows = (int64_t)v;
+  int rc = hip_check(hipMemcpy(v, t->d_rows, TIMER_ROW_BYTES, hipMemcpyDeviceToHost), "hipMemcpy");
+  int64_t tot = 0;
+  for (int i = 0; i < 64; ++i) tot += (int64_t)v[i * 16];
+  *rows = tot;
   return rc;
 }
 

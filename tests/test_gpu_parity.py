@@ -1113,3 +1113,34 @@ def test_liked_prep_vector_form_bitwise(cuda_device, dt, d):
     assert torch.equal(qv.q64, qs.q64)
     assert torch.equal(qv.qimg.view(torch.int16), qs.qimg.view(torch.int16))
     assert torch.equal(qv.eps, qs.eps)
+
+
+def test_rescore_row_count(cuda_device):
+    """bench.py's roofline_topk counts the rows the rescore gathers inside the kernel
+    (ebt_timer_count_rows): per query at least the k rows of pass A, at most the k' candidates,
+    zero when counting is off, and the answer is the same with counting on."""
+    import robot_ebert_amd as ebt
+    from robot_ebert_amd.search import plan
+    dev = cuda_device
+    c = torch.from_numpy(gaussian(31, 20000, 256, "f32").astype(np.float32)).to(dev)
+    q = torch.from_numpy(gaussian(32, 512, 256, "f32").astype(np.float32)).to(dev)
+    cat = ebt.Catalog(c)
+    k = 50
+    kp = plan(cat, 512, k)["kprime"]
+    t = ebt.Timer()
+    s0, r0 = ebt.score_topk(cat, k, queries=q, timer=t)
+    torch.cuda.synchronize(dev)
+    assert t.rows() == 0
+    t.count_rows(True)
+    t.reset()
+    s1, r1 = ebt.score_topk(cat, k, queries=q, timer=t)
+    torch.cuda.synchronize(dev)
+    rows = t.rows()
+    assert 512 * k <= rows <= 512 * kp, (rows, kp)
+    assert torch.equal(r0, r1) and torch.equal(s0, s1)
+    t.only("gemm")                      # the rescore stage not recorded: nothing counted
+    t.reset()
+    ebt.score_topk(cat, k, queries=q, timer=t)
+    torch.cuda.synchronize(dev)
+    assert t.rows() == 0
+    t.count_rows(False)

@@ -175,3 +175,20 @@ def test_c5_batch_and_k_eight_ranks(cuda_device, path):
         assert default_kprime(shard, cfg["k"]) > MERGE_WAVE_KMAX
     # the C path with one batch (8 ranks x a 16384-query workspace of ~8 GB each)
     _sharded_at_scale(cuda_device, cfg, 32, check_plan=plan, path=path, slots=1)
+
+
+def test_c5_batch_and_k_eight_ranks_capi_two_slots(cuda_device):
+    """The C ABI's batches-in-flight mode at C5's batch and k: two slots
+    (batch 0 alone, then batches 0 and 1 submitted before either finishes) on 8 thread ranks of
+    250K x 1536 f16 each -- the 1M-row shards of the test above need ~23 GiB of workspace per
+    slot and rank, more than one GPU holds for 8 ranks x 2 slots."""
+    import bench
+    import robot_ebert_amd as ebt
+    from robot_ebert_amd.search import MERGE_WAVE_KMAX, default_kprime
+    cfg = dict(bench.CONFIGS["C5"], n=8 * 250_000)
+
+    def plan(n, B):
+        shard = ebt.Catalog(torch.zeros((256, cfg["d"]), dtype=torch.float16,
+                                        device=cuda_device))
+        assert default_kprime(shard, cfg["k"]) > MERGE_WAVE_KMAX   # k' = 1256: block merges
+    _sharded_at_scale(cuda_device, cfg, 16, check_plan=plan, path="capi", slots=2)
