@@ -86,24 +86,30 @@ def movies(tmdb_ids):
                   popularity=1.0, vote_average=0.0, vote_count=0) for t in sorted(tmdb_ids)]
 
 
-def drive(fn, uids, threads, seconds):
-    """`threads` threads calling fn(uid) in a loop for `seconds`; (requests, elapsed s, latencies)."""
+def drive(fn, uids, threads, seconds, cpu=None):
+    """`threads` threads calling fn(uid) in a loop for `seconds`; (requests, elapsed s, latencies).
+    cpu (a list): gets the request threads' CPU seconds (time.thread_time of each) appended."""
     lat = [[] for _ in range(threads)]
+    tcpu = [0.0] * threads
     stop = time.monotonic() + seconds
     start = threading.Barrier(threads)
 
     def worker(t):
         rng = np.random.default_rng(t + 1000 * os.getpid())
         start.wait()
+        c0 = time.thread_time()
         while time.monotonic() < stop:
             uid = uids[int(rng.integers(len(uids)))]
             t0 = time.perf_counter()
             fn(uid)
             lat[t].append(time.perf_counter() - t0)
+        tcpu[t] = time.thread_time() - c0
     t0 = time.perf_counter()
     with cf.ThreadPoolExecutor(threads) as ex:
         list(ex.map(worker, range(threads)))
     el = time.perf_counter() - t0
+    if cpu is not None:
+        cpu.append(sum(tcpu))
     flat = np.concatenate([np.asarray(x) for x in lat])
     return len(flat), el, flat
 
@@ -121,12 +127,11 @@ def thread_cpu():
 
 
 def cpu_by_role(before, after, names):
-    """CPU seconds per thread role over a run: the batcher's dispatcher / completion threads by
-    name, every other thread (request threads, the main thread) as 'request+main'."""
+    """CPU seconds of the named long-lived threads (the batcher's dispatcher / completion
+    threads) over a run (the request threads are measured by drive itself)."""
     out = {}
-    for tid, v in after.items():
-        role = names.get(tid, "request+main")
-        out[role] = out.get(role, 0.0) + v - before.get(tid, 0.0)
+    for tid, role in names.items():
+        out[role] = out.get(role, 0.0) + after.get(tid, 0.0) - before.get(tid, 0.0)
     return {k: round(v, 3) for k, v in out.items()}
 
 
@@ -267,8 +272,11 @@ def main():
                 lats.append(time.perf_counter() - t1)
                 m += 1
             out["unbatched_route"] = summary(m, time.perf_counter() - t0, np.asarray(lats))
-            n, el, lat = drive(lambda uid: lib.get_user_recs(uid, k), uids, a.threads, a.seconds)
-            out[f"unbatched_route_{a.threads}_threads"] = summary(n, el, lat)
+            req_cpu = []
+            n, el, lat = drive(lambda uid: lib.get_user_recs(uid, k), uids, a.threads, a.seconds,
+                               cpu=req_cpu)
+            out[f"unbatched_route_{a.threads}_threads"] = dict(
+                summary(n, el, lat), cpu_ms_per_request=round(1e3 * req_cpu[0] / max(n, 1), 3))
             print(f"unbatched: {out[f'unbatched_route_{a.threads}_threads']}", file=sys.stderr,
                   flush=True)
         for mode in ("scoring", "route"):
@@ -287,8 +295,10 @@ def main():
             if b._completer is not None:
                 names[b._completer.native_id] = "batcher completion"
             c0 = thread_cpu()
-            n, el, lat = drive(fn, uids, a.threads, a.seconds)
+            req_cpu = []
+            n, el, lat = drive(fn, uids, a.threads, a.seconds, cpu=req_cpu)
             cpu = cpu_by_role(c0, thread_cpu(), names)
+            cpu["request threads"] = round(req_cpu[0], 3)
             b.close()
             st = b.stats()
             out[f"batched_{mode}"] = dict(
