@@ -678,7 +678,9 @@ def main() -> None:
     head = pl["head_rows"]
     # the speculative screen filters every row (its sample tiles too); the progressive one the
     # rows after its head
-    tail = (n_local if pl.get("spec") else n_local - head) if pl["fused"] else 0
+    # (less the speculative screen's lead tiles, whose hits come from the sample's own scores)
+    spec = pl.get("spec") or {}
+    tail = (n_local - 256 * spec.get("lead", 0) if spec else n_local - head) if pl["fused"] else 0
     # dominant kernel: the fused screening GEMM over the tail rows (else the score-writing GEMM)
     if pl["fused"]:
         dom_name = "screen_gemm_qp2_kernel<filter>"

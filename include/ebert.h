@@ -282,6 +282,17 @@ int ebt_cosine_topk_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprim
 int ebt_cosine_topk_spec_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
                               int flags, int64_t* sample_tiles, int64_t* tile_stride,
                               int32_t* rank, double* hits);
+/* The speculative screen's lead (0.3.0): its sample's first `lead` tiles are the catalog's first
+ * tiles (the rest of the sample strided after them: tiles 0 .. lead-1, lead, lead + s, ...), their
+ * scores are kept and their hits taken at theta, and the filter GEMM covers rows [256 lead, n)
+ * only -- lead is chosen so that those are whole rounds of the persistent grid (one 256 x 256
+ * output tile per CU and round); every segment but the last is whole rounds too. Returns the
+ * lead in tiles (0: none; -1: bad arguments). ebt_spec_lead(on) switches it on (1, default) or
+ * off (0) for the process (on < 0: query); returns the previous setting. Results are the same
+ * either way: the lead's hits are the filter's own, value for value. */
+int64_t ebt_cosine_topk_spec_lead(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
+                                  int flags);
+int ebt_spec_lead(int on);
 /* Workspace bytes needed by ebt_cosine_topk_prepared for these sizes. */
 size_t ebt_cosine_topk_workspace(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
                                  int64_t chunk_rows, int flags);

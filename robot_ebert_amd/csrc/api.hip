@@ -1,5 +1,6 @@
 // extern "C" entry points of libebert.so (declared in include/ebert.h), the pipeline
 // orchestrator ebt_cosine_topk_prepared, the per-stage hipEvent timer and error reporting.
+#include <atomic>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -136,7 +137,11 @@ int pool_kth(const float*, int64_t, int64_t, int64_t, int, int, float*, hipStrea
 int spec_given_init(const float*, int64_t, int64_t, float*, float*, int64_t*, int, int*,
                     hipStream_t);
 int screen_gemm_pool(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
-                     const float*, const float*, int64_t, float*, int64_t, hipStream_t);
+                     const float*, const float*, int64_t, float*, int64_t, hipStream_t,
+                     int64_t lead = 0, float* lead_scores = nullptr, int64_t ld_lead = 0);
+int lead_hits(const float*, int64_t, int64_t, int64_t, const float*, uint64_t*, int64_t, int,
+              uint8_t*, int64_t, int*, hipStream_t);
+int64_t gemm_cus();
 int merge_segment(float*, int64_t*, int64_t, int, const uint64_t*, int64_t, int, const uint8_t*,
                   int64_t, int64_t, int64_t, const int64_t*, const int64_t*, int*, hipStream_t,
                   double expect_hits = 0.0);
@@ -256,8 +261,13 @@ struct WsLayout {
   int64_t spec_tiles, spec_stride;
   int spec_j;
   double spec_hits;
+  // the sample's LEAD: its first spec_lead tiles are the catalog's first tiles, their scores are
+  // kept (ld_lead floats per query at off_lead) and their hits extracted once theta_spec is
+  // known, so the filter GEMM starts after them and covers whole rounds of the persistent grid
+  // (spec_lead_tiles); round_rows = the rows of one such round (0: no rounding)
+  int64_t spec_lead, ld_lead, round_rows;
   size_t off_s, off_segv, off_segi, off_chv, off_chi, off_fv, off_fi, off_cand, off_counts,
-      off_thr, off_ovf, off_eps, off_tspec, bytes;
+      off_thr, off_ovf, off_eps, off_tspec, off_lead, bytes;
 };
 
 constexpr int SPEC_KPRIME_MAX = 2048;
@@ -347,6 +357,34 @@ static bool spec_params(int64_t B_pad, int64_t n_rows, int32_t kprime, int64_t* 
 
 static size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 
+// ebt_spec_lead: 1 = the speculative screen's lead tiles (default; EBT_SPEC_LEAD=0 in the
+// environment starts the process without them)
+static std::atomic<int>& spec_lead_flag() {
+  static std::atomic<int> f([] {
+    const char* v = getenv("EBT_SPEC_LEAD");
+    return v ? (atoi(v) != 0 ? 1 : 0) : 1;
+  }());
+  return f;
+}
+
+// The persistent screening GEMM runs one 256 x 256 output tile per CU and round: a launch of T
+// catalog tiles x Q query tiles takes ceil(T Q / CUs) rounds, the last one partly idle. Catalog
+// tiles per whole round (CUs / Q; 0 when Q does not divide the CU count), and the lead: the
+// catalog tiles the sample takes over from the filter so that the rest, n_tiles - lead, is a
+// whole number of rounds (C2: 391 tiles x 4 query tiles on 256 CUs -> lead 7, the filter's 7th
+// round of 28 tiles disappears; C3: 3907 x 16 -> lead 3).
+static int64_t round_tiles(int64_t B_pad) {
+  const int64_t q = B_pad / 256, cus = gemm_cus();
+  return (q > 0 && cus % q == 0) ? cus / q : 0;
+}
+static int64_t spec_lead_tiles(int64_t B_pad, int64_t n_rows, int64_t sample_tiles) {
+  const int64_t rt = round_tiles(B_pad);
+  if (rt <= 1 || !spec_lead_flag().load(std::memory_order_relaxed)) return 0;
+  const int64_t lead = ceil_div(n_rows, 256) % rt;
+  // a lead of at most half the sample (its strided part keeps the spread), and full tiles only
+  return (lead <= sample_tiles / 2 && lead * 256 <= n_rows - 256) ? lead : 0;
+}
+
 static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
                           int64_t chunk_rows, int flags) {
   WsLayout L{};
@@ -396,6 +434,14 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
     // the speculative screen may use 8 slots per group: counts for ld_cand / 8 groups
     L.ld_counts = (L.ld_cand / 8 + 15) / 16 * 16;
   }
+  if (L.spec && !(flags & EBT_FLAG_THETA)) {
+    L.spec_lead = spec_lead_tiles(B_pad, n_rows, L.spec_tiles);
+    L.ld_lead = L.spec_lead * 256;
+  }
+  if (L.spec) {
+    const int64_t rt = round_tiles(B_pad);
+    L.round_rows = rt > 1 ? rt * 256 : 0;
+  }
   L.chunk = chunk_rows < L.head ? chunk_rows : L.head;
   if (L.spec) L.chunk = L.head / 64;  // the sample's pooled maxima (4 per tile)
   if (L.chunk < 1) L.chunk = 1;
@@ -443,6 +489,8 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
     L.off_tspec = o;
     o = align_up(o + (size_t)B_pad * 4);
   }
+  L.off_lead = o;
+  if (L.spec_lead) o = align_up(o + (size_t)B_pad * L.ld_lead * 4);
   L.bytes = o;
   return L;
 }
@@ -680,6 +728,18 @@ int ebt_cosine_topk_spec_plan(int64_t B, int64_t B_pad, int64_t n_rows, int32_t 
   return EBT_OK;
 }
 
+int64_t ebt_cosine_topk_spec_lead(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
+                                  int flags) {
+  if (B < 0 || B_pad < B || n_rows < 1 || kprime < 1) return -1;
+  const WsLayout L = ws_layout(B, B_pad, n_rows, kprime, 1024, flags);
+  return L.spec ? L.spec_lead : 0;
+}
+
+int ebt_spec_lead(int on) {
+  if (on < 0) return spec_lead_flag().load();
+  return spec_lead_flag().exchange(on != 0 ? 1 : 0);
+}
+
 }  // extern "C"
 
 namespace ebt {
@@ -772,7 +832,8 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
     {
       StageScope s(timer, EBT_STAGE_GEMM, st);
       rc = screen_gemm_pool(a.qimg, B_pad, a.cimg, m, a.d_pad, a.ld_img, a.img_dtype, a.qscale,
-                            a.cscale, 256 * L.spec_stride, pooled, L.ld_s, st);
+                            a.cscale, 256 * L.spec_stride, pooled, L.ld_s, st, L.spec_lead,
+                            (float*)(ws + L.off_lead), L.ld_lead);
     }
     if (rc) return rc;
     {
@@ -820,24 +881,49 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
     f_spread = x / (double)L.spec_j;
     f_spread = f_spread < 2.5 ? 2.5 : f_spread;
   }
-  int64_t r0 = 0;
-  bool verified = false;
+  // the lead tiles' hits at theta_spec, into the first segment's first groups (the filter
+  // then starts after them: its groups follow)
+  const int64_t lead = given ? 0 : L.spec_lead;
+  if (lead > 0) {
+    if (lead * slots > L.ld_cand || lead > L.ld_counts || lead * L.group_rows != 256 * lead) {
+      set_error("run_screen_spec: the lead does not fit the hit slots");
+      return EBT_EINVAL;
+    }
+    StageScope s(timer, EBT_STAGE_SELECT, st);
+    rc = lead_hits((const float*)(ws + L.off_lead), L.ld_lead, lead, B_pad, tspec, cand,
+                   L.ld_cand, slots, counts, L.ld_counts, ovf, st);
+    if (rc) return rc;
+  }
+  int64_t r0 = 256 * lead;
+  bool first = true, verified = false;
   while (r0 < n_rows) {
     // expected hits <= 1 / f_spread of the merge's room beside the list. Hits per row: at
     // theta_spec H / n; after r0 rows the raised threshold (the list's k-th - 2 eps) keeps at
     // most ~k' / r0 of the rows. A remainder of less than half a segment joins the last one.
+    // The first segment also merges the lead's groups: its cap is that much smaller.
+    const int64_t g0 = first ? lead : 0;  // groups of the lead in front of this segment's
+    const int64_t cap_rows = seg_cap - g0 * L.group_rows;
     const double room = (cap - kprime) / f_spread;
     double rate = spec_hits / (double)n_rows;
-    if (r0 > 0 && (double)kprime / (double)r0 < rate) rate = (double)kprime / (double)r0;
+    if (!first && (double)kprime / (double)r0 < rate) rate = (double)kprime / (double)r0;
     int64_t seg = (int64_t)(room / (rate > 1e-12 ? rate : 1e-12));
     seg = (seg + 255) / 256 * 256;
+    // whole rounds of the persistent grid (every segment but a remainder): no partly idle
+    // last round per launch
+    if (L.round_rows > 0 && seg >= L.round_rows) seg = seg / L.round_rows * L.round_rows;
     seg = seg < 256 ? 256 : seg;
-    seg = seg < seg_cap ? seg : seg_cap;
-    if (r0 > 0 && n_rows - r0 - seg < seg / 2) seg = n_rows - r0;
-    if (seg > seg_cap) seg = seg_cap;
+    const int64_t cap_r = L.round_rows > 0 && cap_rows >= L.round_rows
+                              ? cap_rows / L.round_rows * L.round_rows : cap_rows;
+    seg = seg < cap_r ? seg : cap_r;
+    if (!first && n_rows - r0 - seg < seg / 2) seg = n_rows - r0;
+    if (seg > cap_rows) seg = cap_rows;
     if (seg > n_rows - r0) seg = n_rows - r0;
+    if (seg < 1) {
+      set_error("run_screen_spec: no room for a segment");
+      return EBT_EINVAL;
+    }
     const float* t = tspec;
-    if (r0 > 0) {
+    if (!first) {
       rc = spec_threshold(fv, kprime, B, B_pad, k, a.eps, tspec, thr, ovf, 0, st);
       if (rc) return rc;
       t = thr;
@@ -846,27 +932,28 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
       StageScope s(timer, EBT_STAGE_GEMM_FILTER, st);
       rc = screen_gemm_filter(a.qimg, B_pad, (const char*)a.cimg + r0 * a.ld_img * 2, seg,
                               a.d_pad, a.ld_img, a.img_dtype, a.qscale,
-                              a.cscale ? a.cscale + r0 : nullptr, t, cand, L.ld_cand, slots,
-                              counts, L.ld_counts, ovf, r0, st);
+                              a.cscale ? a.cscale + r0 : nullptr, t, cand + g0 * slots,
+                              L.ld_cand, slots, counts + g0, L.ld_counts, ovf, r0, st);
     }
     if (rc) return rc;
     // the last wave merge also runs the final VERIFY of theta_spec (no separate launch)
     const bool fuse_verify = wave && !given && r0 + seg == n_rows;
     verified |= fuse_verify;
+    const int64_t groups = g0 + ceil_div(seg, L.group_rows);
     {
       StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
       if (wave)
         rc = merge_segment_wave(fv, fi, B, kprime, k, cand, L.ld_cand, slots, counts,
-                                L.ld_counts, ceil_div(seg, L.group_rows), a.row_offset,
-                                a.excl_off, a.excl_rows, ovf, st,
-                                fuse_verify ? a.eps : nullptr, fuse_verify ? tspec : nullptr);
+                                L.ld_counts, groups, a.row_offset, a.excl_off, a.excl_rows, ovf,
+                                st, fuse_verify ? a.eps : nullptr, fuse_verify ? tspec : nullptr);
       else  // sorted lists (the block merge sorts the union)
         rc = merge_segment(fv, fi, B, kprime, cand, L.ld_cand, slots, counts, L.ld_counts,
-                           ceil_div(seg, L.group_rows), a.row_offset, a.excl_off, a.excl_rows,
-                           ovf, st, rate * (double)seg);
+                           groups, a.row_offset, a.excl_off, a.excl_rows, ovf, st,
+                           rate * (double)(seg + g0 * L.group_rows));
     }
     if (rc) return rc;
     r0 += seg;
+    first = false;
   }
   // a caller's threshold is verified by the caller against the catalog-wide floor (the local
   // list may hold fewer than k rows: most of the global top k live on other shards)

@@ -519,6 +519,11 @@ struct QpArgs {
   int64_t cstride;
   int n_qtiles, n_ctiles, ktiles;
   int pg_log2;  // log2(QP_GROUP_C * n_qtiles) when that is a power of two, else -1
+  // pool mode: the sample's first `lead` tiles are the catalog's first tiles (contiguous), the
+  // rest strided from there; the lead tiles' scores are also stored (S2, row pitch ld_s2)
+  int lead;
+  float* S2;
+  int64_t ld_s2;
   EpiArgs e;
 };
 typedef const __attribute__((address_space(4))) QpArgs* QpArgsK;
@@ -603,8 +608,12 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
     }
     T.c0 = T.ct * QP_TILE;
     // catalog row of the tile's first row: c0, or ct * cstride for a strided sample of full
-    // tiles (store / pool mode; n_rows then counts the sample's rows and the scores stay dense)
-    T.c0s = T.ct * A->cstride;
+    // tiles (store / pool mode; n_rows then counts the sample's rows and the scores stay dense);
+    // a pool-mode sample with a lead: tiles [0, lead) contiguous, the rest strided after them
+    if constexpr (EPI == EPI_POOL)
+      T.c0s = T.ct < A->lead ? T.c0 : (int64_t)A->lead * QP_TILE + (T.ct - A->lead) * A->cstride;
+    else
+      T.c0s = T.ct * A->cstride;
     T.q0 = (int64_t)qt * QP_TILE;
     return T;
   };
@@ -1219,7 +1228,10 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
   };
   // pool mode: max over the 64 rows (ah, wa) of each query: 4 accumulators x 4 values in the
   // lane, then the 4 lanes of the same fr_ (lane ^ 16, ^ 32); rows past n_rows are skipped
+  // (a lead tile, T.ct < lead: its full tile of scores is also stored, the filter's values, for
+  // ebt's lead-hit extraction once the threshold is known -- the filter then skips those rows)
   auto pool_quadrant = [&](const QpTile& T, const f32x4_t (&acc)[4][2], int ah, int bh) {
+    const bool lead_tile = T.ct < A->lead;  // uniform
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
       const int ql = bh * 128 + wb * 32 + jj * 16 + fr_;
@@ -1234,6 +1246,8 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (T.c0 + il + r < n_rows) mx = fmaxf(mx, v[r]);
+        if (lead_tile)
+          *(float4*)(A->S2 + (T.q0 + ql) * A->ld_s2 + T.c0 + il) = make_float4(v[0], v[1], v[2], v[3]);
       }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
@@ -1343,11 +1357,15 @@ static int64_t n_cus() {
   return v;
 }
 
+// The persistent grid's workgroups (one per CU) -- the planner's round size (api.hip)
+int64_t gemm_cus() { return n_cus(); }
+
 template <int EPI>
 static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
                        int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
                        const float* cscale, const EpiArgs& e, hipStream_t stream,
-                       int64_t cstride = 0) {
+                       int64_t cstride = 0, int lead = 0, float* S2 = nullptr,
+                       int64_t ld_s2 = 0) {
   const bool big = B_pad % QP_TILE == 0;
   if (cstride == 0) cstride = big ? QP_TILE : GBM;
   const int n_qtiles = (int)(B_pad / (big ? QP_TILE : GBN));
@@ -1390,6 +1408,9 @@ static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_
     a.ktiles = ktiles;
     const int per_group = QP_GROUP_C * n_qtiles;
     a.pg_log2 = (per_group & (per_group - 1)) == 0 ? __builtin_ctz((unsigned)per_group) : -1;
+    a.lead = lead;
+    a.S2 = S2;
+    a.ld_s2 = ld_s2;
     a.e = e;
     hipLaunchKernelGGL(k, grid, block, QP_LDS_TOTAL, stream, a);
     return launch_check("screen_gemm_qp2_kernel");
@@ -1455,15 +1476,21 @@ int screen_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_row
 
 // The speculative screen's sample: P full 256-row tiles, cstride rows apart (P = n_rows / 256),
 // -> pooled[q][g] = max score of query q over the sample's 64-row subgroup g (4P per query).
+// With lead > 0 the sample's first `lead` tiles are the catalog's first lead tiles and the rest
+// start there (tile p >= lead at row lead * 256 + (p - lead) * cstride), and the lead tiles' f32
+// scores -- the values the filter epilogue would test -- go to lead_scores[q][0, 256 lead)
+// (row pitch ld_lead).
 int screen_gemm_pool(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
                      int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
                      const float* cscale, int64_t cstride, float* pooled, int64_t ld_pooled,
-                     hipStream_t stream) {
+                     hipStream_t stream, int64_t lead, float* lead_scores, int64_t ld_lead) {
   int rc = check_gemm_args("screen_gemm_pool", qimg, B_pad, cimg, n_rows, d_pad, ld_img,
                            img_dtype, qscale, cscale);
   if (rc) return rc;
   if (!pooled || B_pad % QP_TILE != 0 || n_rows % QP_TILE != 0 || cstride < QP_TILE ||
-      ld_pooled < n_rows / 64) {
+      ld_pooled < n_rows / 64 || lead < 0 || lead > n_rows / QP_TILE ||
+      (lead > 0 && (!lead_scores || ld_lead < lead * QP_TILE || ld_lead % 4 != 0 ||
+                    ((uintptr_t)lead_scores & 15)))) {
     set_error("screen_gemm_pool: bad arguments");
     return EBT_EINVAL;
   }
@@ -1471,7 +1498,54 @@ int screen_gemm_pool(const void* qimg, int64_t B_pad, const void* cimg, int64_t 
   e.S = pooled;
   e.ld_s = ld_pooled;
   return launch_gemm<EPI_POOL>(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale,
-                               cscale, e, stream, cstride);
+                               cscale, e, stream, cstride, (int)lead, lead_scores, ld_lead);
+}
+
+// The lead tiles' hits once the threshold is known: exactly what the filter epilogue writes for
+// those tiles (screen_gemm_qp2_kernel<filter>) -- every score >= thr[q] as the composite
+// f2key(v) << 32 | ~row into the (query, group) slot range, the group's count (u8, saturated)
+// and the overflow flag when the count exceeds the slots. One workgroup per (lead tile, query).
+__global__ __launch_bounds__(256) void lead_hits_kernel(
+    const float* __restrict__ S2, int64_t ld_s2, const float* __restrict__ thr,
+    uint64_t* __restrict__ cand, int64_t ld_cand, int slots, uint8_t* __restrict__ counts,
+    int64_t ld_counts, int* __restrict__ ovf) {
+  __shared__ uint32_t wcnt[4];
+  const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t q = blockIdx.y;
+  const float v = S2[q * ld_s2 + (int64_t)p * QP_TILE + tid];
+  const bool hit = v >= thr[q];
+  const uint64_t bm = __ballot(hit);
+  if (lane == 0) wcnt[wave] = (uint32_t)__popcll(bm);
+  __syncthreads();
+  uint32_t base = 0;
+  for (int w = 0; w < wave; ++w) base += wcnt[w];
+  const uint32_t total = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+  if (hit) {
+    const uint32_t pp = base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+    if (pp < (uint32_t)slots) {
+      const uint32_t row = (uint32_t)(p * QP_TILE + tid);
+      cand[q * ld_cand + (int64_t)p * slots + pp] =
+          ((uint64_t)f2key_select(v) << 32) | (uint64_t)(~row);
+    }
+  }
+  if (tid == 0) {
+    counts[q * ld_counts + p] = (uint8_t)(total < 255u ? total : 255u);
+    if (total > (uint32_t)slots) ovf[q] = 1;
+  }
+}
+
+int lead_hits(const float* lead_scores, int64_t ld_lead, int64_t lead, int64_t B_pad,
+              const float* thr, uint64_t* cand, int64_t ld_cand, int slots, uint8_t* counts,
+              int64_t ld_counts, int* ovf, hipStream_t st) {
+  if (lead <= 0) return EBT_OK;
+  if (!lead_scores || !thr || !cand || !counts || !ovf || ld_lead < lead * QP_TILE ||
+      slots < 1 || ld_cand < lead * slots || ld_counts < lead || B_pad < 1 || B_pad > 65535) {
+    set_error("lead_hits: bad arguments");
+    return EBT_EINVAL;
+  }
+  hipLaunchKernelGGL(lead_hits_kernel, dim3((unsigned)lead, (unsigned)B_pad), dim3(256), 0, st,
+                     lead_scores, ld_lead, thr, cand, ld_cand, slots, counts, ld_counts, ovf);
+  return launch_check("lead_hits_kernel");
 }
 
 int64_t filter_group_rows(int64_t B_pad) { return B_pad % QP_TILE == 0 ? QP_TILE : GBM; }

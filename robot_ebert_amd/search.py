@@ -237,7 +237,10 @@ def spec_plan(B: int, n: int, kprime: int, fuse: bool = True) -> Optional[dict]:
          ctypes.byref(h))
     if t.value == 0:
         return None
-    return {"tiles": t.value, "stride": st.value, "rank": j.value, "hits": round(h.value, 1)}
+    lead = int(_lib.load().ebt_cosine_topk_spec_lead(B, pad_batch(B), n, kprime,
+                                                     0 if fuse else _lib.EBT_FLAG_NO_FUSE))
+    return {"tiles": t.value, "stride": st.value, "rank": j.value, "hits": round(h.value, 1),
+            "lead": lead}
 
 
 def run_pipeline(catalog: Catalog, qb: QueryBatch, k: int, kprime: int,

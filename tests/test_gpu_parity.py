@@ -551,9 +551,11 @@ def test_speculative_threshold_failure_reruns(cuda_device):
     sp = ebt.search.plan(cat0, B, k)["spec"]
     assert sp is not None
     rng = np.random.default_rng(33)
-    for t in range(sp["tiles"]):
+    lead = sp.get("lead", 0)
+    for t in range(sp["tiles"]):   # the sample: tiles 0 .. lead-1, then every stride-th from lead
+        row0 = 256 * (t if t < lead else lead + (t - lead) * sp["stride"])
         for r in range(4):  # 4 near-duplicates per sample tile: >> the rank j in the sample
-            c[t * sp["stride"] * 256 + 17 * r] = q[0] + 1e-3 * rng.standard_normal(d)
+            c[row0 + 17 * r] = q[0] + 1e-3 * rng.standard_normal(d)
     c = c.astype(np.float32)  # the oracle sees the values the GPU catalog holds
     cat = ebt.Catalog(_t(c, "f32", cuda_device))
     qt = _t(q, "f32", cuda_device)
@@ -1144,3 +1146,67 @@ def test_rescore_row_count(cuda_device):
     torch.cuda.synchronize(dev)
     assert t.rows() == 0
     t.count_rows(False)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_speculative_lead_equals_no_lead(cuda_device, dt):
+    """The speculative screen's lead (C2's shape class: 100K rows x 4 query tiles -> 7 lead
+    tiles whose hits come from the sample's stored scores, the filter over 6 whole rounds):
+    the same rows AND scores as without the lead and as the unfused path, bit for bit, with
+    exclusions; f32 (normalised f16 image) and native bf16 (row scales in the epilogue)."""
+    ebt, L = _ebt()
+    lib = L.load()
+    n, d, B, k = 100_000, 128, 1024, 100
+    c = gaussian(61, n, d, dt)
+    q = gaussian(62, B, d, dt)
+    rng = np.random.default_rng(63)
+    excl = [list(np.sort(rng.choice(n, 30, replace=False))) for _ in range(B)]
+    cat = ebt.Catalog(_t(c, dt, cuda_device))
+    qt = _t(q, dt, cuda_device)
+    sp = ebt.search.plan(cat, B, k)["spec"]
+    assert sp is not None and sp["lead"] > 0, sp
+    prev = lib.ebt_spec_lead(1)
+    try:
+        s1, r1 = ebt.score_topk(cat, k, queries=qt, exclude=excl)
+        lib.ebt_spec_lead(0)
+        assert ebt.search.plan(cat, B, k)["spec"]["lead"] == 0
+        s0, r0 = ebt.score_topk(cat, k, queries=qt, exclude=excl)
+    finally:
+        lib.ebt_spec_lead(prev)
+    s2, r2 = ebt.score_topk(cat, k, queries=qt, exclude=excl, fuse=False)
+    assert torch.equal(r1, r0) and torch.equal(s1, s0)
+    assert torch.equal(r1, r2)
+    torch.testing.assert_close(s1, s2, rtol=0, atol=0)
+    idx = [0, 1, 511, 1023]
+    s_ref, r_ref = R.cosine_topk(q[idx].astype(np.float64), c.astype(np.float64), k,
+                                 [excl[i] for i in idx])
+    assert_topk_equal(s1[idx], r1[idx], s_ref, r_ref)
+
+
+def test_speculative_lead_hits_equal_filter_hits(cuda_device):
+    """The lead tiles' hits (the pool GEMM's stored scores + lead_hits_kernel) are the filter
+    epilogue's own: a screen with the lead and one without give the same k' candidate list
+    (values and rows) for every query at the same theta_spec."""
+    ebt, L = _ebt()
+    from robot_ebert_amd.search import prepare_queries, run_screen
+    lib = L.load()
+    n, d, B, k = 100_000, 64, 1024, 100
+    c = gaussian(71, n, d, "f32")
+    q = gaussian(72, B, d, "f32")
+    cat = ebt.Catalog(_t(c, "f32", cuda_device))
+    qb = prepare_queries(cat, queries=_t(q, "f32", cuda_device))
+    kp = ebt.search.plan(cat, B, k)["kprime"]
+    prev = lib.ebt_spec_lead(1)
+    try:
+        assert ebt.search.plan(cat, B, k)["spec"]["lead"] > 0
+        lv1, lr1, ovf1, _ = run_screen(cat, qb, k, kp)
+        lib.ebt_spec_lead(0)
+        lv0, lr0, ovf0, _ = run_screen(cat, qb, k, kp)
+    finally:
+        lib.ebt_spec_lead(prev)
+    # the wave merge writes a partitioned list: compare as sets of (value, row) per query
+    a1 = torch.stack([lv1.view(torch.int32).to(torch.int64), lr1], -1).cpu().numpy()
+    a0 = torch.stack([lv0.view(torch.int32).to(torch.int64), lr0], -1).cpu().numpy()
+    for b in range(0, B, 37):
+        assert sorted(map(tuple, a1[b])) == sorted(map(tuple, a0[b])), b
+    assert torch.equal(ovf1, ovf0)
