@@ -560,6 +560,14 @@ __device__ __forceinline__ void epi_count(char* smem, int wave, int slot) {
 #define EPI_COUNT(sl)
 #endif
 
+#ifdef EBT_WALK_STAMP
+// Diagnostic build only (the persistent walk's schedule, tools/walk_stamp.py): lane 0 of every
+// workgroup of a filter-mode launch records (tile index L, 100 MHz real time) at the start of
+// each of its tiles and (-1, time) at exit into g_walk[(block * WALK_MAX + t) * 2 ..] (vector
+// stores; nothing else reads them). The shipped library has none of it.
+constexpr int WALK_MAX = 4096;
+__device__ unsigned long long* g_walk;
+#endif
 #ifdef EBT_CLOCK_STAMP
 // Diagnostic build only (MI355X_MICROARCH.md "DVFS give-back" item 6): lane 0 of each workgroup
 // of a filter-mode launch records the shader-clock and the 100 MHz real-time counters after the
@@ -854,7 +862,18 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
     wait_vm<8>(); /* B1(t+1) for Q1(t+1) */                                                     \
   }
 
+#ifdef EBT_WALK_STAMP
+  int walk_t = 0;
+#endif
   for (;;) {
+#ifdef EBT_WALK_STAMP
+    if (EPI == EPI_FILTER && tid == 0 && g_walk && walk_t < WALK_MAX - 1) {
+      unsigned long long* o = g_walk + ((int64_t)bid * WALK_MAX + walk_t) * 2;
+      o[0] = (unsigned long long)L;
+      o[1] = __builtin_amdgcn_s_memrealtime();
+    }
+    ++walk_t;
+#endif
     const bool last = !(L + n_x < Lend);  // uniform
     // A0(0) / B0(0) of this tile landed before the last barrier (the prologue's, or the
     // previous tile's last phase)
@@ -1306,6 +1325,14 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
     for (int i = 0; i < 8; ++i) o[i] = e[i];
   }
 #endif
+#ifdef EBT_WALK_STAMP
+  if (EPI == EPI_FILTER && tid == 0 && g_walk) {
+    const int t = walk_t < WALK_MAX - 1 ? walk_t : WALK_MAX - 1;
+    unsigned long long* o = g_walk + ((int64_t)bid * WALK_MAX + t) * 2;
+    o[0] = ~0ull;
+    o[1] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 #ifdef EBT_CLOCK_STAMP
   if (EPI == EPI_FILTER && tid == 0 && g_stamps) {
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -1322,6 +1349,11 @@ __global__ __launch_bounds__(QP_THREADS, 2) void screen_gemm_qp2_kernel(QpArgs a
 #ifdef EBT_EPI_STAMP
 extern "C" int ebt_debug_epi_stamps(unsigned long long* buf) {
   return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_epi), &buf, sizeof(buf)), "hipMemcpyToSymbol");
+}
+#endif
+#ifdef EBT_WALK_STAMP
+extern "C" int ebt_debug_walk_stamps(unsigned long long* buf) {
+  return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_walk), &buf, sizeof(buf)), "hipMemcpyToSymbol");
 }
 #endif
 #ifdef EBT_CLOCK_STAMP
