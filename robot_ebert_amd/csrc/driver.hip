@@ -1037,10 +1037,14 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
   if (S.tiles) {
     float* pool = (float*)(ws + S.off_pool);
     float* gsamp = (float*)(ws + S.off_gsamp);
-    rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)pool, (int)0xff800000u,
-                                     (size_t)L.B_pad * S.G, st), "hipMemsetD32Async");
-    if (rc) return rc;
     const int64_t own = S.tiles < c.n / 256 ? S.tiles : c.n / 256;
+    // -inf where this shard has no sample tile (a shard smaller than the sample); a full sample
+    // writes every maximum itself (one API call less per step)
+    if (own < S.tiles) {
+      rc = hip_check(hipMemsetD32Async((hipDeviceptr_t)pool, (int)0xff800000u,
+                                       (size_t)L.B_pad * S.G, st), "hipMemsetD32Async");
+      if (rc) return rc;
+    }
     if (own >= 1) {
       int64_t stride = (c.n / 256) / own;
       if (stride > 1 && stride % 2 == 0) stride -= 1;

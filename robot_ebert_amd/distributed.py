@@ -659,6 +659,18 @@ class ShardedTopk:
         if isinstance(comm, TorchGatherComm):
             for w in self.ws:
                 comm.register(w)
+        # the per-call constants of submit (host work per step: every ctypes conversion counts)
+        self._fn_submit = lib.ebt_cosine_topk_sharded_submit
+        self._fn_finish = lib.ebt_cosine_topk_sharded_finish
+        self._fn_wait = lib.ebt_cosine_topk_sharded_wait
+        self._cat_ref = ctypes.byref(catalog.cstruct)
+        self._comm_ref = ctypes.byref(self.comm)
+        self._opt_ref = ctypes.byref(self.opt)
+        self._slot_args = [(ptr(self.ws[i]), self.ws_bytes, ptr(self.out[i][0]),
+                            ptr(self.out[i][1]), ptr(self.host[i]), ctypes.byref(self.pend[i]))
+                           for i in range(slots)]
+        self._pend_refs = [ctypes.byref(p) for p in self.pend]
+        self._timer_h = timer.handle if timer is not None else None
 
     def _check(self, rc: int, what: str) -> None:
         if rc != 0:
@@ -684,23 +696,22 @@ class ShardedTopk:
         if exclude is not None:
             eo, er = exclude if isinstance(exclude, tuple) else csr_from_lists(exclude, dev)
         self.keep[slot] = (queries, lo, lr, eo, er)
-        s, r = self.out[slot]
-        rc = _lib.load().ebt_cosine_topk_sharded_submit(
-            ctypes.byref(self.catalog.cstruct), ctypes.byref(self.comm), q_ptr, q_dt, self.B, ldq,
-            ptr(lo), ptr(lr), self.k, ptr(eo), ptr(er), ctypes.byref(self.opt), ptr(self.ws[slot]),
-            self.ws_bytes, ptr(s), ptr(r), ptr(self.host[slot]), ctypes.byref(self.pend[slot]),
-            self.timer.handle if self.timer is not None else None, stream_of(dev))
-        self._check(rc, "submit")
+        ws, ws_bytes, s, r, host, pend = self._slot_args[slot]
+        rc = self._fn_submit(self._cat_ref, self._comm_ref, q_ptr, q_dt, self.B, ldq, ptr(lo),
+                             ptr(lr), self.k, ptr(eo), ptr(er), self._opt_ref, ws, ws_bytes, s, r,
+                             host, pend, self._timer_h, stream_of(dev))
+        if rc:
+            self._check(rc, "submit")
 
     def finish(self, slot: int) -> None:
-        import ctypes
-        self._check(_lib.load().ebt_cosine_topk_sharded_finish(ctypes.byref(self.pend[slot])),
-                    "finish")
+        rc = self._fn_finish(self._pend_refs[slot])
+        if rc:
+            self._check(rc, "finish")
 
     def wait(self, slot: int) -> Tuple[torch.Tensor, torch.Tensor]:
-        import ctypes
-        self._check(_lib.load().ebt_cosine_topk_sharded_wait(ctypes.byref(self.pend[slot])),
-                    "wait")
+        rc = self._fn_wait(self._pend_refs[slot])
+        if rc:
+            self._check(rc, "wait")
         self.keep[slot] = None
         return self.out[slot]
 
