@@ -1185,8 +1185,9 @@ def test_speculative_lead_equals_no_lead(cuda_device, dt):
 
 def test_speculative_lead_hits_equal_filter_hits(cuda_device):
     """The lead tiles' hits (the pool GEMM's stored scores + lead_hits_kernel) are the filter
-    epilogue's own: a screen with the lead and one without give the same k' candidate list
-    (values and rows) for every query at the same theta_spec."""
+    epilogue's own: a screen with the lead and one without give the same k best approx
+    candidates (values and rows) for every query. (Past position k the lists may differ: later
+    segments filter at the list's k-th - 2 eps, and the segments start at different rows.)"""
     ebt, L = _ebt()
     from robot_ebert_amd.search import prepare_queries, run_screen
     lib = L.load()
@@ -1207,6 +1208,6 @@ def test_speculative_lead_hits_equal_filter_hits(cuda_device):
     # the wave merge writes a partitioned list: compare as sets of (value, row) per query
     a1 = torch.stack([lv1.view(torch.int32).to(torch.int64), lr1], -1).cpu().numpy()
     a0 = torch.stack([lv0.view(torch.int32).to(torch.int64), lr0], -1).cpu().numpy()
-    for b in range(0, B, 37):
-        assert sorted(map(tuple, a1[b])) == sorted(map(tuple, a0[b])), b
-    assert torch.equal(ovf1, ovf0)
+    for b in range(0, B, 7):   # positions [0, k): the k best of the partitioned list
+        assert sorted(map(tuple, a1[b, :k])) == sorted(map(tuple, a0[b, :k])), b
+    assert torch.equal(ovf1 != 0, ovf0 != 0)
