@@ -93,6 +93,9 @@ def main():
     ap.add_argument("--batches", type=int, default=12)
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--b", type=int, default=4096)
+    ap.add_argument("--layout", default="probe", choices=["probe", "blocked", "interleaved"],
+                    help="mask bit -> XCD: measured by the probe kernel (HW_REG_XCC_ID), or "
+                         "assumed: 32 consecutive bits per XCD, or bit i on XCD i %% 8")
     a = ap.parse_args()
     import bench
     import robot_ebert_amd as ebt
@@ -104,6 +107,10 @@ def main():
     xcd = xcd_of_bits(h, dev)
     per = {}
     for bit, (x, cu, se) in xcd.items():
+        if a.layout == "blocked":
+            x = bit // 32
+        elif a.layout == "interleaved":
+            x = bit % 8
         per.setdefault(x, []).append(bit)
     tail_bits = [b for x in sorted(per) for b in sorted(per[x])[:a.tail_cus]]
     gemm_bits = [b for b in range(256) if b not in set(tail_bits)]
@@ -173,7 +180,8 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / n * 1e3, outs, prev
 
-    res = {"tail_cus_per_xcd": a.tail_cus, "gemm_cus": len(gemm_bits), "tail_cus": len(tail_bits),
+    res = {"layout": a.layout, "xcds_seen": len(per),
+           "tail_cus_per_xcd": a.tail_cus, "gemm_cus": len(gemm_bits), "tail_cus": len(tail_bits),
            "qp_grid_override": grid_env, "bit_to_xcd_sample": {b: xcd[b] for b in (0, 1, 7, 8, 31, 32)}}
     for mode in ("serial_full", "serial_masked", "overlapped", "serial_full"):
         if mode == "serial_full" and grid_env:
