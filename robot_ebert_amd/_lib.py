@@ -129,6 +129,7 @@ _SIGNATURES = {
     "ebt_merge_block_max_groups": ([_I32], _I64),
     "ebt_cosine_topk_spec_lead": ([_I64, _I64, _I64, _I32, _INT], _I64),
     "ebt_spec_lead": ([_INT], _INT),
+    "ebt_filter_split": ([_I64], _I64),
     "ebt_cosine_screen": ([_VP, _VP, _VP, _VP, _I64, _I64, _VP, _INT, _I64, _VP, _VP, _VP, _INT,
                            _I32, _I64, _I32, _I32, _I64, _VP, _VP, _I32, _I32, _I64, _INT, _VP,
                            ctypes.c_size_t, _VP, _VP, _VP, _VP, _VP, _VP], _INT),

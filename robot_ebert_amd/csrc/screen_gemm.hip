@@ -1582,6 +1582,17 @@ int lead_hits(const float* lead_scores, int64_t ld_lead, int64_t lead, int64_t B
 
 int64_t filter_group_rows(int64_t B_pad) { return B_pad % QP_TILE == 0 ? QP_TILE : GBM; }
 
+// tiles per workgroup of one filter launch before it is split (EBT_FILTER_TPW in the
+// environment at start, ebt_filter_split at run time; 0 = never split)
+static std::atomic<int64_t>& filter_tpw_flag() {
+  static std::atomic<int64_t> v([] {
+    const char* s = getenv("EBT_FILTER_TPW");
+    return s ? (int64_t)atoll(s) : (int64_t)512;
+  }());
+  return v;
+}
+static int64_t filter_tiles_per_wg() { return filter_tpw_flag().load(std::memory_order_relaxed); }
+
 int screen_gemm_filter(const void* qimg, int64_t B_pad, const void* cimg, int64_t n_rows,
                        int32_t d_pad, int32_t ld_img, int img_dtype, const float* qscale,
                        const float* cscale, const float* thr, uint64_t* cand, int64_t ld_cand,
@@ -1607,8 +1618,41 @@ int screen_gemm_filter(const void* qimg, int64_t B_pad, const void* cimg, int64_
   e.ovf = ovf;
   e.idx_base = idx_base;
   e.slots = slots;
-  return launch_gemm<EPI_FILTER>(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale,
-                                 cscale, e, stream);
+  // A long launch is split into consecutive launches of at most filter_tiles_per_wg() tiles per
+  // workgroup (whole rounds): the persistent walk keeps its XCD's workgroups on neighbouring
+  // tiles only while they stay in step, and they drift apart over a launch (tools/walk_stamp.py:
+  // a whole C5 launch, 2034 tiles per workgroup, ends with a median in-flight spread of 48
+  // tiles instead of 32 and +45 % of modelled L2 miss traffic); every launch starts them
+  // together. The tiles, their hits and counts are the one launch's.
+  const int64_t tpw = filter_tiles_per_wg();
+  const int64_t qt = B_pad / QP_TILE;
+  int64_t cap_rows = 0;
+  if (tpw > 0 && B_pad % QP_TILE == 0 && n_cus() % qt == 0)
+    cap_rows = tpw * (n_cus() / qt) * QP_TILE;
+  if (cap_rows <= 0 || n_rows <= cap_rows + cap_rows / 2)
+    return launch_gemm<EPI_FILTER>(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale,
+                                   cscale, e, stream);
+  const int64_t parts = (n_rows + cap_rows - 1) / cap_rows;
+  // equal parts of whole rounds (the last takes the remainder)
+  const int64_t round_rows = (n_cus() / qt) * QP_TILE;
+  int64_t part_rows = (n_rows / parts + round_rows - 1) / round_rows * round_rows;
+  for (int64_t r0 = 0; r0 < n_rows; r0 += part_rows) {
+    const int64_t nr = n_rows - r0 < part_rows ? n_rows - r0 : part_rows;
+    EpiArgs ep = e;
+    ep.cand = cand + (r0 / QP_TILE) * slots;
+    ep.counts = counts + r0 / QP_TILE;
+    ep.idx_base = idx_base + r0;
+    rc = launch_gemm<EPI_FILTER>(qimg, B_pad, (const char*)cimg + r0 * ld_img * 2, nr, d_pad,
+                                 ld_img, img_dtype, qscale, cscale ? cscale + r0 : nullptr, ep,
+                                 stream);
+    if (rc) return rc;
+  }
+  return EBT_OK;
 }
 
 }  // namespace ebt
+
+extern "C" int64_t ebt_filter_split(int64_t tiles_per_workgroup) {
+  if (tiles_per_workgroup < 0) return ebt::filter_tpw_flag().load();
+  return ebt::filter_tpw_flag().exchange(tiles_per_workgroup);
+}

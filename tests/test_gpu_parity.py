@@ -1211,3 +1211,26 @@ def test_speculative_lead_hits_equal_filter_hits(cuda_device):
     for b in range(0, B, 7):   # positions [0, k): the k best of the partitioned list
         assert sorted(map(tuple, a1[b, :k])) == sorted(map(tuple, a0[b, :k])), b
     assert torch.equal(ovf1 != 0, ovf0 != 0)
+
+
+def test_filter_split_launches_equal_one_launch(cuda_device):
+    """A filter screen split into consecutive whole-round launches (ebt_filter_split: here 2
+    tiles per workgroup, so a 100K-row x 1024-query segment runs as several launches) finds the
+    same hits: the same final rows and scores as one launch per segment."""
+    ebt, L = _ebt()
+    lib = L.load()
+    n, d, B, k = 100_000, 128, 1024, 50
+    c = gaussian(81, n, d, "bf16")
+    q = gaussian(82, B, d, "bf16")
+    cat = ebt.Catalog(_t(c, "bf16", cuda_device))
+    qt = _t(q, "bf16", cuda_device)
+    prev = lib.ebt_filter_split(0)
+    try:
+        s0, r0 = ebt.score_topk(cat, k, queries=qt)
+        lib.ebt_filter_split(2)
+        t = ebt.Timer()
+        s1, r1 = ebt.score_topk(cat, k, queries=qt, timer=t)
+        assert t.query("gemm_filter")[1] >= 1
+    finally:
+        lib.ebt_filter_split(prev)
+    assert torch.equal(r0, r1) and torch.equal(s0, s1)
