@@ -172,6 +172,21 @@ EOF
                    $G bench r4f C4 --steps 5 --warmup 1 --parity 32
                    $G bench r4f C5 --steps 3 --warmup 1 --parity 32 ;;
       r4_prof_c45) $G prof r4p_c4 C4 3; $G prof r4p_c5 C5 2 ;;
+      # round 5 (profiles/r5/README.md)
+      r5_lead)     $G ab r5c_ab EBT_SPEC_LEAD=0 C2,C3 2 ;;
+      r5_split)    $G ab r5f_ab EBT_FILTER_TPW=0 C5,C4 1 ;;
+      r5_walk)     for sh in "c5 --n 520192 --b 16384 --cscale" "c3 --n 333312 --b 4096" \
+                             "c5full --n 2083072 --b 16384 --cscale"; do
+                     set -- $sh; nm=$1; shift
+                     $G py "r5_walk_$nm" tools/walk_stamp.py "$@"
+                     timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex screen_gemm \
+                       --output-format csv -d "$O/pmc_$nm" -o run -- python3 tools/walk_stamp.py "$@" --warm 2 \
+                       > "$O/pmc_$nm.log" 2>&1
+                   done ;;
+      r5_overlap)  for lay in probe blocked interleaved; do
+                     EBERT_LIB=_abl/libebert_grid.so EBT_QP_GRID=240 $G py "r5_overlap_$lay" \
+                       tools/overlap_probe.py --tail-cus 2 --layout "$lay"
+                   done ;;
       *) echo "unknown recipe $N" >&2; exit 2 ;;
     esac
     ;;
