@@ -133,7 +133,10 @@ int spec_threshold(const float*, int64_t, int64_t, int64_t, int, const float*, c
 int kth_threshold(const float*, int64_t, int64_t, int64_t, int, const float*, float*,
                   hipStream_t);
 int pool_kth(const float*, int64_t, int64_t, int64_t, int, int, float*, hipStream_t,
-             float* fv = nullptr, int64_t* fi = nullptr, int kprime = 0, int* ovf = nullptr);
+             float* fv = nullptr, int64_t* fi = nullptr, int kprime = 0, int* ovf = nullptr,
+             const float* lead_s = nullptr, int64_t ld_lead = 0, int lead = 0,
+             uint64_t* cand = nullptr, int64_t ld_cand = 0, int slots = 0,
+             uint8_t* counts = nullptr, int64_t ld_counts = 0);
 int spec_given_init(const float*, int64_t, int64_t, float*, float*, int64_t*, int, int*,
                     hipStream_t);
 int screen_gemm_pool(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
@@ -824,26 +827,6 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
   float* tspec = (float*)(ws + L.off_tspec);
   const int64_t m = L.head;
   const bool given = a.theta != nullptr;  // ebt_cosine_screen_at: the caller's threshold
-  if (given) {
-    // the threshold, the empty list (-inf / -1), no overflow yet: one launch
-    rc = spec_given_init(a.theta, B, B_pad, tspec, fv, fi, kprime, ovf, st);
-    if (rc) return rc;
-  } else {
-    {
-      StageScope s(timer, EBT_STAGE_GEMM, st);
-      rc = screen_gemm_pool(a.qimg, B_pad, a.cimg, m, a.d_pad, a.ld_img, a.img_dtype, a.qscale,
-                            a.cscale, 256 * L.spec_stride, pooled, L.ld_s, st, L.spec_lead,
-                            (float*)(ws + L.off_lead), L.ld_lead);
-    }
-    if (rc) return rc;
-    {
-      StageScope s(timer, EBT_STAGE_SELECT, st);
-      // theta_spec, and the empty list (-inf / -1) with no overflow yet
-      rc = pool_kth(pooled, L.ld_s, B, B_pad, (int)(m / 64), L.spec_j, tspec, st, fv, fi, kprime,
-                    ovf);
-    }
-    if (rc) return rc;
-  }
   const double spec_hits = given ? (a.hits > 0.0 ? a.hits : 1.0) : L.spec_hits;
   // hits per group ~ H group_rows / n (per query; its threshold's own spread ~ 1/sqrt(j) on
   // top): slots for 4x that + 4, and at least enough that a group overflow (which costs its
@@ -854,6 +837,35 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
   while (slots < EBT_FILTER_SLOTS_MAX &&
          (slots < 4.0 * per_group + 4.0 || n_cells * poisson_tail(1.5 * per_group, slots) > 1e-3))
     slots *= 2;
+  // the lead tiles (the sample's first tiles, their scores kept by the pool GEMM): their hits
+  // at theta_spec go into the first segment's first groups, taken by the same launch that finds
+  // theta_spec (pool_kth); the filter then starts after them
+  const int64_t lead = given ? 0 : L.spec_lead;
+  if (lead > 0 && (lead * slots > L.ld_cand || lead > L.ld_counts || L.group_rows != 256)) {
+    set_error("run_screen_spec: the lead does not fit the hit slots");
+    return EBT_EINVAL;
+  }
+  if (given) {
+    // the threshold, the empty list (-inf / -1), no overflow yet: one launch
+    rc = spec_given_init(a.theta, B, B_pad, tspec, fv, fi, kprime, ovf, st);
+    if (rc) return rc;
+  } else {
+    {
+      StageScope s(timer, EBT_STAGE_GEMM, st);
+      rc = screen_gemm_pool(a.qimg, B_pad, a.cimg, m, a.d_pad, a.ld_img, a.img_dtype, a.qscale,
+                            a.cscale, 256 * L.spec_stride, pooled, L.ld_s, st, lead,
+                            (float*)(ws + L.off_lead), L.ld_lead);
+    }
+    if (rc) return rc;
+    {
+      StageScope s(timer, EBT_STAGE_SELECT, st);
+      // theta_spec, the empty list (-inf / -1) with no overflow yet, the lead's hits
+      rc = pool_kth(pooled, L.ld_s, B, B_pad, (int)(m / 64), L.spec_j, tspec, st, fv, fi, kprime,
+                    ovf, (const float*)(ws + L.off_lead), L.ld_lead, (int)lead, cand, L.ld_cand,
+                    slots, counts, L.ld_counts);
+    }
+    if (rc) return rc;
+  }
   const bool wave = merge_wave_fits(kprime);
   int64_t seg_cap = L.ld_cand / slots;
   const int64_t max_groups = wave ? merge_wave_max_groups() : merge_block_max_groups(kprime);
@@ -880,19 +892,6 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
     }
     f_spread = x / (double)L.spec_j;
     f_spread = f_spread < 2.5 ? 2.5 : f_spread;
-  }
-  // the lead tiles' hits at theta_spec, into the first segment's first groups (the filter
-  // then starts after them: its groups follow)
-  const int64_t lead = given ? 0 : L.spec_lead;
-  if (lead > 0) {
-    if (lead * slots > L.ld_cand || lead > L.ld_counts || lead * L.group_rows != 256 * lead) {
-      set_error("run_screen_spec: the lead does not fit the hit slots");
-      return EBT_EINVAL;
-    }
-    StageScope s(timer, EBT_STAGE_SELECT, st);
-    rc = lead_hits((const float*)(ws + L.off_lead), L.ld_lead, lead, B_pad, tspec, cand,
-                   L.ld_cand, slots, counts, L.ld_counts, ovf, st);
-    if (rc) return rc;
   }
   int64_t r0 = 256 * lead;
   bool first = true, verified = false;

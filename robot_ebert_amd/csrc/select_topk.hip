@@ -1327,13 +1327,52 @@ __global__ void spec_threshold_kernel(const float* __restrict__ vals, int64_t ld
 // (ebt_pool_kth over the all-gathered samples of a row-sharded catalog).
 // Optionally (fv != null) the same wave also starts query b's empty list for the speculative
 // screen (fv -inf / fi -1 over k' entries, ovf 0): three memsets fewer per batch.
+// With a lead (the speculative screen's sample lead, lead > 0): the wave then takes its query's
+// hits among the lead tiles' stored scores at the threshold just found -- what the filter
+// epilogue writes for those tiles (screen_gemm.hip lead_hits_kernel, the same composites, counts
+// and overflow flag), without a launch of its own.
+struct LeadArgs {
+  const float* s;
+  int64_t ld;
+  int lead;
+  uint64_t* cand;
+  int64_t ld_cand;
+  int slots;
+  uint8_t* counts;
+  int64_t ld_counts;
+};
+__device__ __forceinline__ void lead_hits_wave(const LeadArgs& la, int64_t b, float th, int* ovf) {
+  const int lane = threadIdx.x & 63;
+  int over = 0;
+  for (int p = 0; p < la.lead; ++p) {
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = la.s[b * la.ld + (int64_t)p * 256 + e * 64 + lane];
+    uint32_t base = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool hit = v[e] >= th;
+      const uint64_t bm = __ballot(hit);
+      const uint32_t pp = base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+      if (hit && pp < (uint32_t)la.slots) {
+        const uint32_t row = (uint32_t)(p * 256 + e * 64 + lane);
+        la.cand[b * la.ld_cand + (int64_t)p * la.slots + pp] =
+            ((uint64_t)f2key(v[e]) << 32) | (uint64_t)(~row);
+      }
+      base += (uint32_t)__popcll(bm);
+    }
+    if (lane == 0) la.counts[b * la.ld_counts + p] = (uint8_t)(base < 255u ? base : 255u);
+    over |= base > (uint32_t)la.slots ? 1 : 0;
+  }
+  if (lane == 0 && over) ovf[b] = 1;
+}
 template <int E>
 __global__ __launch_bounds__(256) void pool_kth_kernel(const float* __restrict__ pool, int64_t ld,
                                                        int64_t B, int64_t B_pad, int G, int j,
                                                        float* __restrict__ thr,
                                                        float* __restrict__ fv,
                                                        int64_t* __restrict__ fi, int kprime,
-                                                       int* __restrict__ ovf) {
+                                                       int* __restrict__ ovf, LeadArgs la) {
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B_pad) return;
@@ -1347,6 +1386,7 @@ __global__ __launch_bounds__(256) void pool_kth_kernel(const float* __restrict__
   }
   if (b >= B) {
     if (lane == 0) thr[b] = __builtin_inff();
+    if (la.lead > 0) lead_hits_wave(la, b, __builtin_inff(), ovf);   // zero counts
     return;
   }
   uint32_t kx[E];
@@ -1362,31 +1402,37 @@ __global__ __launch_bounds__(256) void pool_kth_kernel(const float* __restrict__
     return c;
   };
   uint64_t lo = 1, hi = 0xffffffffull;  // largest t with count(key >= t) >= j
-  if (count_ge(1u) < j) {
-    if (lane == 0) thr[b] = -__builtin_inff();
-    return;
+  float th = -__builtin_inff();
+  if (count_ge(1u) >= j) {
+    while (lo < hi) {
+      const uint64_t mid = lo + ((hi - lo + 1) >> 1);
+      if (count_ge((uint32_t)mid) >= j) lo = mid;
+      else hi = mid - 1;
+    }
+    th = key2f((uint32_t)lo);
   }
-  while (lo < hi) {
-    const uint64_t mid = lo + ((hi - lo + 1) >> 1);
-    if (count_ge((uint32_t)mid) >= j) lo = mid;
-    else hi = mid - 1;
-  }
-  if (lane == 0) thr[b] = key2f((uint32_t)lo);
+  if (lane == 0) thr[b] = th;
+  if (la.lead > 0) lead_hits_wave(la, b, th, ovf);
 }
 int pool_kth(const float* pool, int64_t ld, int64_t B, int64_t B_pad, int G, int j, float* thr,
-             hipStream_t st, float* fv, int64_t* fi, int kprime, int* ovf) {
+             hipStream_t st, float* fv, int64_t* fi, int kprime, int* ovf,
+             const float* lead_s, int64_t ld_lead, int lead, uint64_t* cand, int64_t ld_cand,
+             int slots, uint8_t* counts, int64_t ld_counts) {
   if (!pool || !thr || B < 0 || B_pad < B || G < 1 || G > 2048 || j < 1 || ld < G ||
-      (fv && (!fi || !ovf || kprime < 1))) {
-    set_error("pool_kth: bad arguments (G=%d j=%d ld=%lld)", G, j, (long long)ld);
+      (fv && (!fi || !ovf || kprime < 1)) ||
+      (lead > 0 && (!lead_s || ld_lead < 256LL * lead || !cand || slots < 1 ||
+                    ld_cand < (int64_t)lead * slots || !counts || ld_counts < lead || !ovf))) {
+    set_error("pool_kth: bad arguments (G=%d j=%d ld=%lld lead=%d)", G, j, (long long)ld, lead);
     return EBT_EINVAL;
   }
+  LeadArgs la{lead_s, ld_lead, lead > 0 ? lead : 0, cand, ld_cand, slots, counts, ld_counts};
   const dim3 grid((unsigned)ceil_div(B_pad, 4)), block(256);
   if (G <= 256)
     hipLaunchKernelGGL(pool_kth_kernel<4>, grid, block, 0, st, pool, ld, B, B_pad, G, j, thr, fv,
-                       fi, kprime, ovf);
+                       fi, kprime, ovf, la);
   else
     hipLaunchKernelGGL(pool_kth_kernel<32>, grid, block, 0, st, pool, ld, B, B_pad, G, j, thr, fv,
-                       fi, kprime, ovf);
+                       fi, kprime, ovf, la);
   return launch_check("pool_kth_kernel");
 }
 
