@@ -325,8 +325,12 @@ static bool spec_params(int64_t B_pad, int64_t n_rows, int32_t kprime, int64_t* 
 #ifndef EBT_SPEC_SAMPLE_DIV
 #define EBT_SPEC_SAMPLE_DIV 200
 #endif
+#ifndef EBT_SPEC_SAMPLE_MIN
+#define EBT_SPEC_SAMPLE_MIN 64  // (build knob for A/B: the sample's size on mid-size catalogs)
+#endif
   const int64_t pdiv = full / EBT_SPEC_SAMPLE_DIV;
-  const int64_t pmax = pdiv > 64 ? (pdiv < 512 ? pdiv : 512) : 64;
+  const int64_t pmin = EBT_SPEC_SAMPLE_MIN;
+  const int64_t pmax = pdiv > pmin ? (pdiv < 512 ? pdiv : 512) : pmin;
   P = P > pmax ? pmax : P;
   // whole rounds of workgroups: P x (query tiles) a multiple of 256 when that keeps >= 8 tiles
   const int64_t per = 256 / (B_pad / 256) > 0 ? 256 / (B_pad / 256) : 1;
