@@ -429,9 +429,13 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
     L.group_rows = filter_group_rows(B_pad);
     // 1 GiB at B_pad <= 4096, growing with the batch up to 8 GiB (C5: 16384 queries): larger
     // segments, fewer merges
+    static const int64_t small_budget = [] {   // EBT_SLOT_BUDGET_MB: A/B knob, B_pad <= 4096
+      const char* v = getenv("EBT_SLOT_BUDGET_MB");
+      return (v ? atoll(v) : 1024LL) << 20;
+    }();
     int64_t bytes = B_pad * (512LL << 10);
     bytes = bytes < (1LL << 30) ? (1LL << 30) : (bytes > (8LL << 30) ? (8LL << 30) : bytes);
-    if (B_pad <= 4096) bytes = 1LL << 30;
+    if (B_pad <= 4096) bytes = small_budget;
     const int64_t budget = bytes / (B_pad * 8);
     const int64_t need = ceil_div(n_rows - (L.spec ? 0 : H), L.group_rows) * 16 +
                          8 * EBT_FILTER_SLOTS_MAX;
