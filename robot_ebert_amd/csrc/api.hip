@@ -122,7 +122,8 @@ int mask_excluded(float*, int64_t, int64_t, int64_t, int64_t, const int64_t*, co
                   hipStream_t);
 int rescore(const double*, int64_t, int32_t, const void*, int, int64_t, const double*, int64_t,
             const float*, const int64_t*, int32_t, int32_t, int64_t, const float*, const double*,
-            double*, int64_t*, int32_t*, hipStream_t, const int*, int, unsigned long long*);
+            double*, int64_t*, int32_t*, hipStream_t, const int*, int, unsigned long long*,
+            int64_t list_base = 0, const float* theta = nullptr);
 int screen_gemm_filter(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
                        const float*, const float*, const float*, uint64_t*, int64_t, int,
                        uint8_t*, int64_t, int*, int64_t, hipStream_t);
@@ -136,7 +137,8 @@ int pool_kth(const float*, int64_t, int64_t, int64_t, int, int, float*, hipStrea
              float* fv = nullptr, int64_t* fi = nullptr, int kprime = 0, int* ovf = nullptr,
              const float* lead_s = nullptr, int64_t ld_lead = 0, int lead = 0,
              uint64_t* cand = nullptr, int64_t ld_cand = 0, int slots = 0,
-             uint8_t* counts = nullptr, int64_t ld_counts = 0);
+             uint8_t* counts = nullptr, int64_t ld_counts = 0, int gj = 0,
+             int64_t rstride = 0);
 int spec_given_init(const float*, int64_t, int64_t, float*, float*, int64_t*, int, int*,
                     hipStream_t);
 int screen_gemm_pool(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
@@ -325,11 +327,13 @@ static bool spec_params(int64_t B_pad, int64_t n_rows, int32_t kprime, int64_t* 
 #ifndef EBT_SPEC_SAMPLE_DIV
 #define EBT_SPEC_SAMPLE_DIV 200
 #endif
+  // at least 32 tiles (round 5: C3 32 instead of 64, two rounds of the pool GEMM instead of four:
+  // +0.4 %, profiles/r5/ab/sample32_*), and at least one workgroup per CU (C2 keeps 64)
 #ifndef EBT_SPEC_SAMPLE_MIN
-#define EBT_SPEC_SAMPLE_MIN 64  // (build knob for A/B: the sample's size on mid-size catalogs)
+#define EBT_SPEC_SAMPLE_MIN 32  // (build knob for A/B)
 #endif
   const int64_t pdiv = full / EBT_SPEC_SAMPLE_DIV;
-  const int64_t pmin = EBT_SPEC_SAMPLE_MIN;
+  const int64_t pmin = fill > EBT_SPEC_SAMPLE_MIN ? fill : EBT_SPEC_SAMPLE_MIN;
   const int64_t pmax = pdiv > pmin ? (pdiv < 512 ? pdiv : 512) : pmin;
   P = P > pmax ? pmax : P;
   // whole rounds of workgroups: P x (query tiles) a multiple of 256 when that keeps >= 8 tiles
@@ -566,6 +570,22 @@ static int head_topk(const WsLayout& L, char* ws, const void* qimg, const float*
     if (rc) return rc;
   }
   return EBT_OK;
+}
+
+// The rescore of the row-sharded step (driver.hip): the shard's list holds GLOBAL rows
+// (list_base = row_offset: no local-rows pass), and the certificate also takes ebt_certify_cut's
+// tests (an overflowed fused list, a caller's threshold above the floor's cut) -- two launches
+// fewer per step. Timed and row-counted as ebt_rescore.
+int rescore_sharded(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
+                    int64_t ld, const double* gnorm64, int64_t row_offset, const float* cand_vals,
+                    const int64_t* cand_rows_global, int32_t kprime, int32_t k, int64_t n_rows,
+                    const float* eps, const double* t_floor, double* out_s, int64_t* out_r,
+                    int32_t* certified, const int* ovf, const float* theta, void* timer,
+                    hipStream_t st) {
+  StageScope sc(timer, EBT_STAGE_RESCORE, st);
+  return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, cand_vals, cand_rows_global,
+                 kprime, k, n_rows, eps, t_floor, out_s, out_r, certified, st, ovf, 0,
+                 timer_rows(timer), row_offset, theta);
 }
 
 }  // namespace ebt

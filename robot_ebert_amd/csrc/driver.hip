@@ -28,6 +28,13 @@ size_t large_topk_bytes(int64_t B, int64_t n, int64_t* Bg_out);
 int large_topk(const double*, int64_t, int32_t, const void*, int, int64_t, const double*, int64_t,
                int64_t, const int64_t*, const int64_t*, int32_t, double*, int64_t*, void*, size_t,
                hipStream_t);
+int rescore_sharded(const double*, int64_t, int32_t, const void*, int, int64_t, const double*,
+                    int64_t, const float*, const int64_t*, int32_t, int32_t, int64_t, const float*,
+                    const double*, double*, int64_t*, int32_t*, const int*, const float*, void*,
+                    hipStream_t);
+int pool_kth(const float*, int64_t, int64_t, int64_t, int, int, float*, hipStream_t, float*,
+             int64_t*, int, int*, const float*, int64_t, int, uint64_t*, int64_t, int, uint8_t*,
+             int64_t, int, int64_t);
 
 namespace {
 
@@ -743,7 +750,7 @@ struct ShardLayout {
   size_t screen_bytes;
   int64_t fw, cap;  // floor gather width per shard and query; packed results per rank (0: full)
   size_t pack_bytes;
-  size_t off_spass, off_pool, off_gsamp, off_perm, off_theta, off_lv, off_lr, off_lloc, off_ovf,
+  size_t off_spass, off_pool, off_gsamp, off_theta, off_lv, off_lr, off_ovf,
       off_eps, off_fsend, off_frecv, off_tfloor, off_ls, off_lrr, off_gs, off_gr, off_scale,
       off_qrecv, off_psend, off_precv, off_incomplete, bytes;
 };
@@ -798,15 +805,11 @@ bool shard_layout(const ebt_catalog& c, const ebt_comm& cm, int64_t B, int32_t k
   o = al(o + (size_t)D.B_pad * L.G * 4);
   L.off_gsamp = o;
   o = al(o + (size_t)B * L.GJ * 4 * (R + 1));  // this shard's J largest, then every shard's
-  L.off_perm = o;
-  o = al(o + (size_t)B * R * L.GJ * 4);
   L.off_theta = o;
   o = al(o + (size_t)D.B_pad * 4);
   L.off_lv = o;
   o = al(o + (size_t)B * kp * 4);
   L.off_lr = o;
-  o = al(o + (size_t)B * kp * 8);
-  L.off_lloc = o;
   o = al(o + (size_t)B * kp * 8);
   L.off_ovf = o;
   o = al(o + (size_t)B * 4);
@@ -844,25 +847,6 @@ bool shard_layout(const ebt_catalog& c, const ebt_comm& cm, int64_t B, int32_t k
   o = al(o + 4);
   L.bytes = o;
   return true;
-}
-
-// GLOBAL candidate rows -> rows of this shard (-1 stays empty)
-__global__ void local_rows_kernel(const int64_t* __restrict__ g, int64_t n, int64_t off,
-                                  int64_t* __restrict__ out) {
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;
-       t += (int64_t)gridDim.x * blockDim.x)
-    out[t] = g[t] >= 0 ? g[t] - off : -1;
-}
-
-// gathered sample maxima [R][B][G] -> [B][R * G] (ebt_pool_kth's rows)
-__global__ void permute_samples_kernel(const float* __restrict__ g, int R, int64_t B, int G,
-                                       float* __restrict__ out) {
-  const int64_t total = (int64_t)R * B * G;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = t / (B * G), rem = t - r * B * G, b = rem / G, j = rem - b * G;
-    out[b * R * G + r * G + j] = g[t];
-  }
 }
 
 // out[t] = sum over ranks r (in rank order) of in[r * total + t]: the all-reduce of the liked
@@ -1064,14 +1048,12 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
     // exact for j <= J; when J was clamped to G every shard sent all of its maxima, and any
     // j <= RG / 2 is (distributed.theta_from_samples decides alike)
     if (j <= S.J || (S.J == S.G && j <= S.RG / 2)) {
-      float* perm = (float*)(ws + S.off_perm);
       theta = (float*)(ws + S.off_theta);
       const int64_t RGJ = (int64_t)R * S.GJ;
       if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
-      hipLaunchKernelGGL(permute_samples_kernel, dim3(grid_for(RGJ * B)), dim3(256), 0, st, recv,
-                         R, B, (int)S.GJ, perm);
-      rc = launch_check("permute_samples_kernel");
-      if (!rc) rc = ebt_pool_kth(perm, RGJ, B, L.B_pad, (int32_t)RGJ, j, theta, st);
+      // the j-th of every rank's maxima, read in the gathered [R][B][J + 1] layout
+      rc = pool_kth(recv, RGJ, B, L.B_pad, (int)RGJ, j, theta, st, nullptr, nullptr, 0, nullptr,
+                    nullptr, 0, 0, nullptr, 0, 0, nullptr, 0, (int)S.GJ, B * S.GJ);
       if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
       if (rc) return rc;
       hits = ((double)j + (double)j * j / (2.0 * (double)S.RG)) * (double)c.n / m_total;
@@ -1110,23 +1092,16 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
   if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
   if (rc) return rc;
   // 5. the rescore of the rows that can enter the global top k, the certificate
-  int64_t* lloc = (int64_t*)(ws + S.off_lloc);
   double* ls = (double*)(ws + S.off_ls);
   int64_t* lrr = (int64_t*)(ws + S.off_lrr);
   const bool padded = L.k_eff < k;
   double* rs = padded ? (double*)(ws + L.off_res_s) : ls;
   int64_t* rr = padded ? (int64_t*)(ws + L.off_res_r) : lrr;
   int32_t* cert = (int32_t*)(ws + L.off_cert);
-  hipLaunchKernelGGL(local_rows_kernel, dim3(grid_for(B * L.kprime)), dim3(256), 0, st, lr,
-                     B * L.kprime, c.row_offset, lloc);
-  rc = launch_check("local_rows_kernel");
-  if (!rc)
-    rc = ebt_rescore(q64, B, c.d, c.data, c.dtype, c.ld, c.gnorm64, c.row_offset, lv, lloc,
-                     L.kprime, L.k_eff, c.n, eps, tfloor, rs, rr, cert, timer, st);
-  if (rc) return rc;
-  if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
-  rc = ebt_certify_cut(cert, ovf, use_theta ? theta : nullptr, tfloor, eps, B, st);
-  if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
+  // (the list's GLOBAL rows read as they are; the certificate with ebt_certify_cut's tests)
+  rc = rescore_sharded(q64, B, c.d, c.data, c.dtype, c.ld, c.gnorm64, c.row_offset, lv, lr,
+                       L.kprime, L.k_eff, c.n, eps, tfloor, rs, rr, cert, ovf,
+                       use_theta ? theta : nullptr, timer, st);
   if (rc) return rc;
   if (excl_off) {
     rc = hip_check(hipMemsetAsync(cert + B, 0, 4, st), "hipMemsetAsync");

@@ -150,7 +150,8 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     const int64_t* __restrict__ cand_rows, int kprime, int kpp, int k, int64_t n_rows,
     const float* __restrict__ eps, const double* __restrict__ t_floor, double* __restrict__ out_s,
     int64_t* __restrict__ out_r, int32_t* __restrict__ certified, const int* __restrict__ ovf_cnt,
-    int ovf_cap, unsigned long long* __restrict__ gathered) {
+    int ovf_cap, unsigned long long* __restrict__ gathered, int64_t list_base,
+    const float* __restrict__ theta) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* qs = (double*)smem;                           // d (NU = 0 only)
   double* sc = qs + (NU > 0 ? 0 : ((d + 1) & ~1));      // kpp: approx, then exact
@@ -215,6 +216,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     if (c < kprime) {
       row = cr[c];
       v = cv[c];
+      row = row >= 0 ? row - list_base : -1;  // a list of GLOBAL rows (list_base = row_offset)
     }
     const bool bad = c < kprime && row >= n_rows;  // corrupt entry, never dereferenced
     const bool valid = c < kprime && row >= 0 && !bad;
@@ -501,6 +503,9 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
       ok = amin < cut2;
     }
     if (ovf_cnt && ovf_cnt[b] > ovf_cap) ok = -1;  // fused screen dropped candidates
+    // a caller's screening threshold above the floor's cut may have dropped a row of the
+    // global top k (ebt_certify_cut's test, folded in)
+    if (theta && t_floor && !((double)theta[b] <= t_floor[b] - (double)eps[b])) ok = -1;
     if (corrupt) ok = -2;                           // internal error: row out of range
     certified[b] = ok;
     // rows gathered by the two passes (roofline accounting: ebt_timer_count_rows), spread over
@@ -750,7 +755,8 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
             const double* gnorm, int64_t row_offset, const float* cand_vals,
             const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
             const double* t_floor, double* out_s, int64_t* out_r, int32_t* certified,
-            hipStream_t st, const int* ovf_cnt, int ovf_cap, unsigned long long* gathered) {
+            hipStream_t st, const int* ovf_cnt, int ovf_cap, unsigned long long* gathered,
+            int64_t list_base, const float* theta) {
   if (!q64 || !cat || !gnorm || !cand_vals || !cand_rows || !eps || !out_s || !out_r ||
       !certified || B < 0 || d <= 0 || ld < d || k < 1 || kprime < k || kprime > 4096 ||
       dtype < 0 || dtype > 3) {
@@ -807,7 +813,8 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
   set_max_lds((const void*)rescore_kernel<DT, true, NU>, (int)lds_r);                          \
   hipLaunchKernelGGL((rescore_kernel<DT, true, NU>), grid, block, lds_r, st, q64, d, cat, ld,   \
                      gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,      \
-                     t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap, gathered);
+                     t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap, gathered, list_base,   \
+                     theta);
 #define EBT_RSR_NU(DT)                                                                          \
   switch (nu) {                                                                                 \
     case 1: EBT_RSR(DT, 1) break;                                                               \
@@ -833,11 +840,13 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
   if (vec)                                                                                      \
     hipLaunchKernelGGL((rescore_kernel<DT, true>), grid, block, lds, st, q64, d, cat, ld,       \
                        gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,    \
-                       t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap, gathered);           \
+                       t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap, gathered, list_base, \
+                       theta);                                                                  \
   else                                                                                          \
     hipLaunchKernelGGL((rescore_kernel<DT, false>), grid, block, lds, st, q64, d, cat, ld,      \
                        gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,    \
-                       t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap, gathered);
+                       t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap, gathered, list_base, \
+                       theta);
   switch (dtype) {
     case EBT_F32: EBT_RS(EBT_F32) break;
     case EBT_BF16: EBT_RS(EBT_BF16) break;

@@ -1372,7 +1372,8 @@ __global__ __launch_bounds__(256) void pool_kth_kernel(const float* __restrict__
                                                        float* __restrict__ thr,
                                                        float* __restrict__ fv,
                                                        int64_t* __restrict__ fi, int kprime,
-                                                       int* __restrict__ ovf, LeadArgs la) {
+                                                       int* __restrict__ ovf, LeadArgs la,
+                                                       int gj, int64_t rstride) {
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B_pad) return;
@@ -1389,11 +1390,16 @@ __global__ __launch_bounds__(256) void pool_kth_kernel(const float* __restrict__
     if (la.lead > 0) lead_hits_wave(la, b, __builtin_inff(), ovf);   // zero counts
     return;
   }
+  // gj > 0: the all-gathered [R][B][gj] layout of a row-sharded catalog's samples, read in place
+  // (value g of query b at rank g / gj), instead of a [B][ld] row
   uint32_t kx[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int g = lane + 64 * e;
-    kx[e] = g < G ? f2key(pool[b * ld + g]) : 0u;
+    const int gg = g < G ? g : 0;
+    const int64_t off = gj > 0 ? (int64_t)(gg / gj) * rstride + b * gj + gg % gj : b * ld + gg;
+    const float x = pool[off];
+    kx[e] = g < G ? f2key(x) : 0u;
   }
   auto count_ge = [&](uint32_t t) {
     int c = 0;
@@ -1417,8 +1423,9 @@ __global__ __launch_bounds__(256) void pool_kth_kernel(const float* __restrict__
 int pool_kth(const float* pool, int64_t ld, int64_t B, int64_t B_pad, int G, int j, float* thr,
              hipStream_t st, float* fv, int64_t* fi, int kprime, int* ovf,
              const float* lead_s, int64_t ld_lead, int lead, uint64_t* cand, int64_t ld_cand,
-             int slots, uint8_t* counts, int64_t ld_counts) {
-  if (!pool || !thr || B < 0 || B_pad < B || G < 1 || G > 2048 || j < 1 || ld < G ||
+             int slots, uint8_t* counts, int64_t ld_counts, int gj, int64_t rstride) {
+  if (!pool || !thr || B < 0 || B_pad < B || G < 1 || G > 2048 || j < 1 ||
+      (gj > 0 ? (G % gj != 0 || rstride < B * (int64_t)gj) : ld < G) ||
       (fv && (!fi || !ovf || kprime < 1)) ||
       (lead > 0 && (!lead_s || ld_lead < 256LL * lead || !cand || slots < 1 ||
                     ld_cand < (int64_t)lead * slots || !counts || ld_counts < lead || !ovf))) {
@@ -1429,10 +1436,10 @@ int pool_kth(const float* pool, int64_t ld, int64_t B, int64_t B_pad, int G, int
   const dim3 grid((unsigned)ceil_div(B_pad, 4)), block(256);
   if (G <= 256)
     hipLaunchKernelGGL(pool_kth_kernel<4>, grid, block, 0, st, pool, ld, B, B_pad, G, j, thr, fv,
-                       fi, kprime, ovf, la);
+                       fi, kprime, ovf, la, gj, rstride);
   else
     hipLaunchKernelGGL(pool_kth_kernel<32>, grid, block, 0, st, pool, ld, B, B_pad, G, j, thr, fv,
-                       fi, kprime, ovf, la);
+                       fi, kprime, ovf, la, gj, rstride);
   return launch_check("pool_kth_kernel");
 }
 

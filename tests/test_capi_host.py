@@ -197,10 +197,11 @@ def test_spec_plan_poisson_rank():
         lam = kp * 256 * P / n
         assert poisson.sf(j - 1, lam) <= 1e-6 < poisson.sf(j - 2, lam), (n, P, j)
         assert H >= j * n / (256 * P)
-    assert sp(4096, 1_000_000, 200)[:3] == (64, 61, 16)
+    assert sp(4096, 1_000_000, 200)[:3] == (32, 121, 12)   # round 5: 32 tiles (2 pool rounds)
     assert sp(4096, 125_000, 200)[0] == 16          # one round of 256 workgroups
+    assert sp(1024, 100_000, 120)[0] == 64          # C2: one workgroup per CU (64 tiles x 4)
     assert sp(100, 1_000_000, 104)[0] == 0          # B_pad = 128: the 128-tile kernel, no spec
-    assert sp(4096, 1_000_000, 1016)[0] == 64       # k' <= 2048: spec with block merges
+    assert sp(4096, 1_000_000, 1016)[0] == 32       # k' <= 2048: spec with block merges
     assert sp(4096, 1_000_000, 2052)[0] == 0        # k' > 2048: no spec
     assert sp(4096, 20_000, 200)[0] == 0            # too few tiles for a sample
     assert sp(4096, 1_000_000, 200, _lib.EBT_FLAG_NO_FUSE)[0] == 0
