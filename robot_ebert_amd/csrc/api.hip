@@ -128,6 +128,7 @@ int screen_gemm_filter(const void*, int64_t, const void*, int64_t, int32_t, int3
                        const float*, const float*, const float*, uint64_t*, int64_t, int,
                        uint8_t*, int64_t, int*, int64_t, hipStream_t);
 int64_t filter_group_rows(int64_t);
+int64_t filter_split_rows(int64_t B_pad, int64_t n_rows);
 
 int spec_threshold(const float*, int64_t, int64_t, int64_t, int, const float*, const float*, float*,
                    int*, int, hipStream_t);
@@ -842,6 +843,28 @@ static int check_pipe(const PipeArgs& a, const char* who) {
 //      the query is rerun unfused. So theta_spec needs no proof: a wrong guess costs a rerun.
 // Sample rows are screened twice (in the sample and in the filter pass); they enter the list
 // only through the filter, so nothing is counted twice.
+// One fused segment's filter screen over rows [r0, r0 + seg): one launch, or consecutive
+// launches of whole rounds when the segment is long (filter_split_rows, screen_gemm.hip), each
+// its own timed launch (the roofline's per-launch average stays a kernel's). The hits and counts
+// of group g of the segment land at cand + g * slots / counts + g, whatever the parts.
+static int filter_screen(const PipeArgs& a, int64_t r0, int64_t seg, const float* thr,
+                         uint64_t* cand, int64_t ld_cand, int slots, uint8_t* counts,
+                         int64_t ld_counts, int* ovf, void* timer, hipStream_t st) {
+  const int64_t part = filter_split_rows(a.B_pad, seg);
+  const int64_t step = part > 0 ? part : seg;
+  for (int64_t p0 = 0; p0 < seg; p0 += step) {
+    const int64_t nr = seg - p0 < step ? seg - p0 : step;
+    const int64_t r = r0 + p0, g = p0 / 256;  // part boundaries are whole 256-row groups
+    StageScope s(timer, EBT_STAGE_GEMM_FILTER, st);
+    const int rc = screen_gemm_filter(a.qimg, a.B_pad, (const char*)a.cimg + r * a.ld_img * 2, nr,
+                                      a.d_pad, a.ld_img, a.img_dtype, a.qscale,
+                                      a.cscale ? a.cscale + r : nullptr, thr, cand + g * slots,
+                                      ld_cand, slots, counts + g, ld_counts, ovf, r, st);
+    if (rc) return rc;
+  }
+  return EBT_OK;
+}
+
 static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float* fv,
                            int64_t* fi, void* timer, hipStream_t st) {
   int rc;
@@ -955,13 +978,8 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
       if (rc) return rc;
       t = thr;
     }
-    {
-      StageScope s(timer, EBT_STAGE_GEMM_FILTER, st);
-      rc = screen_gemm_filter(a.qimg, B_pad, (const char*)a.cimg + r0 * a.ld_img * 2, seg,
-                              a.d_pad, a.ld_img, a.img_dtype, a.qscale,
-                              a.cscale ? a.cscale + r0 : nullptr, t, cand + g0 * slots,
-                              L.ld_cand, slots, counts + g0, L.ld_counts, ovf, r0, st);
-    }
+    rc = filter_screen(a, r0, seg, t, cand + g0 * slots, L.ld_cand, slots, counts + g0,
+                       L.ld_counts, ovf, timer, st);
     if (rc) return rc;
     // the last wave merge also runs the final VERIFY of theta_spec (no separate launch)
     const bool fuse_verify = wave && !given && r0 + seg == n_rows;
@@ -1073,12 +1091,8 @@ static int run_screen(const PipeArgs& a, const WsLayout& L, char* ws, float* fv,
     const int64_t groups = ceil_div(seg, L.group_rows);
     rc = kth_threshold(fv, kprime, B, B_pad, k, a.eps, thr, st);
     if (rc) return rc;
-    {
-      StageScope s(timer, EBT_STAGE_GEMM_FILTER, st);
-      rc = screen_gemm_filter(a.qimg, B_pad, (const char*)a.cimg + r0 * ld_img * 2, seg, d_pad,
-                              ld_img, a.img_dtype, a.qscale, a.cscale ? a.cscale + r0 : nullptr,
-                              thr, cand, L.ld_cand, slots, counts, L.ld_counts, ovf, r0, st);
-    }
+    rc = filter_screen(a, r0, seg, thr, cand, L.ld_cand, slots, counts, L.ld_counts, ovf,
+                       timer, st);
     if (rc) return rc;
     {
       StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);

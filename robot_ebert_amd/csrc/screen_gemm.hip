@@ -1618,36 +1618,26 @@ int screen_gemm_filter(const void* qimg, int64_t B_pad, const void* cimg, int64_
   e.ovf = ovf;
   e.idx_base = idx_base;
   e.slots = slots;
-  // A long launch is split into consecutive launches of at most filter_tiles_per_wg() tiles per
-  // workgroup (whole rounds): the persistent walk keeps its XCD's workgroups on neighbouring
-  // tiles only while they stay in step, and they drift apart over a launch (tools/walk_stamp.py:
-  // a whole C5 launch, 2034 tiles per workgroup, ends with a median in-flight spread of 48
-  // tiles instead of 32 and +45 % of modelled L2 miss traffic); every launch starts them
-  // together. The tiles, their hits and counts are the one launch's.
+  return launch_gemm<EPI_FILTER>(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale,
+                                 cscale, e, stream);
+}
+
+// Rows per part of a long filter screen (0: not split): at most filter_tiles_per_wg() tiles per
+// workgroup, whole rounds. The persistent walk keeps its XCD's workgroups on neighbouring tiles
+// only while they stay in step, and they drift apart over a long launch (tools/walk_stamp.py: a
+// whole C5 launch, 2034 tiles per workgroup, ends with a median in-flight spread of 48 tiles
+// instead of 32 and +45 % of modelled L2 miss traffic); every launch starts them together. The
+// pipeline (api.hip filter_screen) launches a screen of more than 1.5 parts as consecutive
+// parts over the same groups: the same tiles, hits and counts as one launch.
+int64_t filter_split_rows(int64_t B_pad, int64_t n_rows) {
   const int64_t tpw = filter_tiles_per_wg();
   const int64_t qt = B_pad / QP_TILE;
-  int64_t cap_rows = 0;
-  if (tpw > 0 && B_pad % QP_TILE == 0 && n_cus() % qt == 0)
-    cap_rows = tpw * (n_cus() / qt) * QP_TILE;
-  if (cap_rows <= 0 || n_rows <= cap_rows + cap_rows / 2)
-    return launch_gemm<EPI_FILTER>(qimg, B_pad, cimg, n_rows, d_pad, ld_img, img_dtype, qscale,
-                                   cscale, e, stream);
-  const int64_t parts = (n_rows + cap_rows - 1) / cap_rows;
-  // equal parts of whole rounds (the last takes the remainder)
+  if (tpw <= 0 || B_pad % QP_TILE != 0 || qt < 1 || n_cus() % qt != 0) return 0;
   const int64_t round_rows = (n_cus() / qt) * QP_TILE;
-  int64_t part_rows = (n_rows / parts + round_rows - 1) / round_rows * round_rows;
-  for (int64_t r0 = 0; r0 < n_rows; r0 += part_rows) {
-    const int64_t nr = n_rows - r0 < part_rows ? n_rows - r0 : part_rows;
-    EpiArgs ep = e;
-    ep.cand = cand + (r0 / QP_TILE) * slots;
-    ep.counts = counts + r0 / QP_TILE;
-    ep.idx_base = idx_base + r0;
-    rc = launch_gemm<EPI_FILTER>(qimg, B_pad, (const char*)cimg + r0 * ld_img * 2, nr, d_pad,
-                                 ld_img, img_dtype, qscale, cscale ? cscale + r0 : nullptr, ep,
-                                 stream);
-    if (rc) return rc;
-  }
-  return EBT_OK;
+  const int64_t cap_rows = tpw * round_rows;
+  if (n_rows <= cap_rows + cap_rows / 2) return 0;
+  const int64_t parts = (n_rows + cap_rows - 1) / cap_rows;
+  return (n_rows / parts + round_rows - 1) / round_rows * round_rows;
 }
 
 }  // namespace ebt
