@@ -145,8 +145,6 @@ int spec_given_init(const float*, int64_t, int64_t, float*, float*, int64_t*, in
 int screen_gemm_pool(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
                      const float*, const float*, int64_t, float*, int64_t, hipStream_t,
                      int64_t lead = 0, float* lead_scores = nullptr, int64_t ld_lead = 0);
-int lead_hits(const float*, int64_t, int64_t, int64_t, const float*, uint64_t*, int64_t, int,
-              uint8_t*, int64_t, int*, hipStream_t);
 int64_t gemm_cus();
 int merge_segment(float*, int64_t*, int64_t, int, const uint64_t*, int64_t, int, const uint8_t*,
                   int64_t, int64_t, int64_t, const int64_t*, const int64_t*, int*, hipStream_t,

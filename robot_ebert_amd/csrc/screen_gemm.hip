@@ -1533,52 +1533,7 @@ int screen_gemm_pool(const void* qimg, int64_t B_pad, const void* cimg, int64_t 
                                cscale, e, stream, cstride, (int)lead, lead_scores, ld_lead);
 }
 
-// The lead tiles' hits once the threshold is known: exactly what the filter epilogue writes for
-// those tiles (screen_gemm_qp2_kernel<filter>) -- every score >= thr[q] as the composite
-// f2key(v) << 32 | ~row into the (query, group) slot range, the group's count (u8, saturated)
-// and the overflow flag when the count exceeds the slots. One workgroup per (lead tile, query).
-__global__ __launch_bounds__(256) void lead_hits_kernel(
-    const float* __restrict__ S2, int64_t ld_s2, const float* __restrict__ thr,
-    uint64_t* __restrict__ cand, int64_t ld_cand, int slots, uint8_t* __restrict__ counts,
-    int64_t ld_counts, int* __restrict__ ovf) {
-  __shared__ uint32_t wcnt[4];
-  const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t q = blockIdx.y;
-  const float v = S2[q * ld_s2 + (int64_t)p * QP_TILE + tid];
-  const bool hit = v >= thr[q];
-  const uint64_t bm = __ballot(hit);
-  if (lane == 0) wcnt[wave] = (uint32_t)__popcll(bm);
-  __syncthreads();
-  uint32_t base = 0;
-  for (int w = 0; w < wave; ++w) base += wcnt[w];
-  const uint32_t total = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-  if (hit) {
-    const uint32_t pp = base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
-    if (pp < (uint32_t)slots) {
-      const uint32_t row = (uint32_t)(p * QP_TILE + tid);
-      cand[q * ld_cand + (int64_t)p * slots + pp] =
-          ((uint64_t)f2key_select(v) << 32) | (uint64_t)(~row);
-    }
-  }
-  if (tid == 0) {
-    counts[q * ld_counts + p] = (uint8_t)(total < 255u ? total : 255u);
-    if (total > (uint32_t)slots) ovf[q] = 1;
-  }
-}
 
-int lead_hits(const float* lead_scores, int64_t ld_lead, int64_t lead, int64_t B_pad,
-              const float* thr, uint64_t* cand, int64_t ld_cand, int slots, uint8_t* counts,
-              int64_t ld_counts, int* ovf, hipStream_t st) {
-  if (lead <= 0) return EBT_OK;
-  if (!lead_scores || !thr || !cand || !counts || !ovf || ld_lead < lead * QP_TILE ||
-      slots < 1 || ld_cand < lead * slots || ld_counts < lead || B_pad < 1 || B_pad > 65535) {
-    set_error("lead_hits: bad arguments");
-    return EBT_EINVAL;
-  }
-  hipLaunchKernelGGL(lead_hits_kernel, dim3((unsigned)lead, (unsigned)B_pad), dim3(256), 0, st,
-                     lead_scores, ld_lead, thr, cand, ld_cand, slots, counts, ld_counts, ovf);
-  return launch_check("lead_hits_kernel");
-}
 
 int64_t filter_group_rows(int64_t B_pad) { return B_pad % QP_TILE == 0 ? QP_TILE : GBM; }
 

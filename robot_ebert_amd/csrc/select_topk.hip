@@ -1329,7 +1329,7 @@ __global__ void spec_threshold_kernel(const float* __restrict__ vals, int64_t ld
 // screen (fv -inf / fi -1 over k' entries, ovf 0): three memsets fewer per batch.
 // With a lead (the speculative screen's sample lead, lead > 0): the wave then takes its query's
 // hits among the lead tiles' stored scores at the threshold just found -- what the filter
-// epilogue writes for those tiles (screen_gemm.hip lead_hits_kernel, the same composites, counts
+// epilogue writes for those tiles (screen_gemm.hip filter_tile: the same composites, counts
 // and overflow flag), without a launch of its own.
 struct LeadArgs {
   const float* s;
