@@ -58,7 +58,9 @@ extern "C" {
 /* Library version (major*10000 + minor*100 + patch).
  * 0.2.0: ebt_rescore gained `timer`; ebt_comm gained the trailing `all_reduce_f64` pointer (the
  *        library calls it whenever it is non-NULL: zero-initialise every ebt_comm).
- * 0.3.0: ebt_timer_count_rows / ebt_timer_rows (additive). */
+ * 0.3.0: ebt_timer_count_rows / ebt_timer_rows (additive).
+ * 0.3.1: eps from the measured image errors (ebt_query_image); ebt_catalog_init measures u_cat
+ *        and its state holds 256 bytes more for a non-native catalog (ebt_catalog_state_bytes). */
 int ebt_version(void);
 
 /* Message for the last non-zero return on this thread ("" if none). */
@@ -104,12 +106,14 @@ int ebt_scale_rows_f64(double* q64, int64_t B, int32_t d, const double* scale, v
  *   qimg[b][j] = round_to(img_dtype, q64[b][j]) (rows B..B_pad-1 and columns d..ld_img-1 = 0),
  *   qscale[b]  = 1,
  *   eps[b]     = a rigorous bound on |approx score - exact float64 score| for every catalog
- *                row, given the catalog image rounding `u_cat` (0 for a native image whose
- *                values are exact, 2^-11 for a float16-rounded normalised image):
- *                eps = 1.05*(|q|*(u_q + u_cat + u_q*u_cat) + (d+8)*2^-24*(|q|+1)) + 1e-9,
- *                with u_q the unit round-off of img_dtype.
+ *                row, given `u_cat` >= ||image row - row/gnorm||_2 for every row (0 for a
+ *                native image whose values are exact; ebt_catalog_init measures it for a
+ *                float16-rounded normalised image, and the unit round-off 2^-11 always holds):
+ *                eps = 1.05*(dq + |q|*u_cat + dq*u_cat + (d+8)*2^-24*(|q|+1)) + 1e-9,
+ *                with dq = ||qimg[b] - q64[b]||_2 measured by the kernel (ABI 0.3.1; before it
+ *                dq was bounded by |q| times the unit round-off of img_dtype).
  * With `native_q` != 0 the image is instead the raw query `q` (same dtype as img_dtype, the
- * native-catalog screening mode): qimg = q, qscale[b] = 1/gnorm(q[b]) and u_q = 0. */
+ * native-catalog screening mode): qimg = q, qscale[b] = 1/gnorm(q[b]) and dq = 0. */
 int ebt_query_image(const double* q64, int64_t B, int64_t B_pad, int32_t d, int img_dtype,
                     const void* q_native, int64_t ldq, int native_q, float u_cat, void* qimg,
                     int32_t ld_img, float* qscale, float* eps, void* stream);
@@ -359,7 +363,8 @@ typedef struct ebt_catalog {
   const void* image;      /* [n][ld_img] f16/bf16  (state, or `data` itself)                */
   const float* cscale;    /* epilogue row scales: inv32 for native images, NULL otherwise   */
   int32_t img_dtype, ld_img, d_pad, native;
-  float u_cat;            /* unit round-off of the image (0: exact native values)           */
+  float u_cat;            /* bound on ||image row - row/gnorm||_2 (0: exact native values;
+                             measured by ebt_catalog_init; 2^-11 is always a valid value)    */
 } ebt_catalog;
 
 size_t ebt_catalog_state_bytes(const void* data, int dtype, int64_t n, int32_t d, int64_t ld);

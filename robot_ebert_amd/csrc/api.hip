@@ -108,7 +108,7 @@ int select_topk(const float*, const int64_t*, int64_t, int64_t, int64_t, int64_t
                 int32_t, float*, int64_t*, int64_t, hipStream_t);
 int row_norms(const void*, int, int64_t, int32_t, int64_t, double*, float*, hipStream_t);
 int screen_image(const void*, int, int64_t, int32_t, int64_t, const double*, int, int, void*,
-                 int32_t, hipStream_t);
+                 int32_t, hipStream_t, unsigned int* err_max = nullptr);
 int query_dense(const void*, int, int64_t, int32_t, int64_t, double*, hipStream_t);
 int query_liked_sum(const void*, int, int32_t, int64_t, const double*, int64_t, const int64_t*,
                     const int64_t*, double*, hipStream_t, int64_t row_offset = 0,
@@ -593,7 +593,7 @@ using namespace ebt;
 
 extern "C" {
 
-int ebt_version(void) { return 300; }  // 0.3.0: ebt_timer_count_rows / _rows (see ebert.h)
+int ebt_version(void) { return 301; }  // 0.3.1: measured image errors in eps (see ebert.h)
 
 const char* ebt_last_error(void) { return g_err; }
 

@@ -341,6 +341,10 @@ bool valid_catalog(const ebt_catalog* c) {
 }
 
 }  // namespace
+
+int screen_image(const void*, int, int64_t, int32_t, int64_t, const double*, int, int, void*,
+                 int32_t, hipStream_t, unsigned int* err_max);
+
 }  // namespace ebt
 
 using namespace ebt;
@@ -354,6 +358,7 @@ size_t ebt_catalog_state_bytes(const void* data, int dtype, int64_t n, int32_t d
   const bool alias = native && d % 64 == 0 && ld % 64 == 0 && ((uintptr_t)data & 15) == 0;
   size_t o = al((size_t)n * 8) + al((size_t)round_up(n, 128) * 4);
   if (!alias) o += al((size_t)n * d_pad * 2);
+  if (!native) o += al(4);  // the image's measured rounding error (ebt_catalog_init)
   return o;
 }
 
@@ -407,13 +412,30 @@ int ebt_catalog_init(ebt_catalog* cat, const void* data, int dtype, int64_t n, i
       rc = ebt_screen_image(data, dtype, n, d, ld, c.gnorm64, 0, c.img_dtype, img, c.ld_img, st);
     }
   } else {
+    // f16 image of the normalised rows. u_cat = the largest ||image row - row / gnorm||_2 over
+    // the rows, measured by the image kernel (rounded up to a float; rows with non-finite
+    // values left out) -- ~0.4 x the unit round-off 2^-11 that bounds it a priori, so the
+    // certificate's eps band (and the rows the rescore gathers) is about half as wide; one
+    // stream sync to read it back, once per catalog
     c.img_dtype = EBT_F16;
-    c.u_cat = 1.0f / 2048.0f;  // 2^-11: f16 image of the normalised rows
     c.cscale = nullptr;
     c.native = 0;
     c.ld_img = c.d_pad;
     c.image = img;
-    rc = ebt_screen_image(data, dtype, n, d, ld, c.gnorm64, 1, c.img_dtype, img, c.ld_img, st);
+    unsigned int* d_err = (unsigned int*)(img + al((size_t)n * c.d_pad * 2));
+    unsigned int h_err = 0;
+    rc = hip_check(hipMemsetAsync(d_err, 0, 4, st), "hipMemsetAsync");
+    if (!rc)
+      rc = screen_image(data, dtype, n, d, ld, c.gnorm64, 1, c.img_dtype, img, c.ld_img, st,
+                        d_err);
+    if (!rc)
+      rc = hip_check(hipMemcpyAsync(&h_err, d_err, 4, hipMemcpyDeviceToHost, st),
+                     "hipMemcpyAsync");
+    if (!rc) rc = hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+    if (rc) return rc;
+    float u;
+    memcpy(&u, &h_err, 4);
+    c.u_cat = std::isfinite(u) && u >= 0.0f ? u : 1.0f / 2048.0f;
   }
   if (rc) return rc;
   *cat = c;

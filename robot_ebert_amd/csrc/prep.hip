@@ -118,13 +118,21 @@ __device__ __forceinline__ void load8_f64(const void* __restrict__ x, int64_t of
   }
 }
 
+// (image value - x)^2 in float64, for the image's measured rounding error
+template <int IMG>
+__device__ __forceinline__ double sq_err(uint16_t h, double x) {
+  const double r = (IMG == EBT_F16 ? f16_bits_to_f64(h) : bf16_bits_to_f64(h)) - x;
+  return r * r;
+}
+
 template <int DT, int IMG, bool VEC>
 __global__ __launch_bounds__(256) void screen_image_kernel(const void* __restrict__ x, int64_t n,
                                                             int d, int64_t ld,
                                                             const double* __restrict__ gnorm,
                                                             int normalize,
                                                             uint16_t* __restrict__ img,
-                                                            int ld_img) {
+                                                            int ld_img,
+                                                            unsigned int* __restrict__ err_max) {
   constexpr int SI_CH = 4;     // chunks per lane whose loads are in flight together
   const int cpr = ld_img / 8;  // 16-byte chunks per image row
   const int lane = threadIdx.x & 63;
@@ -132,6 +140,7 @@ __global__ __launch_bounds__(256) void screen_image_kernel(const void* __restric
   for (int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); row < n;
        row += waves) {
     const double s = normalize ? 1.0 / gnorm[row] : 1.0;
+    double es = 0.0;   // err_max: sum of (image - x s)^2 over the lane's elements
     for (int c0 = lane; c0 < cpr; c0 += 64 * SI_CH) {
       if (VEC) {
         // all of the lane's full chunks loaded before any is converted (a loop that converts
@@ -150,13 +159,17 @@ __global__ __launch_bounds__(256) void screen_image_kernel(const void* __restric
           u16x8_t o;
           if (c * 8 + 8 <= d) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = f64_to_img<IMG>(v[u][e] * s);
+            for (int e = 0; e < 8; ++e) {
+              o[e] = f64_to_img<IMG>(v[u][e] * s);
+              if (err_max) es += sq_err<IMG>(o[e], v[u][e] * s);
+            }
           } else {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const int jj = c * 8 + e;
               const double w = jj < d ? load_as_f64<DT>(x, row * ld + jj) * s : 0.0;
               o[e] = f64_to_img<IMG>(w);
+              if (err_max) es += sq_err<IMG>(o[e], w);
             }
           }
           *(u16x8_t*)(img + row * ld_img + c * 8) = o;
@@ -169,9 +182,22 @@ __global__ __launch_bounds__(256) void screen_image_kernel(const void* __restric
             const int jj = c * 8 + e;
             const double w = jj < d ? load_as_f64<DT>(x, row * ld + jj) * s : 0.0;
             o[e] = f64_to_img<IMG>(w);
+            if (err_max) es += sq_err<IMG>(o[e], w);
           }
           *(u16x8_t*)(img + row * ld_img + c * 8) = o;
         }
+      }
+    }
+    if (err_max) {
+      // the row's ||image - x s||_2, rounded up to a float; the largest over the rows by an
+      // unsigned max on the bits (non-negative floats order as their bits). A row with
+      // non-finite values is left out (its scores are not certified by any rounding bound)
+      es = wave_sum_f64(es);
+      if (lane == 0 && es <= 1.0) {
+        const double e = sqrt(es);
+        float f = (float)e;
+        if ((double)f < e) f = nextafterf(f, 1.0f);
+        atomicMax(err_max, __float_as_uint(f));
       }
     }
   }
@@ -179,7 +205,7 @@ __global__ __launch_bounds__(256) void screen_image_kernel(const void* __restric
 
 int screen_image(const void* x, int dtype, int64_t n, int32_t d, int64_t ld,
                  const double* gnorm, int normalize, int img_dtype, void* img, int32_t ld_img,
-                 hipStream_t st) {
+                 hipStream_t st, unsigned int* err_max) {
   if (!x || !img || n < 0 || d <= 0 || ld < d || ld_img < d || ld_img % 64 != 0 ||
       (normalize && !gnorm) || (img_dtype != EBT_F16 && img_dtype != EBT_BF16) || dtype < 0 ||
       dtype > 3 || ((uintptr_t)img & 15)) {
@@ -195,10 +221,10 @@ int screen_image(const void* x, int dtype, int64_t n, int32_t d, int64_t ld,
 #define EBT_SI_V(DT, IMG)                                                                      \
   if (vec)                                                                                     \
     hipLaunchKernelGGL((screen_image_kernel<DT, IMG, true>), grid, block, 0, st, x, n, d, ld,  \
-                       gnorm, normalize, (uint16_t*)img, ld_img);                              \
+                       gnorm, normalize, (uint16_t*)img, ld_img, err_max);                     \
   else                                                                                         \
     hipLaunchKernelGGL((screen_image_kernel<DT, IMG, false>), grid, block, 0, st, x, n, d, ld, \
-                       gnorm, normalize, (uint16_t*)img, ld_img);
+                       gnorm, normalize, (uint16_t*)img, ld_img, err_max);
 #define EBT_SI(DT)                                                                             \
   if (img_dtype == EBT_F16) {                                                                  \
     EBT_SI_V(DT, EBT_F16)                                                                      \
@@ -413,6 +439,17 @@ int scale_rows_f64(double* q64, int64_t B, int32_t d, const double* scale, hipSt
 }
 
 // ---------------------------------------------------------------------- query image/eps ----
+// The certificate's bound on |approx score - exact float64 score| for one query and every
+// catalog row: with q the float64 query (norm qnrm), dq = ||image(q) - q||_2
+// measured here, and u_cat a bound on ||image(c) - c/|c|||_2 for every row (measured at catalog
+// init, or the unit round-off 2^-11; 0 for a native image), image(q).image(c) - q.c/|c| =
+// dq_vec.c + q.dc_vec + dq_vec.dc_vec is at most dq + qnrm u_cat + dq u_cat by Cauchy-Schwarz;
+// the float32 accumulation of d products (and the epilogue's scales) adds (d+8) 2^-24 (qnrm+1).
+__device__ __forceinline__ float query_eps(double qnrm, double dq, float u_cat, int d) {
+  const double uc = (double)u_cat;
+  return (float)(1.05 * (dq + qnrm * uc + dq * uc + (d + 8) * 0x1p-24 * (qnrm + 1.0)) + 1e-9);
+}
+
 template <int IMG>
 __global__ __launch_bounds__(256) void query_image_kernel(
     const double* __restrict__ q64, int64_t B, int d, const uint16_t* __restrict__ qn,
@@ -454,17 +491,19 @@ __global__ __launch_bounds__(256) void query_image_kernel(
   }
   const double qnrm = sqrt(block_sum_f64(s, red));
   const double nrm_native = native_q ? sqrt(block_sum_f64(sn, red)) : 1.0;
+  double se = 0.0;
   for (int j = threadIdx.x; j < ld_img; j += blockDim.x) {
     uint16_t o = 0;
-    if (j < d) o = native_q ? qn[b * ldq + j] : f64_to_img<IMG>(q64[b * d + j]);
+    if (j < d) {
+      o = native_q ? qn[b * ldq + j] : f64_to_img<IMG>(q64[b * d + j]);
+      if (!native_q) se += sq_err<IMG>(o, q64[b * d + j]);
+    }
     orow[j] = o;
   }
+  const double dq = native_q ? 0.0 : sqrt(block_sum_f64(se, red));
   if (threadIdx.x == 0) {
     qscale[b] = native_q ? (float)(1.0 / guard_norm(nrm_native)) : 1.f;
-    const double uq = native_q ? 0.0 : (IMG == EBT_F16 ? 0x1p-11 : 0x1p-8);
-    const double uc = (double)u_cat;
-    const double e = 1.05 * (qnrm * (uq + uc + uq * uc) + (d + 8) * 0x1p-24 * (qnrm + 1.0)) + 1e-9;
-    if (eps) eps[b] = (float)e;
+    if (eps) eps[b] = query_eps(qnrm, dq, u_cat, d);
   }
 }
 
@@ -522,7 +561,7 @@ __global__ __launch_bounds__(256) void query_prep_kernel(
   }
   const double nq = sqrt(block_sum_f64(s, red));
   const double g = guard_norm(nq);
-  double s2 = 0.0;
+  double s2 = 0.0, se = 0.0;
 #pragma unroll
   for (int e = 0; e < QP_PER; ++e) {
     const int j = tid + e * 256;
@@ -530,18 +569,18 @@ __global__ __launch_bounds__(256) void query_prep_kernel(
       const double x = v[e] / g;
       q64[b * d + j] = x;
       s2 += x * x;
-      orow[j] = native_q ? ((const uint16_t*)q)[b * ldq + j] : f64_to_img<IMG>(x);
+      const uint16_t o = native_q ? ((const uint16_t*)q)[b * ldq + j] : f64_to_img<IMG>(x);
+      if (!native_q) se += sq_err<IMG>(o, x);
+      orow[j] = o;
     }
   }
   for (int j = d + tid; j < ld_img; j += blockDim.x) orow[j] = 0;
   const double qnrm = sqrt(block_sum_f64(s2, red));
+  const double dq = native_q ? 0.0 : sqrt(block_sum_f64(se, red));
   if (tid == 0) {
     // native: the image holds q itself, scaled by 1 / ||q|| in the epilogue (query_image)
     qscale[b] = native_q ? (float)(1.0 / g) : 1.f;
-    const double uq = native_q ? 0.0 : (IMG == EBT_F16 ? 0x1p-11 : 0x1p-8);
-    const double uc = (double)u_cat;
-    eps[b] = (float)(1.05 * (qnrm * (uq + uc + uq * uc) + (d + 8) * 0x1p-24 * (qnrm + 1.0)) +
-                     1e-9);
+    eps[b] = query_eps(qnrm, dq, u_cat, d);
   }
 }
 
@@ -598,7 +637,7 @@ __global__ __launch_bounds__(256) void query_prep_wave_kernel(
     }
   }
   const double g = guard_norm(sqrt(wave_sum_f64(s)));
-  double s2 = 0.0;
+  double s2 = 0.0, se = 0.0;
 #pragma unroll
   for (int i = 0; i < QPW_CH; ++i) {
     const int c = lane + 64 * i;
@@ -610,6 +649,7 @@ __global__ __launch_bounds__(256) void query_prep_wave_kernel(
         x[e] = v[i][e] / g;
         s2 += x[e] * x[e];
         o[e] = f64_to_img<IMG>(x[e]);
+        if (!native_q) se += sq_err<IMG>(o[e], x[e]);
       }
       double2* dst = (double2*)(q64 + b * d + c * 8);
 #pragma unroll
@@ -620,12 +660,10 @@ __global__ __launch_bounds__(256) void query_prep_wave_kernel(
   }
   for (int c = nch + lane; c < cpr; c += 64) *(u16x8_t*)(orow + c * 8) = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
   const double qnrm = sqrt(wave_sum_f64(s2));
+  const double dq = native_q ? 0.0 : sqrt(wave_sum_f64(se));
   if (lane == 0) {
     qscale[b] = native_q ? (float)(1.0 / g) : 1.f;
-    const double uq = native_q ? 0.0 : (IMG == EBT_F16 ? 0x1p-11 : 0x1p-8);
-    const double uc = (double)u_cat;
-    eps[b] = (float)(1.05 * (qnrm * (uq + uc + uq * uc) + (d + 8) * 0x1p-24 * (qnrm + 1.0)) +
-                     1e-9);
+    eps[b] = query_eps(qnrm, dq, u_cat, d);
   }
 }
 

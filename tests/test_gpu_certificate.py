@@ -106,6 +106,34 @@ def test_screen_error_within_eps(cuda_device, kind, cdt, qdt, d, n, B):
     assert r <= 1.0, f"screen error exceeds eps: ratio {r}"
 
 
+@pytest.mark.parametrize("kind", ["gauss", "mixed"])
+def test_catalog_image_error_measured(cuda_device, kind):
+    """ebt_catalog_init measures u_cat = max over rows of ||image row - row / gnorm||_2 (the
+    bound's catalog term): not below the float64 value torch computes from the same image, not
+    above it by more than float rounding, and well under the a-priori 2^-11 for Gaussian rows;
+    a query batch's eps is then below the a-priori formula's."""
+    import robot_ebert_amd as ebt
+    from robot_ebert_amd.search import prepare_queries
+    dev = cuda_device
+    n, d = 20000, 768
+    cat = ebt.Catalog(_rows(kind, n, d, 404, dev))
+    x = cat.data.double() / cat.gnorm[:, None]
+    err = (cat.image[:, :d].double() - x).norm(dim=1)
+    want = float(err[torch.isfinite(err)].max())
+    assert want <= cat.u_cat <= want * (1 + 2.0 ** -20), (cat.u_cat, want)
+    if kind == "gauss":
+        assert cat.u_cat < 0.6 * 2.0 ** -11, cat.u_cat
+    q = _rows(kind, 256, d, 405, dev)
+    qb = prepare_queries(cat, queries=q)
+    qn = qb.q64.norm(dim=1)
+    dq = (qb.qimg[:256, :d].double() - qb.q64).norm(dim=1)
+    u = cat.u_cat
+    want_eps = 1.05 * (dq + qn * u + dq * u + (d + 8) * 2.0 ** -24 * (qn + 1.0)) + 1e-9
+    torch.testing.assert_close(qb.eps[:256].double(), want_eps, rtol=2.0 ** -20, atol=0)
+    prior = 1.05 * (qn * 2 * 2.0 ** -11 + (d + 8) * 2.0 ** -24 * (qn + 1.0)) + 1e-9
+    assert bool((qb.eps[:256].double() < prior).all())
+
+
 @pytest.mark.parametrize("cdt", ["f32", "bf16"])
 def test_screen_error_liked_queries(cuda_device, cdt):
     """Liked-mean queries (lib.py:51-52 folded into q: |q| < 1) through ebt_query_liked_sum."""

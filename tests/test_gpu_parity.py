@@ -702,6 +702,46 @@ def test_batched_user_recs_match_reference(cuda_device, k):
     assert max(b.batches) > 1
 
 
+def test_score_server_user_recs_match_reference(cuda_device):
+    """§8f-2, the multi-process shape (serving.py): the route's requests go through ScoreClients
+    (three connections, as three server processes would hold) to one ScoreServer over the GPU
+    RecBatcher; the answers are get_user_recs' golden ones at k = 10, errors keep their text,
+    and the server coalesced requests of different connections into one batch."""
+    import concurrent.futures as cf
+    from robot_ebert_amd.batcher import RecBatcher
+    from robot_ebert_amd.serving import ScoreClient, ScoreServer
+    lib, gold = _collab_setup(cuda_device)
+    b = RecBatcher(lib.movies_collab_catalog, max_batch=64, max_wait_ms=20.0)
+    srv = ScoreServer(b)
+    clients = [ScoreClient(srv.address) for _ in range(3)]
+    users = list(gold["users"].items())
+
+    def one(i):
+        uid, rec = users[i]
+        try:
+            return uid, rec, lib.get_user_recs_batched(clients[i % 3], uid, 10), None
+        except ValueError as e:
+            return uid, rec, None, e
+    try:
+        with cf.ThreadPoolExecutor(16) as ex:
+            out = list(ex.map(one, range(len(users))))
+    finally:
+        for c in clients:
+            c.close()
+        srv.close()
+        b.close()
+    for uid, rec, got, err in out:
+        want = rec["k10"]
+        if isinstance(want, dict):
+            assert err is not None and str(err) == want["message"], uid
+            continue
+        assert err is None, (uid, err)
+        assert [g.movie.tmdb_id for g in got] == [w[0] for w in want], uid
+        np.testing.assert_allclose([g.score for g in got], [w[1] for w in want], rtol=0,
+                                   atol=SCORE_ATOL)
+    assert srv.requests > 0 and max(b.batches) > 1
+
+
 def test_catalog_from_chroma_matches_reference(cuda_device):
     """§8f-3: the C1 catalog ingested from a Chroma-style get() result (ids + embeddings, the
     constants.py:55-56 source) serves get_user_recs with the reference's golden answers."""
