@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import itertools
 import os
+import queue
 import struct
 import threading
 from concurrent.futures import Future
@@ -134,6 +135,10 @@ class ScoreServer:
         self.address = address or os.path.join(
             "/tmp", f"ebert-score-{os.getpid()}-{id(self):x}.sock")
         self._listener = Listener(self.address, family="AF_UNIX", authkey=AUTHKEY)
+        try:   # this user's processes only (the handshake key is not a secret)
+            os.chmod(self.address, 0o600)
+        except OSError:
+            pass
         self._closed = False
         self._conns: list = []
         self._lock = threading.Lock()
@@ -162,14 +167,27 @@ class ScoreServer:
                              daemon=True).start()
 
     def _serve(self, conn) -> None:
-        send_lock = threading.Lock()
+        # answers go out through this connection's writer thread: the batcher's completion
+        # thread only queues a frame, so a client that stops reading (a full socket buffer)
+        # blocks its own writer, never the batcher and the other connections
+        outq: "queue.SimpleQueue[Optional[bytes]]" = queue.SimpleQueue()
 
-        def reply(frame: bytes) -> None:
-            with send_lock:
+        def write_loop() -> None:
+            while True:
+                frame = outq.get()
+                if frame is None:
+                    return
                 try:
                     conn.send_bytes(frame)
                 except (OSError, EOFError, ValueError):
-                    pass   # the client went away; its other answers are dropped as well
+                    # the client went away: drop its answers, wake its reader
+                    _shutdown(conn)
+                    while outq.get() is not None:
+                        pass
+                    return
+        writer = threading.Thread(target=write_loop, name="ebert-score-write", daemon=True)
+        writer.start()
+        reply = outq.put
 
         while True:
             try:
@@ -195,6 +213,10 @@ class ScoreServer:
         with self._lock:
             if conn in self._conns:
                 self._conns.remove(conn)
+        # answers still pending in the batcher are queued after the sentinel and dropped; the
+        # writer sends what was queued before it (an error reply of a malformed frame included)
+        outq.put(None)
+        writer.join(5.0)
         try:
             conn.close()
         except OSError:

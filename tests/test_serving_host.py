@@ -121,6 +121,26 @@ def test_malformed_frame_ends_only_its_connection():
     b.close()
 
 
+def test_client_that_stops_reading_does_not_block_others():
+    """A connection whose client never reads its answers (its socket buffer full) blocks only
+    its own writer: the batcher's completion thread and the other clients go on."""
+    from multiprocessing.connection import Client
+    from robot_ebert_amd.serving import AUTHKEY
+    x = np.random.default_rng(5).standard_normal((6000, 8))
+    b = RecBatcher(_Cat(x), max_batch=8, max_wait_ms=1.0, score_fn=_oracle_score([]))
+    srv = ScoreServer(b)
+    stuck = Client(srv.address, family="AF_UNIX", authkey=AUTHKEY)
+    for i in range(40):   # 40 answers of 5000 rows (80 KB each): far more than a socket buffer
+        stuck.send_bytes(encode_request(i + 1, [1, 2], [], 5000))
+    good = ScoreClient(srv.address, timeout=30.0)
+    for i in range(5):
+        assert len(good.score([3 + i], [], 7)[1]) == 7
+    good.close()
+    srv.close()
+    stuck.close()
+    b.close()
+
+
 def test_server_close_fails_pending_callers():
     x = np.random.default_rng(2).standard_normal((100, 8))
     gate = threading.Event()
