@@ -60,7 +60,8 @@ extern "C" {
  *        library calls it whenever it is non-NULL: zero-initialise every ebt_comm).
  * 0.3.0: ebt_timer_count_rows / ebt_timer_rows (additive).
  * 0.3.1: eps from the measured image errors (ebt_query_image); ebt_catalog_init measures u_cat
- *        and its state holds 256 bytes more for a non-native catalog (ebt_catalog_state_bytes). */
+ *        and its state holds 256 bytes more for a non-native catalog (ebt_catalog_state_bytes);
+ *        ebt_cosine_sample_lead / ebt_cosine_screen_at_lead (additive). */
 int ebt_version(void);
 
 /* Message for the last non-zero return on this thread ("" if none). */
@@ -590,6 +591,29 @@ int ebt_cosine_screen_at(const double* q64, const void* qimg, const float* qscal
                          void* workspace, size_t ws_bytes, float* list_vals, int64_t* list_rows,
                          int32_t* ovf_out, float* eps_out, const float* theta, double hits,
                          void* timer, void* stream);
+/* The same two calls with a LEAD (0.3.1; lead = 0 is the calls above): the sample's first `lead`
+ * tiles are the shard's first `lead` tiles (rows 0 .. 256 lead), the other tiles - lead follow
+ * from tile `lead` on, `tile_stride` apart, and the lead tiles' scores are kept in
+ * lead_scores[b * ld_lead + r] (ld_lead >= 256 lead). ebt_cosine_screen_at_lead takes the lead's
+ * hits at theta from those scores and filters rows 256 lead .. n_rows only, so that the shard's
+ * filter launches cover whole rounds of the persistent grid (driver.hip: the C ABI's sharded
+ * step picks lead = ceil(n/256) mod (catalog tiles per round); 0 turns it off). */
+int ebt_cosine_sample_lead(const void* qimg, const float* qscale, int64_t B_pad,
+                           const void* cimg, const float* cscale, int img_dtype, int32_t ld_img,
+                           int64_t n_rows, int32_t d_pad, int64_t tiles, int64_t tile_stride,
+                           float* pooled, int64_t ld_pooled, int64_t lead, float* lead_scores,
+                           int64_t ld_lead, void* timer, void* stream);
+int ebt_cosine_screen_at_lead(const double* q64, const void* qimg, const float* qscale,
+                              const float* eps, int64_t B, int64_t B_pad, const void* cat,
+                              int dtype, int64_t ld, const double* gnorm64, const void* cimg,
+                              const float* cscale, int img_dtype, int32_t ld_img, int64_t n_rows,
+                              int32_t d, int32_t d_pad, int64_t row_offset,
+                              const int64_t* excl_off, const int64_t* excl_rows, int32_t k,
+                              int32_t kprime, int64_t chunk_rows, int flags, void* workspace,
+                              size_t ws_bytes, float* list_vals, int64_t* list_rows,
+                              int32_t* ovf_out, float* eps_out, const float* theta, double hits,
+                              int64_t lead, const float* lead_scores, int64_t ld_lead,
+                              void* timer, void* stream);
 /* After the floor all-gather of the per-shard path: g = [R][B][ld] float32 (each shard's k best
  * approx in columns [0, ld-1), its eps in column ld-1) ->
  * t_floor[b] = the k-th largest of g[r][b][j] - g[r][b][ld-1] over all r and j < ld-1, in float64

@@ -139,6 +139,12 @@ _SIGNATURES = {
                               ctypes.c_double, _VP, _VP], _INT),
     "ebt_cosine_sample": ([_VP, _VP, _I64, _VP, _VP, _INT, _I32, _I64, _I32, _I64, _I64, _VP,
                            _I64, _VP, _VP], _INT),
+    "ebt_cosine_sample_lead": ([_VP, _VP, _I64, _VP, _VP, _INT, _I32, _I64, _I32, _I64, _I64,
+                                _VP, _I64, _I64, _VP, _I64, _VP, _VP], _INT),
+    "ebt_cosine_screen_at_lead": ([_VP, _VP, _VP, _VP, _I64, _I64, _VP, _INT, _I64, _VP, _VP,
+                                   _VP, _INT, _I32, _I64, _I32, _I32, _I64, _VP, _VP, _I32,
+                                   _I32, _I64, _INT, _VP, ctypes.c_size_t, _VP, _VP, _VP, _VP,
+                                   _VP, ctypes.c_double, _I64, _VP, _I64, _VP, _VP], _INT),
     "ebt_pool_kth": ([_VP, _I64, _I64, _I64, _I32, _I32, _VP, _VP], _INT),
     "ebt_union_floor": ([_VP, _I32, _I64, _I32, _I32, _VP, _VP], _INT),
     "ebt_certify_cut": ([_VP, _VP, _VP, _VP, _VP, _I64, _VP], _INT),

@@ -141,7 +141,9 @@ int pool_kth(const float*, int64_t, int64_t, int64_t, int, int, float*, hipStrea
              uint8_t* counts = nullptr, int64_t ld_counts = 0, int gj = 0,
              int64_t rstride = 0);
 int spec_given_init(const float*, int64_t, int64_t, float*, float*, int64_t*, int, int*,
-                    hipStream_t);
+                    hipStream_t, const float* lead_s = nullptr, int64_t ld_lead = 0, int lead = 0,
+                    uint64_t* cand = nullptr, int64_t ld_cand = 0, int slots = 0,
+                    uint8_t* counts = nullptr, int64_t ld_counts = 0);
 int screen_gemm_pool(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
                      const float*, const float*, int64_t, float*, int64_t, hipStream_t,
                      int64_t lead = 0, float* lead_scores = nullptr, int64_t ld_lead = 0);
@@ -393,6 +395,20 @@ static int64_t spec_lead_tiles(int64_t B_pad, int64_t n_rows, int64_t sample_til
   const int64_t lead = ceil_div(n_rows, 256) % rt;
   // a lead of at most half the sample (its strided part keeps the spread), and full tiles only
   return (lead <= sample_tiles / 2 && lead * 256 <= n_rows - 256) ? lead : 0;
+}
+
+// A row-sharded catalog's sample lead (ebt_cosine_sample_lead / ebt_cosine_screen_at_lead): the
+// same rule over the shard's rows and its own sample tiles
+// A row-sharded catalog's sample lead (ebt_cosine_sample_lead / ebt_cosine_screen_at_lead): the
+// shard's filter then covers whole rounds too. The shards' samples together spread over the
+// catalog, so a shard's lead may take all but 4 of its sample tiles (C3 on 8 ranks: 489 tiles
+// per shard, 16 sample tiles of which the first 9 are the lead; the filter's 31st round of 9 x 16
+// tiles disappears).
+int64_t shard_lead_tiles(int64_t B_pad, int64_t n_rows, int64_t sample_tiles) {
+  const int64_t rt = round_tiles(B_pad);
+  if (rt <= 1 || !spec_lead_flag().load(std::memory_order_relaxed)) return 0;
+  const int64_t lead = ceil_div(n_rows, 256) % rt;
+  return (lead <= sample_tiles - 4 && lead * 256 <= n_rows - 256) ? lead : 0;
 }
 
 static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
@@ -806,6 +822,11 @@ struct PipeArgs {
   // ebt_cosine_screen_at: the caller's per-query threshold [B] and expected hits per query
   const float* theta = nullptr;
   double hits = 0.0;
+  // ebt_cosine_screen_at_lead: the caller's sample lead -- the shard's first `lead` 256-row tiles,
+  // their scores [B_pad][ld_lead] stored by ebt_cosine_sample_lead
+  int64_t lead = 0;
+  const float* lead_s = nullptr;
+  int64_t ld_lead = 0;
 };
 
 static int check_pipe(const PipeArgs& a, const char* who) {
@@ -889,14 +910,16 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
   // the lead tiles (the sample's first tiles, their scores kept by the pool GEMM): their hits
   // at theta_spec go into the first segment's first groups, taken by the same launch that finds
   // theta_spec (pool_kth); the filter then starts after them
-  const int64_t lead = given ? 0 : L.spec_lead;
+  const int64_t lead = given ? a.lead : L.spec_lead;
   if (lead > 0 && (lead * slots > L.ld_cand || lead > L.ld_counts || L.group_rows != 256)) {
     set_error("run_screen_spec: the lead does not fit the hit slots");
     return EBT_EINVAL;
   }
   if (given) {
     // the threshold, the empty list (-inf / -1), no overflow yet: one launch
-    rc = spec_given_init(a.theta, B, B_pad, tspec, fv, fi, kprime, ovf, st);
+    // (+ the caller's lead hits at theta into the first groups' slots)
+    rc = spec_given_init(a.theta, B, B_pad, tspec, fv, fi, kprime, ovf, st, a.lead_s, a.ld_lead,
+                         (int)lead, cand, L.ld_cand, slots, counts, L.ld_counts);
     if (rc) return rc;
   } else {
     {
@@ -1185,6 +1208,24 @@ int ebt_cosine_screen_at(const double* q64, const void* qimg, const float* qscal
                          void* workspace, size_t ws_bytes, float* list_vals, int64_t* list_rows,
                          int32_t* ovf_out, float* eps_out, const float* theta, double hits,
                          void* timer, void* stream) {
+  return ebt_cosine_screen_at_lead(q64, qimg, qscale, eps, B, B_pad, cat, dtype, ld, gnorm64,
+                                   cimg, cscale, img_dtype, ld_img, n_rows, d, d_pad, row_offset,
+                                   excl_off, excl_rows, k, kprime, chunk_rows, flags, workspace,
+                                   ws_bytes, list_vals, list_rows, ovf_out, eps_out, theta, hits,
+                                   0, nullptr, 0, timer, stream);
+}
+
+int ebt_cosine_screen_at_lead(const double* q64, const void* qimg, const float* qscale,
+                              const float* eps, int64_t B, int64_t B_pad, const void* cat,
+                              int dtype, int64_t ld, const double* gnorm64, const void* cimg,
+                              const float* cscale, int img_dtype, int32_t ld_img, int64_t n_rows,
+                              int32_t d, int32_t d_pad, int64_t row_offset,
+                              const int64_t* excl_off, const int64_t* excl_rows, int32_t k,
+                              int32_t kprime, int64_t chunk_rows, int flags, void* workspace,
+                              size_t ws_bytes, float* list_vals, int64_t* list_rows,
+                              int32_t* ovf_out, float* eps_out, const float* theta, double hits,
+                              int64_t lead, const float* lead_scores, int64_t ld_lead,
+                              void* timer, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   flags |= EBT_FLAG_THETA;
   PipeArgs a{q64, qimg, qscale, eps, B, B_pad, cat, dtype, ld, gnorm64, cimg, cscale,
@@ -1192,8 +1233,16 @@ int ebt_cosine_screen_at(const double* q64, const void* qimg, const float* qscal
              chunk_rows, flags};
   a.theta = theta;
   a.hits = hits;
+  a.lead = lead;
+  a.lead_s = lead_scores;
+  a.ld_lead = ld_lead;
   int rc = check_pipe(a, "ebt_cosine_screen_at");
   if (rc) return rc;
+  if (lead < 0 || (lead > 0 && (!lead_scores || ld_lead < 256 * lead || 256 * lead >= n_rows))) {
+    set_error("ebt_cosine_screen_at_lead: bad lead (lead=%lld, ld_lead=%lld, n_rows=%lld)",
+              (long long)lead, (long long)ld_lead, (long long)n_rows);
+    return EBT_EINVAL;
+  }
   if (!workspace || !list_vals || !list_rows || !ovf_out || !eps_out || !theta) {
     set_error("ebt_cosine_screen_at: null pointer");
     return EBT_EINVAL;
@@ -1220,15 +1269,29 @@ int ebt_cosine_sample(const void* qimg, const float* qscale, int64_t B_pad, cons
                       const float* cscale, int img_dtype, int32_t ld_img, int64_t n_rows,
                       int32_t d_pad, int64_t tiles, int64_t tile_stride, float* pooled,
                       int64_t ld_pooled, void* timer, void* stream) {
-  if (tiles < 1 || tile_stride < 1 || (tiles - 1) * tile_stride * 256 + 256 > n_rows) {
-    set_error("ebt_cosine_sample: %lld tiles %lld apart do not fit %lld rows", (long long)tiles,
-              (long long)tile_stride, (long long)n_rows);
+  return ebt_cosine_sample_lead(qimg, qscale, B_pad, cimg, cscale, img_dtype, ld_img, n_rows,
+                                d_pad, tiles, tile_stride, pooled, ld_pooled, 0, nullptr, 0, timer,
+                                stream);
+}
+
+int ebt_cosine_sample_lead(const void* qimg, const float* qscale, int64_t B_pad,
+                           const void* cimg, const float* cscale, int img_dtype, int32_t ld_img,
+                           int64_t n_rows, int32_t d_pad, int64_t tiles, int64_t tile_stride,
+                           float* pooled, int64_t ld_pooled, int64_t lead, float* lead_scores,
+                           int64_t ld_lead, void* timer, void* stream) {
+  // tiles 0 .. lead-1 are the first tiles, tile t >= lead starts at row 256 (lead + (t - lead)
+  // tile_stride): the last one ends within (tiles - 1) tile_stride + 1 tiles
+  const int64_t last = tiles > lead ? lead + (tiles - lead - 1) * tile_stride : lead - 1;
+  if (tiles < 1 || tile_stride < 1 || lead < 0 || lead > tiles || 256 * (last + 1) > n_rows ||
+      (lead > 0 && (!lead_scores || ld_lead < 256 * lead))) {
+    set_error("ebt_cosine_sample: %lld tiles %lld apart (lead %lld) do not fit %lld rows",
+              (long long)tiles, (long long)tile_stride, (long long)lead, (long long)n_rows);
     return EBT_EINVAL;
   }
   hipStream_t st = (hipStream_t)stream;
   StageScope s(timer, EBT_STAGE_GEMM, st);
   return screen_gemm_pool(qimg, B_pad, cimg, 256 * tiles, d_pad, ld_img, img_dtype, qscale, cscale,
-                          256 * tile_stride, pooled, ld_pooled, st);
+                          256 * tile_stride, pooled, ld_pooled, st, lead, lead_scores, ld_lead);
 }
 
 int ebt_pool_kth(const float* pooled, int64_t ld, int64_t B, int64_t B_pad, int32_t G, int32_t j,

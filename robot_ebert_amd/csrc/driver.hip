@@ -344,6 +344,7 @@ bool valid_catalog(const ebt_catalog* c) {
 
 int screen_image(const void*, int, int64_t, int32_t, int64_t, const double*, int, int, void*,
                  int32_t, hipStream_t, unsigned int* err_max);
+int64_t shard_lead_tiles(int64_t B_pad, int64_t n_rows, int64_t sample_tiles);
 
 }  // namespace ebt
 
@@ -763,18 +764,22 @@ int64_t sh_tiles(int64_t n_global, int world, int64_t B_pad) {
   P = P < cap ? P : cap;
   const int64_t per = 256 / (B_pad / 256) > 1 ? 256 / (B_pad / 256) : 1;
   if (P / per * per >= 8) P = P / per * per;
+  // a sample GEMM of less than one round of the persistent grid takes a round's time anyway:
+  // fill it (C3 on 8 ranks: 8 -> 16 tiles per shard, room for the lead)
+  if (P < per && per <= full / 6) P = per;
   return (P >= 1 && world * P >= 8) ? P : 0;
 }
 
 struct ShardLayout {
   DriverLayout D;
   int64_t tiles, G, RG, J, GJ;  // sample maxima per shard (G), sent per shard (J + 1 of them)
+  int64_t lead, ld_lead;        // this shard's sample lead (its first tiles' scores kept)
   size_t screen_bytes;
   int64_t fw, cap;  // floor gather width per shard and query; packed results per rank (0: full)
   size_t pack_bytes;
   size_t off_spass, off_pool, off_gsamp, off_theta, off_lv, off_lr, off_ovf,
       off_eps, off_fsend, off_frecv, off_tfloor, off_ls, off_lrr, off_gs, off_gr, off_scale,
-      off_qrecv, off_psend, off_precv, off_incomplete, bytes;
+      off_qrecv, off_psend, off_precv, off_incomplete, off_lead, bytes;
 };
 
 bool shard_layout(const ebt_catalog& c, const ebt_comm& cm, int64_t B, int32_t k,
@@ -825,6 +830,15 @@ bool shard_layout(const ebt_catalog& c, const ebt_comm& cm, int64_t B, int32_t k
   }
   L.off_pool = o;
   o = al(o + (size_t)D.B_pad * L.G * 4);
+  // the lead: only where the shared threshold drives the screen (ebt_cosine_screen_at_lead)
+  L.lead = L.ld_lead = 0;
+  if (L.tiles && D.flags == 0 && D.kprime <= SH_MERGE_WAVE_KMAX) {
+    const int64_t own = L.tiles < c.n / 256 ? L.tiles : c.n / 256;
+    L.lead = own == L.tiles ? shard_lead_tiles(D.B_pad, c.n, own) : 0;
+    L.ld_lead = 256 * L.lead;
+  }
+  L.off_lead = o;
+  o = al(o + (size_t)D.B_pad * L.ld_lead * 4);
   L.off_gsamp = o;
   o = al(o + (size_t)B * L.GJ * 4 * (R + 1));  // this shard's J largest, then every shard's
   L.off_theta = o;
@@ -1052,10 +1066,12 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
       if (rc) return rc;
     }
     if (own >= 1) {
-      int64_t stride = (c.n / 256) / own;
+      // the lead's tiles first, the rest evenly spaced over the shard after them
+      int64_t stride = (c.n / 256 - S.lead) / (own - S.lead);
       if (stride > 1 && stride % 2 == 0) stride -= 1;
-      rc = ebt_cosine_sample(qimg, qscale, L.B_pad, c.image, c.cscale, c.img_dtype, c.ld_img,
-                             c.n, c.d_pad, own, stride, pool, S.G, timer, st);
+      rc = ebt_cosine_sample_lead(qimg, qscale, L.B_pad, c.image, c.cscale, c.img_dtype,
+                                  c.ld_img, c.n, c.d_pad, own, stride, pool, S.G, S.lead,
+                                  (float*)(ws + S.off_lead), S.ld_lead, timer, st);
       if (rc) return rc;
     }
     float* send = gsamp;                          // [B][J + 1]
@@ -1088,11 +1104,12 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
   int32_t* ovf = (int32_t*)(ws + S.off_ovf);
   float* eps = (float*)(ws + S.off_eps);
   if (use_theta)
-    rc = ebt_cosine_screen_at(q64, qimg, qscale, qeps, B, L.B_pad, c.data, c.dtype, c.ld,
-                              c.gnorm64, c.image, c.cscale, c.img_dtype, c.ld_img, c.n, c.d,
-                              c.d_pad, c.row_offset, excl_off, excl_rows, L.k_eff, L.kprime,
-                              L.chunk, 0, ws + S.off_spass, S.screen_bytes, lv, lr, ovf, eps,
-                              theta, hits, timer, st);
+    rc = ebt_cosine_screen_at_lead(q64, qimg, qscale, qeps, B, L.B_pad, c.data, c.dtype, c.ld,
+                                   c.gnorm64, c.image, c.cscale, c.img_dtype, c.ld_img, c.n, c.d,
+                                   c.d_pad, c.row_offset, excl_off, excl_rows, L.k_eff, L.kprime,
+                                   L.chunk, 0, ws + S.off_spass, S.screen_bytes, lv, lr, ovf, eps,
+                                   theta, hits, S.lead, (const float*)(ws + S.off_lead),
+                                   S.ld_lead, timer, st);
   else
     rc = ebt_cosine_screen(q64, qimg, qscale, qeps, B, L.B_pad, c.data, c.dtype, c.ld, c.gnorm64,
                            c.image, c.cscale, c.img_dtype, c.ld_img, c.n, c.d, c.d_pad,

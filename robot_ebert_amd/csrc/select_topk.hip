@@ -1464,8 +1464,44 @@ __global__ __launch_bounds__(256) void spec_given_init_kernel(const float* __res
   }
 }
 
+// The same with a lead (a row-sharded catalog's sample lead, ebt_cosine_screen_at_lead): one wave
+// per query also takes its hits among the lead tiles' stored scores at the caller's threshold,
+// as pool_kth_kernel does at its own.
+__global__ __launch_bounds__(256) void spec_given_lead_kernel(const float* __restrict__ theta,
+                                                              int64_t B, int64_t B_pad,
+                                                              float* __restrict__ tspec,
+                                                              float* __restrict__ fv,
+                                                              int64_t* __restrict__ fi, int kprime,
+                                                              int* __restrict__ ovf, LeadArgs la) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B_pad) return;
+  if (lane == 0) ovf[b] = 0;
+  const float th = b < B ? theta[b] : __builtin_inff();
+  if (lane == 0) tspec[b] = th;
+  if (b < B)
+    for (int i = lane; i < kprime; i += 64) {
+      fv[b * kprime + i] = -__builtin_inff();
+      fi[b * kprime + i] = -1;
+    }
+  lead_hits_wave(la, b, th, ovf);   // padding rows: +inf, zero counts
+}
+
 int spec_given_init(const float* theta, int64_t B, int64_t B_pad, float* tspec, float* fv,
-                    int64_t* fi, int kprime, int* ovf, hipStream_t st) {
+                    int64_t* fi, int kprime, int* ovf, hipStream_t st, const float* lead_s,
+                    int64_t ld_lead, int lead, uint64_t* cand, int64_t ld_cand, int slots,
+                    uint8_t* counts, int64_t ld_counts) {
+  if (lead > 0) {
+    if (!lead_s || ld_lead < 256LL * lead || !cand || slots < 1 ||
+        ld_cand < (int64_t)lead * slots || !counts || ld_counts < lead) {
+      set_error("spec_given_init: bad lead arguments (lead=%d)", lead);
+      return EBT_EINVAL;
+    }
+    LeadArgs la{lead_s, ld_lead, lead, cand, ld_cand, slots, counts, ld_counts};
+    hipLaunchKernelGGL(spec_given_lead_kernel, dim3((unsigned)ceil_div(B_pad, 4)), dim3(256), 0,
+                       st, theta, B, B_pad, tspec, fv, fi, kprime, ovf, la);
+    return launch_check("spec_given_lead_kernel");
+  }
   const int64_t n_list = B * (int64_t)kprime;
   const int64_t n = n_list > B_pad ? n_list : B_pad;
   int64_t blocks = ceil_div(n, 256);

@@ -267,6 +267,9 @@ def shared_sample_tiles(n_global: int, world: int, B_pad: int) -> int:
     per = max(1, 256 // (B_pad // 256))
     if P // per * per >= 8:
         P = P // per * per
+    # less than one round of the persistent grid takes a round's time anyway: fill it
+    if P < per and per <= full // 6:
+        P = per
     return P if P >= 1 and world * P >= 8 else 0
 
 

@@ -223,7 +223,7 @@ def test_shared_threshold_plan():
                                              ctypes.byref(s), ctypes.byref(j),
                                              ctypes.byref(h)) == 0
         assert spec_rank(kp * 256 * t.value / n) == j.value
-    assert shared_sample_tiles(1_000_000, 8, 4096) == 8
+    assert shared_sample_tiles(1_000_000, 8, 4096) == 16     # one round of the sample GEMM
     assert shared_sample_tiles(1_000_000, 2, 4096) == 0       # 500K-row shards: own sample
     assert shared_sample_tiles(300_000, 2, 4096) == 16
     assert shared_sample_tiles(1_000_000, 1, 4096) == 0      # one rank: its own sample
