@@ -328,13 +328,16 @@ static bool spec_params(int64_t B_pad, int64_t n_rows, int32_t kprime, int64_t* 
 #ifndef EBT_SPEC_SAMPLE_DIV
 #define EBT_SPEC_SAMPLE_DIV 200
 #endif
-  // at least 32 tiles (round 5: C3 32 instead of 64, two rounds of the pool GEMM instead of four:
-  // +0.4 %, profiles/r5/ab/sample32_*), and at least one workgroup per CU (C2 keeps 64)
+  // at least 16 tiles (round 5: C3 16 instead of 64, one round of the pool GEMM instead of four:
+  // +0.4 % at 32, +0.5-0.8 % more at 16, profiles/r5/ab/sample32_*, sample16_*), and at least
+  // one workgroup per CU (C2 keeps 64)
 #ifndef EBT_SPEC_SAMPLE_MIN
-#define EBT_SPEC_SAMPLE_MIN 32  // (build knob for A/B)
+#define EBT_SPEC_SAMPLE_MIN 16  // (build knob for A/B)
 #endif
   const int64_t pdiv = full / EBT_SPEC_SAMPLE_DIV;
-  const int64_t pmin = fill > EBT_SPEC_SAMPLE_MIN ? fill : EBT_SPEC_SAMPLE_MIN;
+  // (k' > 512, the block merges: 32 -- their cost grows with the hits a smaller sample lets in)
+  const int64_t smin = merge_wave_fits(kprime) ? EBT_SPEC_SAMPLE_MIN : 32;
+  const int64_t pmin = fill > smin ? fill : smin;
   const int64_t pmax = pdiv > pmin ? (pdiv < 512 ? pdiv : 512) : pmin;
   P = P > pmax ? pmax : P;
   // whole rounds of workgroups: P x (query tiles) a multiple of 256 when that keeps >= 8 tiles

@@ -1202,6 +1202,138 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
   }
 }
 
+// ebt_merge_packed: the co-rank merge over the packed lists as they are -- each rank's entries
+// of query b (about k / R + the floor's band of them, instead of k slots mostly padding) staged
+// compactly in LDS, then every entry placed at j + (entries of the other lists before it), by
+// a binary search in each (score desc, row asc; equal keys ordered by list). A list found
+// unsorted flags the batch incomplete (the caller merges the full lists instead): the packed
+// lists come sorted from ebt_shard_pack.
+size_t merge_packed_lds(int R, int k) {
+  const size_t n = (size_t)R * k;
+  return n * 8 + ((n * 4 + 15) & ~(size_t)15) + (((size_t)(3 * R + 1) * 4 + 15) & ~(size_t)15);
+}
+
+__global__ __launch_bounds__(RTHREADS) void merge_packed_kernel(
+    const PackedSrc src, int R, int64_t B, int k, double* __restrict__ out_s,
+    int64_t* __restrict__ out_r, int32_t* __restrict__ incomplete) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nmax = R * k;
+  double* sc = (double*)smem;                                  // nmax
+  int32_t* rw = (int32_t*)(sc + nmax);                         // nmax
+  int* pst = (int*)((char*)rw + (((size_t)nmax * 4 + 15) & ~(size_t)15));  // R: packed start
+  int* len = pst + R;                                          // R: entries sent
+  int* off = len + R;                                          // R + 1: compact starts
+  __shared__ int wsum[RTHREADS / 64];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // 1. each rank's entries for this query (a list cut by its rank's capacity, or longer than
+  //    k, makes the batch incomplete), and their compact starts (a block scan over the ranks)
+  int carry = 0;
+  for (int r0 = 0; r0 < R; r0 += RTHREADS) {
+    const int r = r0 + tid;
+    int v = 0;
+    if (r < R) {
+      const uint32_t* st = pk_starts(src, r);
+      const int64_t s0 = st[b], s1 = st[b + 1];
+      const int64_t a = s0 < src.cap ? s0 : src.cap, e = s1 < src.cap ? s1 : src.cap;
+      v = (int)(e - a < k ? e - a : k);
+      pst[r] = (int)a;
+      len[r] = v;
+      if (s1 > src.cap || s1 - s0 > k) incomplete[0] = 1;
+    }
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int base = carry, total = 0;
+#pragma unroll
+    for (int w = 0; w < RTHREADS / 64; ++w) {
+      base += w < wave ? wsum[w] : 0;
+      total += wsum[w];
+    }
+    if (r < R) off[r] = base + incl - v;
+    carry += total;
+    __syncthreads();
+  }
+  if (tid == 0) off[R] = carry;
+  __syncthreads();
+  const int N = carry;
+  auto list_of = [&](int e) {   // the last list whose compact start is <= e (a non-empty one)
+    int lo = 0, hi = R - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (off[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  };
+  // 2. the entries into LDS, four per thread in flight
+  for (int e0 = tid; e0 < N; e0 += 4 * RTHREADS) {
+    double sv[4];
+    int32_t rv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * RTHREADS;
+      const int ec = e < N ? e : N - 1;
+      const int rr = list_of(ec);
+      const int64_t ix = (int64_t)pst[rr] + (ec - off[rr]);
+      sv[u] = pk_scores(src, rr, B)[ix];
+      rv[u] = pk_rows(src, rr, B)[ix];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * RTHREADS;
+      issued(sv[u]);
+      if (e < N) {
+        sc[e] = sv[u] != sv[u] ? -__builtin_inf() : sv[u];
+        rw[e] = rv[u];
+      }
+    }
+  }
+  __syncthreads();
+  // 3. sorted lists only
+  int bad = 0;
+  for (int e = tid; e < N; e += RTHREADS) {
+    const int rr = list_of(e);
+    if (e + 1 < off[rr] + len[rr] && mt_before(sc[e + 1], rw[e + 1], sc[e], rw[e])) bad = 1;
+  }
+  if (__syncthreads_or(bad)) {
+    if (tid == 0) incomplete[0] = 1;
+    return;
+  }
+  // 4. positions: j + the entries of every other list before this one
+  for (int e = tid; e < N; e += RTHREADS) {
+    const int rr = list_of(e);
+    const double es = sc[e];
+    const int64_t er = rw[e];
+    int pos = e - off[rr];
+    for (int o = 0; o < R && pos < k; ++o) {
+      if (o == rr) continue;
+      int lo = off[o], hi = off[o] + len[o];
+      const int o0 = lo;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const bool before = mt_before(sc[mid], rw[mid], es, er) ||
+                            (o < rr && sc[mid] == es && (int64_t)rw[mid] == er);
+        if (before) lo = mid + 1; else hi = mid;
+      }
+      pos += lo - o0;
+    }
+    if (pos < k) {
+      out_s[b * k + pos] = es;
+      out_r[b * k + pos] = er;
+    }
+  }
+  // fewer entries than k: padding takes the rest
+  for (int j = N + tid; j < k; j += RTHREADS) {
+    out_s[b * k + j] = __builtin_nan("");
+    out_r[b * k + j] = -1;
+  }
+}
+
 int merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, int32_t k,
                double* out_s, int64_t* out_r, hipStream_t st) {
   if (!scores || !rows || !out_s || !out_r || R < 1 || B < 0 || k < 1 || k > MERGE_CAP / 2) {
@@ -1244,11 +1376,31 @@ __global__ __launch_bounds__(SHARD_PACK_QPB) void shard_pack_count_kernel(
     const double tf = t_floor ? t_floor[b] : -__builtin_inf();
     const double* sr = scores + b * k;
     const int64_t* rr = rows + b * k;
-    int lo = 0, hi = k;  // the first position failing the predicate
+    // the first position failing the predicate (it holds on a prefix), by an 8-way search:
+    // each round trip loads up to 8 evenly spaced probes of [lo, hi) at once and keeps the gap
+    // between the last probe passing and the first failing (k = 100: three round trips, not 7)
+    int lo = 0, hi = k;
     while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (rr[mid] >= 0 && sr[mid] >= tf) lo = mid + 1;
-      else hi = mid;
+      const int span = hi - lo, m = span < 8 ? span : 8;
+      int p[8];
+      int64_t pr[8];
+      double ps[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        p[i] = lo + (int)((int64_t)(i + 1) * span / (m + 1));
+        const int pc = i < m ? p[i] : lo;
+        pr[i] = rr[pc];
+        ps[i] = sr[pc];
+      }
+      int nlo = lo, nhi = hi;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (i >= m) continue;
+        if (pr[i] >= 0 && ps[i] >= tf) nlo = p[i] + 1 > nlo ? p[i] + 1 : nlo;
+        else nhi = p[i] < nhi ? p[i] : nhi;
+      }
+      lo = nlo;
+      hi = nhi;
     }
     cnt = lo;
   }
@@ -1270,7 +1422,10 @@ __global__ __launch_bounds__(SHARD_PACK_QPB) void shard_pack_count_kernel(
   if (tid == 0) hdr[B + 1 + blockIdx.x] = (uint32_t)total;
 }
 
-__global__ __launch_bounds__(SHARD_PACK_QPB) void shard_pack_copy_kernel(
+// (launched with SHARD_PACK_COPY_THREADS threads: a workgroup's ~15 x 256 entries at C3/8 in
+// four rounds instead of fifteen)
+constexpr int SHARD_PACK_COPY_THREADS = 1024;
+__global__ __launch_bounds__(SHARD_PACK_COPY_THREADS) void shard_pack_copy_kernel(
     const double* __restrict__ scores, const int64_t* __restrict__ rows, int64_t B, int k,
     int64_t cap, char* __restrict__ send) {
   __shared__ uint32_t lst[SHARD_PACK_QPB + 1];
@@ -1295,7 +1450,7 @@ __global__ __launch_bounds__(SHARD_PACK_QPB) void shard_pack_copy_kernel(
   const uint32_t g0 = gbase, n = lst[nq];
   if (tid < nq) hdr[q0 + tid] = g0 + lst[tid];
   if (blockIdx.x == gridDim.x - 1 && tid == 0) hdr[B] = g0 + n;
-  for (uint32_t t = tid; t < n; t += SHARD_PACK_QPB) {
+  for (uint32_t t = tid; t < n; t += SHARD_PACK_COPY_THREADS) {
     int lo = 0, hi = nq - 1;  // the last query whose start <= t
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
@@ -1845,8 +2000,8 @@ extern "C" int ebt_shard_pack(const double* scores, const int64_t* rows, int64_t
                      rows, B, k, t_floor, (uint32_t*)send);
   int rc = launch_check("shard_pack_count_kernel");
   if (rc) return rc;
-  hipLaunchKernelGGL(shard_pack_copy_kernel, dim3(grid), dim3(SHARD_PACK_QPB), 0, st, scores, rows,
-                     B, k, cap, (char*)send);
+  hipLaunchKernelGGL(shard_pack_copy_kernel, dim3(grid), dim3(SHARD_PACK_COPY_THREADS), 0, st,
+                     scores, rows, B, k, cap, (char*)send);
   return launch_check("shard_pack_copy_kernel");
 }
 
@@ -1860,13 +2015,12 @@ extern "C" int ebt_merge_packed(const void* recv, int32_t R, int64_t B, int32_t 
               (long long)B, k, (long long)cap, MERGE_CORANK_CAP);
     return EBT_EINVAL;
   }
-  const int P = next_pow2_h(R * k);
-  const size_t lds = merge_corank_lds(R, P);
-  set_max_lds((const void*)merge_topk_corank_kernel<PackedSrc>, (int)lds);
+  const size_t lds = merge_packed_lds(R, k);
+  set_max_lds((const void*)merge_packed_kernel, (int)lds);
   const PackedSrc src{(const char*)recv, (int64_t)ebt_shard_pack_bytes(B, cap), cap};
-  hipLaunchKernelGGL(merge_topk_corank_kernel<PackedSrc>, dim3((unsigned)B), dim3(RTHREADS), lds,
-                     (hipStream_t)stream, src, R, B, k, P, out_scores, out_rows, incomplete);
-  return launch_check("merge_topk_corank_kernel");
+  hipLaunchKernelGGL(merge_packed_kernel, dim3((unsigned)B), dim3(RTHREADS), lds,
+                     (hipStream_t)stream, src, R, B, k, out_scores, out_rows, incomplete);
+  return launch_check("merge_packed_kernel");
 }
 
 // ------------------------------------------------------------------------ floor all-gather --

@@ -197,7 +197,7 @@ def test_spec_plan_poisson_rank():
         lam = kp * 256 * P / n
         assert poisson.sf(j - 1, lam) <= 1e-6 < poisson.sf(j - 2, lam), (n, P, j)
         assert H >= j * n / (256 * P)
-    assert sp(4096, 1_000_000, 200)[:3] == (32, 121, 12)   # round 5: 32 tiles (2 pool rounds)
+    assert sp(4096, 1_000_000, 200)[:3] == (16, 243, 9)    # round 5: 16 tiles (one pool round)
     assert sp(4096, 125_000, 200)[0] == 16          # one round of 256 workgroups
     assert sp(1024, 100_000, 120)[0] == 64          # C2: one workgroup per CU (64 tiles x 4)
     assert sp(100, 1_000_000, 104)[0] == 0          # B_pad = 128: the 128-tile kernel, no spec
