@@ -221,9 +221,9 @@ __device__ __forceinline__ double guard_norm(double nrm) {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// ebt_shard_pack's buffer: u32 starts[B + 1], u32 block totals[ceil(B / 256)] (scratch of the
+// ebt_shard_pack's buffer: u32 starts[B + 1], u32 block totals[ceil(B / SHARD_PACK_QPB)] (scratch of the
 // pack, sent along), 16-byte aligned; then f64 scores[cap]; then i32 rows[cap]
-constexpr int SHARD_PACK_QPB = 256;  // queries per pack workgroup
+constexpr int SHARD_PACK_QPB = 64;  // queries per pack workgroup (one wave counts them)
 __host__ __device__ inline int64_t shard_pack_hdr_bytes(int64_t B) {
   return ((B + 1 + (B + SHARD_PACK_QPB - 1) / SHARD_PACK_QPB) * 4 + 15) & ~(int64_t)15;
 }

@@ -1422,9 +1422,9 @@ __global__ __launch_bounds__(SHARD_PACK_QPB) void shard_pack_count_kernel(
   if (tid == 0) hdr[B + 1 + blockIdx.x] = (uint32_t)total;
 }
 
-// (launched with SHARD_PACK_COPY_THREADS threads: a workgroup's ~15 x 256 entries at C3/8 in
-// four rounds instead of fifteen)
-constexpr int SHARD_PACK_COPY_THREADS = 1024;
+// (64 queries per workgroup -- 64 workgroups at B = 4096, not 16 -- and SHARD_PACK_COPY_THREADS
+// threads: a workgroup's ~15 x 64 entries at C3/8 in four rounds)
+constexpr int SHARD_PACK_COPY_THREADS = 256;
 __global__ __launch_bounds__(SHARD_PACK_COPY_THREADS) void shard_pack_copy_kernel(
     const double* __restrict__ scores, const int64_t* __restrict__ rows, int64_t B, int k,
     int64_t cap, char* __restrict__ send) {
