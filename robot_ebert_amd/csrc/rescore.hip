@@ -1213,7 +1213,11 @@ size_t merge_packed_lds(int R, int k) {
   return n * 8 + ((n * 4 + 15) & ~(size_t)15) + (((size_t)(3 * R + 1) * 4 + 15) & ~(size_t)15);
 }
 
-__global__ __launch_bounds__(RTHREADS) void merge_packed_kernel(
+// one wave per query: 4096 queries all resident at once (16 workgroups per CU by their ~10 KiB of
+// LDS at C3/8) instead of two rounds of 256-thread workgroups, each query's chain of dependent
+// loads paid once
+constexpr int MP_THREADS = 64;
+__global__ __launch_bounds__(MP_THREADS) void merge_packed_kernel(
     const PackedSrc src, int R, int64_t B, int k, double* __restrict__ out_s,
     int64_t* __restrict__ out_r, int32_t* __restrict__ incomplete) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1223,13 +1227,13 @@ __global__ __launch_bounds__(RTHREADS) void merge_packed_kernel(
   int* pst = (int*)((char*)rw + (((size_t)nmax * 4 + 15) & ~(size_t)15));  // R: packed start
   int* len = pst + R;                                          // R: entries sent
   int* off = len + R;                                          // R + 1: compact starts
-  __shared__ int wsum[RTHREADS / 64];
+  __shared__ int wsum[MP_THREADS / 64];
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // 1. each rank's entries for this query (a list cut by its rank's capacity, or longer than
   //    k, makes the batch incomplete), and their compact starts (a block scan over the ranks)
   int carry = 0;
-  for (int r0 = 0; r0 < R; r0 += RTHREADS) {
+  for (int r0 = 0; r0 < R; r0 += MP_THREADS) {
     const int r = r0 + tid;
     int v = 0;
     if (r < R) {
@@ -1251,7 +1255,7 @@ __global__ __launch_bounds__(RTHREADS) void merge_packed_kernel(
     __syncthreads();
     int base = carry, total = 0;
 #pragma unroll
-    for (int w = 0; w < RTHREADS / 64; ++w) {
+    for (int w = 0; w < MP_THREADS / 64; ++w) {
       base += w < wave ? wsum[w] : 0;
       total += wsum[w];
     }
@@ -1271,12 +1275,12 @@ __global__ __launch_bounds__(RTHREADS) void merge_packed_kernel(
     return lo;
   };
   // 2. the entries into LDS, four per thread in flight
-  for (int e0 = tid; e0 < N; e0 += 4 * RTHREADS) {
+  for (int e0 = tid; e0 < N; e0 += 4 * MP_THREADS) {
     double sv[4];
     int32_t rv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * RTHREADS;
+      const int e = e0 + u * MP_THREADS;
       const int ec = e < N ? e : N - 1;
       const int rr = list_of(ec);
       const int64_t ix = (int64_t)pst[rr] + (ec - off[rr]);
@@ -1285,7 +1289,7 @@ __global__ __launch_bounds__(RTHREADS) void merge_packed_kernel(
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * RTHREADS;
+      const int e = e0 + u * MP_THREADS;
       issued(sv[u]);
       if (e < N) {
         sc[e] = sv[u] != sv[u] ? -__builtin_inf() : sv[u];
@@ -1296,7 +1300,7 @@ __global__ __launch_bounds__(RTHREADS) void merge_packed_kernel(
   __syncthreads();
   // 3. sorted lists only
   int bad = 0;
-  for (int e = tid; e < N; e += RTHREADS) {
+  for (int e = tid; e < N; e += MP_THREADS) {
     const int rr = list_of(e);
     if (e + 1 < off[rr] + len[rr] && mt_before(sc[e + 1], rw[e + 1], sc[e], rw[e])) bad = 1;
   }
@@ -1305,7 +1309,7 @@ __global__ __launch_bounds__(RTHREADS) void merge_packed_kernel(
     return;
   }
   // 4. positions: j + the entries of every other list before this one
-  for (int e = tid; e < N; e += RTHREADS) {
+  for (int e = tid; e < N; e += MP_THREADS) {
     const int rr = list_of(e);
     const double es = sc[e];
     const int64_t er = rw[e];
@@ -1328,7 +1332,7 @@ __global__ __launch_bounds__(RTHREADS) void merge_packed_kernel(
     }
   }
   // fewer entries than k: padding takes the rest
-  for (int j = N + tid; j < k; j += RTHREADS) {
+  for (int j = N + tid; j < k; j += MP_THREADS) {
     out_s[b * k + j] = __builtin_nan("");
     out_r[b * k + j] = -1;
   }
@@ -2018,7 +2022,7 @@ extern "C" int ebt_merge_packed(const void* recv, int32_t R, int64_t B, int32_t 
   const size_t lds = merge_packed_lds(R, k);
   set_max_lds((const void*)merge_packed_kernel, (int)lds);
   const PackedSrc src{(const char*)recv, (int64_t)ebt_shard_pack_bytes(B, cap), cap};
-  hipLaunchKernelGGL(merge_packed_kernel, dim3((unsigned)B), dim3(RTHREADS), lds,
+  hipLaunchKernelGGL(merge_packed_kernel, dim3((unsigned)B), dim3(MP_THREADS), lds,
                      (hipStream_t)stream, src, R, B, k, out_scores, out_rows, incomplete);
   return launch_check("merge_packed_kernel");
 }
