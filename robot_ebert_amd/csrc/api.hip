@@ -978,8 +978,12 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
     const int64_t g0 = first ? lead : 0;  // groups of the lead in front of this segment's
     const int64_t cap_rows = seg_cap - g0 * L.group_rows;
     const double room = (cap - kprime) / f_spread;
+    // after r0 rows the raised threshold keeps about k + (the 2 eps band) of every r0 rows; k'
+    // budgets that band at k' - k, so (k + k') / 2 per r0 rows still leaves the band twice its
+    // budget (round 5; k' per r0 before: C3 took four filter launches per batch instead of three)
+    const double kept = 0.5 * ((double)k + (double)kprime);
     double rate = spec_hits / (double)n_rows;
-    if (!first && (double)kprime / (double)r0 < rate) rate = (double)kprime / (double)r0;
+    if (!first && kept / (double)r0 < rate) rate = kept / (double)r0;
     int64_t seg = (int64_t)(room / (rate > 1e-12 ? rate : 1e-12));
     seg = (seg + 255) / 256 * 256;
     // whole rounds of the persistent grid (every segment but a remainder): no partly idle
