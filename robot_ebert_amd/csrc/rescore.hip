@@ -930,23 +930,21 @@ __device__ __forceinline__ bool mt_before(double xs, int64_t xr, double es, int6
 }
 
 size_t merge_corank_lds(int R, int P) {
-  return (size_t)P * 16 + RTHREADS * 16 + (((size_t)(4 * R + 1) * 4 + 15) & ~(size_t)15);
+  return (size_t)P * 16 + RTHREADS * 16 + (((size_t)(2 * R + 1) * 4 + 15) & ~(size_t)15);
 }
 
-// The lists' sources. DenseSrc: [R][B][k] f64 scores + i64 rows (row < 0 = padding).
-// PackedSrc: every rank's packed list of ebt_shard_pack (one all-gathered byte buffer, `stride`
-// bytes per rank): u32 starts[B + 1], then f64 scores[cap], then i32 rows[cap]; query b's
-// entries are [starts[b], starts[b + 1]) clipped to cap (the rest was not sent), the positions
-// past them padding.
+// The lists' sources. DenseSrc (merge_topk_corank_kernel): [R][B][k] f64 scores + i64 rows
+// (row < 0 = padding). PackedSrc (merge_packed_kernel): every rank's packed list of
+// ebt_shard_pack (one all-gathered byte buffer, `stride` bytes per rank): u32 starts[B + 1], then
+// f64 scores[cap], then i32 rows[cap]; query b's entries are [starts[b], starts[b + 1]) clipped
+// to cap (the rest was not sent).
 struct DenseSrc {
   const double* scores;
   const int64_t* rows;
-  static constexpr bool packed = false;
 };
 struct PackedSrc {
   const char* recv;
   int64_t stride, cap;
-  static constexpr bool packed = true;
 };
 
 __device__ __forceinline__ const uint32_t* pk_starts(const PackedSrc& p, int r) {
@@ -962,7 +960,7 @@ __device__ __forceinline__ const int32_t* pk_rows(const PackedSrc& p, int r, int
 template <class Src>
 __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
     const Src src, int R, int64_t B, int k, int P, double* __restrict__ out_s,
-    int64_t* __restrict__ out_r, int32_t* __restrict__ incomplete) {
+    int64_t* __restrict__ out_r) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = R * k;
   double* sc = (double*)smem;
@@ -972,21 +970,6 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
   int* plen = (int*)(red_r + RTHREADS / 2);
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x;
-  // packed lists: each rank's start and length for this query (LDS, after plen / cst); a list
-  // cut by its rank's capacity makes the query incomplete (the caller then merges the full lists)
-  int* pst = plen + 2 * R + 1;
-  int* pcn = pst + R;
-  if constexpr (Src::packed) {
-    for (int r = tid; r < R; r += RTHREADS) {
-      const uint32_t* st = pk_starts(src, r);
-      const int64_t s0 = st[b], s1 = st[b + 1];
-      const int64_t a = s0 < src.cap ? s0 : src.cap, e = s1 < src.cap ? s1 : src.cap;
-      pst[r] = (int)a;
-      pcn[r] = (int)(e - a < k ? e - a : k);
-      if (s1 > src.cap || s1 - s0 > k) incomplete[0] = 1;
-    }
-    __syncthreads();
-  }
   // four entries per thread in flight (a loop over e would wait for each load in turn: the
   // compiler peels the trip count's remainder into a serial loop)
   for (int e0 = tid; e0 < n; e0 += 4 * RTHREADS) {
@@ -997,18 +980,9 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
       const int e = e0 + u * RTHREADS;
       const int ec = e < n ? e : n - 1;
       const int rr = ec / k, j = ec - rr * k;
-      if constexpr (Src::packed) {
-        // a clamped index loaded unconditionally, masked afterwards (all loads in flight)
-        int64_t ix = (int64_t)pst[rr] + (j < pcn[rr] ? j : 0);
-        ix = ix < src.cap ? ix : src.cap - 1;
-        rv[u] = pk_rows(src, rr, B)[ix];
-        sv[u] = pk_scores(src, rr, B)[ix];
-        if (j >= pcn[rr]) rv[u] = -1;
-      } else {
-        const int64_t off = ((int64_t)rr * B + b) * k + j;
-        rv[u] = src.rows[off];
-        sv[u] = src.scores[off];
-      }
+      const int64_t off = ((int64_t)rr * B + b) * k + j;
+      rv[u] = src.rows[off];
+      sv[u] = src.scores[off];
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1351,7 +1325,7 @@ int merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t B, 
     const size_t lds = merge_corank_lds(R, P);
     set_max_lds((const void*)merge_topk_corank_kernel<DenseSrc>, (int)lds);
     hipLaunchKernelGGL(merge_topk_corank_kernel<DenseSrc>, dim3((unsigned)B), dim3(RTHREADS),
-                       lds, st, DenseSrc{scores, rows}, R, B, k, P, out_s, out_r, nullptr);
+                       lds, st, DenseSrc{scores, rows}, R, B, k, P, out_s, out_r);
     return launch_check("merge_topk_corank_kernel");
   }
   const int P = next_pow2_h((int)(n < MERGE_CAP ? n : MERGE_CAP));
