@@ -392,12 +392,18 @@ static int64_t round_tiles(int64_t B_pad) {
   const int64_t q = B_pad / 256, cus = gemm_cus();
   return (q > 0 && cus % q == 0) ? cus / q : 0;
 }
-static int64_t spec_lead_tiles(int64_t B_pad, int64_t n_rows, int64_t sample_tiles) {
+// (the room for it regardless of ebt_spec_lead, so that a workspace sized before the knob
+// changes still fits: the layout's offsets never depend on the knob)
+static int64_t spec_lead_room(int64_t B_pad, int64_t n_rows, int64_t sample_tiles) {
   const int64_t rt = round_tiles(B_pad);
-  if (rt <= 1 || !spec_lead_flag().load(std::memory_order_relaxed)) return 0;
+  if (rt <= 1) return 0;
   const int64_t lead = ceil_div(n_rows, 256) % rt;
   // a lead of at most half the sample (its strided part keeps the spread), and full tiles only
   return (lead <= sample_tiles / 2 && lead * 256 <= n_rows - 256) ? lead : 0;
+}
+static int64_t spec_lead_tiles(int64_t B_pad, int64_t n_rows, int64_t sample_tiles) {
+  return spec_lead_flag().load(std::memory_order_relaxed)
+             ? spec_lead_room(B_pad, n_rows, sample_tiles) : 0;
 }
 
 // A row-sharded catalog's sample lead (ebt_cosine_sample_lead / ebt_cosine_screen_at_lead): the
@@ -407,11 +413,15 @@ static int64_t spec_lead_tiles(int64_t B_pad, int64_t n_rows, int64_t sample_til
 // catalog, so a shard's lead may take all but 4 of its sample tiles (C3 on 8 ranks: 489 tiles
 // per shard, 16 sample tiles of which the first 9 are the lead; the filter's 31st round of 9 x 16
 // tiles disappears).
-int64_t shard_lead_tiles(int64_t B_pad, int64_t n_rows, int64_t sample_tiles) {
+int64_t shard_lead_room(int64_t B_pad, int64_t n_rows, int64_t sample_tiles) {
   const int64_t rt = round_tiles(B_pad);
-  if (rt <= 1 || !spec_lead_flag().load(std::memory_order_relaxed)) return 0;
+  if (rt <= 1) return 0;
   const int64_t lead = ceil_div(n_rows, 256) % rt;
   return (lead <= sample_tiles - 4 && lead * 256 <= n_rows - 256) ? lead : 0;
+}
+int64_t shard_lead_tiles(int64_t B_pad, int64_t n_rows, int64_t sample_tiles) {
+  return spec_lead_flag().load(std::memory_order_relaxed)
+             ? shard_lead_room(B_pad, n_rows, sample_tiles) : 0;
 }
 
 static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kprime,
@@ -469,7 +479,7 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
   }
   if (L.spec && !(flags & EBT_FLAG_THETA)) {
     L.spec_lead = spec_lead_tiles(B_pad, n_rows, L.spec_tiles);
-    L.ld_lead = L.spec_lead * 256;
+    L.ld_lead = spec_lead_room(B_pad, n_rows, L.spec_tiles) * 256;
   }
   if (L.spec) {
     const int64_t rt = round_tiles(B_pad);
@@ -523,7 +533,7 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
     o = align_up(o + (size_t)B_pad * 4);
   }
   L.off_lead = o;
-  if (L.spec_lead) o = align_up(o + (size_t)B_pad * L.ld_lead * 4);
+  if (L.ld_lead) o = align_up(o + (size_t)B_pad * L.ld_lead * 4);
   L.bytes = o;
   return L;
 }

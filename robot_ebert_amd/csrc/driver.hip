@@ -345,6 +345,7 @@ bool valid_catalog(const ebt_catalog* c) {
 int screen_image(const void*, int, int64_t, int32_t, int64_t, const double*, int, int, void*,
                  int32_t, hipStream_t, unsigned int* err_max);
 int64_t shard_lead_tiles(int64_t B_pad, int64_t n_rows, int64_t sample_tiles);
+int64_t shard_lead_room(int64_t B_pad, int64_t n_rows, int64_t sample_tiles);
 
 }  // namespace ebt
 
@@ -834,8 +835,9 @@ bool shard_layout(const ebt_catalog& c, const ebt_comm& cm, int64_t B, int32_t k
   L.lead = L.ld_lead = 0;
   if (L.tiles && D.flags == 0 && D.kprime <= SH_MERGE_WAVE_KMAX) {
     const int64_t own = L.tiles < c.n / 256 ? L.tiles : c.n / 256;
+    // (the room regardless of ebt_spec_lead: offsets never depend on the knob)
     L.lead = own == L.tiles ? shard_lead_tiles(D.B_pad, c.n, own) : 0;
-    L.ld_lead = 256 * L.lead;
+    L.ld_lead = own == L.tiles ? 256 * shard_lead_room(D.B_pad, c.n, own) : 0;
   }
   L.off_lead = o;
   o = al(o + (size_t)D.B_pad * L.ld_lead * 4);

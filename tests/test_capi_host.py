@@ -236,3 +236,24 @@ def test_shared_threshold_plan():
         for r in range(world):
             a, b = shard_range(1_000_003, r, world)
             assert (b - a) // 256 >= P
+
+
+def test_workspace_size_does_not_depend_on_the_lead_knob():
+    """ebt_spec_lead changes whether the speculative sample's lead is used, never the workspace
+    layout: a workspace sized with the knob in one state still fits the other (round 5)."""
+    from robot_ebert_amd import _lib
+    lib = _lib.load()
+    prev = lib.ebt_spec_lead(1)
+    try:
+        for (B, n, kp) in [(1024, 100_000, 128), (4096, 1_000_000, 200), (4096, 125_000, 200)]:
+            on = lib.ebt_cosine_topk_workspace(B, B, n, kp, 1 << 20, 0)
+            lead_on = lib.ebt_cosine_topk_spec_lead(B, B, n, kp, 0)
+            lib.ebt_spec_lead(0)
+            off = lib.ebt_cosine_topk_workspace(B, B, n, kp, 1 << 20, 0)
+            assert lib.ebt_cosine_topk_spec_lead(B, B, n, kp, 0) == 0
+            lib.ebt_spec_lead(1)
+            assert on == off > 0, (B, n, on, off)
+            assert lead_on >= 0
+        assert lib.ebt_cosine_topk_spec_lead(1024, 1024, 100_000, 128, 0) == 7   # C2
+    finally:
+        lib.ebt_spec_lead(prev)
