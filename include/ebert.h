@@ -354,7 +354,9 @@ int ebt_cosine_topk_prepared(const double* q64, const void* qimg, const float* q
  * device matrix and a caller-provided device STATE buffer of ebt_catalog_state_bytes() bytes
  * (float64 guarded row norms, float32 inverse norms, and the f16 screening image unless the
  * matrix itself is the MFMA operand: f16 / bf16 with d, ld % 64 == 0). Immutable afterwards;
- * the struct and the state buffer must outlive every call that uses them. */
+ * the struct and the state buffer must outlive every call that uses them. For a non-native
+ * catalog (f32 / f64) ebt_catalog_init waits for `stream` once, to read back u_cat, the largest
+ * row error of the image its kernel measured (0.3.1); a native catalog's init stays asynchronous. */
 typedef struct ebt_catalog {
   const void* data;       /* [n][ld] of dtype (device, caller-owned)                        */
   int32_t dtype, d;
