@@ -150,13 +150,14 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
-// The butterflies of NR (1, 2 or 4) values at once, each bitwise equal to its own
-// wave_sum_f64: the first log2(NR) levels pair values up (pair_sum32 / pair_sum16), so that
+// The butterflies of NR (1, 2, 4 or 8) values at once, each bitwise equal to its own
+// wave_sum_f64: the first log2(NR) levels pair values up (pair_sum32 / pair_sum16 / DPP), so that
 // from then on each lane carries one value through the remaining levels. Returns, in every lane,
-// the total of value (lane >> 5) (NR = 2) or (lane >> 4) (NR = 4): wave_rows_owner<NR>(lane).
+// the total of value (lane >> 5) (NR = 2), (lane >> 4) (NR = 4) or (lane >> 3) (NR = 8):
+// wave_rows_owner<NR>(lane).
 template <int NR>
 __device__ __forceinline__ double wave_sum_f64_rows(const double (&s)[NR]) {
-  static_assert(NR == 1 || NR == 2 || NR == 4, "NR");
+  static_assert(NR == 1 || NR == 2 || NR == 4 || NR == 8, "NR");
   const int lane = (int)(threadIdx.x & (kWave - 1));
   double v;
   if constexpr (NR == 1) {
@@ -164,12 +165,32 @@ __device__ __forceinline__ double wave_sum_f64_rows(const double (&s)[NR]) {
   } else if constexpr (NR == 2) {
     v = pair_sum32_f64(s[0], s[1]);  // lanes < 32: value 0, lanes >= 32: value 1
     v += xor16_f64(v, lane);
-  } else {
+    v += dpp_f64<0x128>(v);
+  } else if constexpr (NR == 4) {
     const double t0 = pair_sum32_f64(s[0], s[2]);  // lanes < 32: 0, >= 32: 2
     const double t1 = pair_sum32_f64(s[1], s[3]);  // lanes < 32: 1, >= 32: 3
     v = pair_sum16_f64(t0, t1);                    // 16-lane rows: 0, 1, 2, 3
+    v += dpp_f64<0x128>(v);
+  } else {
+    // levels 32 and 16 pair the eight values into two per lane (u0: values 0, 2, 4, 6 by
+    // 16-lane row; u1: 1, 3, 5, 7), level 8 (row_ror:8 = xor 8) keeps u0 in the lanes with
+    // bit 3 clear and u1 in the others: lane l then carries value l >> 3
+    const double t0 = pair_sum32_f64(s[0], s[4]);
+    const double t1 = pair_sum32_f64(s[1], s[5]);
+    const double t2 = pair_sum32_f64(s[2], s[6]);
+    const double t3 = pair_sum32_f64(s[3], s[7]);
+    const double u0 = pair_sum16_f64(t0, t2);
+    const double u1 = pair_sum16_f64(t1, t3);
+    const double a = dpp_f64<0x128>(u0), b = dpp_f64<0x128>(u1);
+    v = (lane & 8) ? u1 + b : u0 + a;
+    // level 4 inside each 8-lane group (its neighbours hold other values, so row_ror:4 would
+    // cross into them): lane ^ 4 as row_shl:4 for lanes with bit 2 clear, row_shr:4 otherwise
+    const double up = dpp_f64<0x104>(v), dn = dpp_f64<0x114>(v);
+    v += (lane & 4) ? dn : up;
+    v += dpp_f64<0x4E>(v);
+    v += dpp_f64<0xB1>(v);
+    return v;
   }
-  v += dpp_f64<0x128>(v);
   v += dpp_f64<0x124>(v);
   v += dpp_f64<0x4E>(v);
   v += dpp_f64<0xB1>(v);
@@ -177,7 +198,7 @@ __device__ __forceinline__ double wave_sum_f64_rows(const double (&s)[NR]) {
 }
 template <int NR>
 __device__ __forceinline__ int wave_rows_owner(int lane) {
-  return NR == 1 ? 0 : (NR == 2 ? lane >> 5 : lane >> 4);
+  return NR == 1 ? 0 : (NR == 2 ? lane >> 5 : (NR == 4 ? lane >> 4 : lane >> 3));
 }
 
 // Inclusive wave scans of a 32-bit value in DPP moves (no LDS): Hillis-Steele steps row_shr 1, 2,

@@ -123,8 +123,13 @@ __device__ __forceinline__ double chunk_dot_reg(const double (&q)[PER], uint4 ra
 #ifndef EBT_RESCORE_NR_WIDE
 #define EBT_RESCORE_NR_WIDE 2  // rows per trip at 3..6 chunks per lane (build knob for A/B)
 #endif
+#ifndef EBT_RESCORE_NR_NARROW
+#define EBT_RESCORE_NR_NARROW 4  // rows per trip at <= 2 chunks per lane (build knob for A/B)
+#endif
 template <int NU>
-constexpr int rescore_rows_per_trip() { return NU <= 2 ? 4 : (NU <= 6 ? EBT_RESCORE_NR_WIDE : 1); }
+constexpr int rescore_rows_per_trip() {
+  return NU <= 2 ? EBT_RESCORE_NR_NARROW : (NU <= 6 ? EBT_RESCORE_NR_WIDE : 1);
+}
 
 // NU = 0: the query staged in LDS (any d), two rows per wave round trip. NU > 0 (VEC, d / PER
 // <= 64 NU 16-byte chunks): each lane keeps its chunks' query values (chunks lane + 64 u) in
