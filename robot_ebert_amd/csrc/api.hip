@@ -606,14 +606,14 @@ static int head_topk(const WsLayout& L, char* ws, const void* qimg, const float*
 // fewer per step. Timed and row-counted as ebt_rescore.
 int rescore_sharded(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
                     int64_t ld, const double* gnorm64, int64_t row_offset, const float* cand_vals,
-                    const int64_t* cand_rows_global, int32_t kprime, int32_t k, int64_t n_rows,
+                    const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows,
                     const float* eps, const double* t_floor, double* out_s, int64_t* out_r,
                     int32_t* certified, const int* ovf, const float* theta, void* timer,
-                    hipStream_t st) {
+                    hipStream_t st, int64_t list_base) {
   StageScope sc(timer, EBT_STAGE_RESCORE, st);
-  return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, cand_vals, cand_rows_global,
+  return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, cand_vals, cand_rows,
                  kprime, k, n_rows, eps, t_floor, out_s, out_r, certified, st, ovf, 0,
-                 timer_rows(timer), row_offset, theta);
+                 timer_rows(timer), list_base, theta);
 }
 
 }  // namespace ebt
@@ -1281,6 +1281,55 @@ int ebt_cosine_screen_at_lead(const double* q64, const void* qimg, const float* 
   if (rc) return rc;
   return export_list(list_rows, B, kprime, row_offset, so.ovf, so.eps, ovf_out, eps_out, st);
 }
+
+}  // extern "C"
+
+namespace ebt {
+// The sharded step's screen at the shared threshold without ebt_cosine_screen_at_lead's export
+// launch (driver.hip): the list keeps LOCAL rows (the sharded rescore reads them with list base
+// 0), and the screen's own overflow flags and eps stay where the pipeline wrote them (*ovf_dev,
+// *eps_dev point into the workspace / the prepared queries).
+int screen_at_local(const double* q64, const void* qimg, const float* qscale, const float* eps,
+                    int64_t B, int64_t B_pad, const void* cat, int dtype, int64_t ld,
+                    const double* gnorm64, const void* cimg, const float* cscale, int img_dtype,
+                    int32_t ld_img, int64_t n_rows, int32_t d, int32_t d_pad, int64_t row_offset,
+                    const int64_t* excl_off, const int64_t* excl_rows, int32_t k, int32_t kprime,
+                    int64_t chunk_rows, void* workspace, size_t ws_bytes, float* list_vals,
+                    int64_t* list_rows, const float* theta, double hits, int64_t lead,
+                    const float* lead_scores, int64_t ld_lead, const int** ovf_dev,
+                    const float** eps_dev, void* timer, hipStream_t st) {
+  const int flags = EBT_FLAG_THETA;
+  PipeArgs a{q64, qimg, qscale, eps, B, B_pad, cat, dtype, ld, gnorm64, cimg, cscale,
+             img_dtype, ld_img, n_rows, d, d_pad, row_offset, excl_off, excl_rows, k, kprime,
+             chunk_rows, flags};
+  a.theta = theta;
+  a.hits = hits;
+  a.lead = lead;
+  a.lead_s = lead_scores;
+  a.ld_lead = ld_lead;
+  int rc = check_pipe(a, "screen_at_local");
+  if (rc) return rc;
+  if (!workspace || !list_vals || !list_rows || !theta || !ovf_dev || !eps_dev ||
+      !merge_wave_fits(kprime) || !(hits >= 0.0) || lead < 0 ||
+      (lead > 0 && (!lead_scores || ld_lead < 256 * lead || 256 * lead >= n_rows))) {
+    set_error("screen_at_local: bad arguments (kprime=%d, lead=%lld)", kprime, (long long)lead);
+    return EBT_EINVAL;
+  }
+  const WsLayout L = ws_layout(B, B_pad, n_rows, kprime, chunk_rows, flags);
+  if (ws_bytes < L.bytes) {
+    set_error("screen_at_local: workspace %zu < %zu bytes", ws_bytes, L.bytes);
+    return EBT_ENOMEM;
+  }
+  ScreenOut so{};
+  rc = run_screen(a, L, (char*)workspace, list_vals, list_rows, timer, st, &so);
+  if (rc) return rc;
+  *ovf_dev = so.ovf;
+  *eps_dev = so.eps;
+  return EBT_OK;
+}
+}  // namespace ebt
+
+extern "C" {
 
 int ebt_cosine_sample(const void* qimg, const float* qscale, int64_t B_pad, const void* cimg,
                       const float* cscale, int img_dtype, int32_t ld_img, int64_t n_rows,

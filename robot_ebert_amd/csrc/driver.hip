@@ -31,6 +31,12 @@ int large_topk(const double*, int64_t, int32_t, const void*, int, int64_t, const
 int rescore_sharded(const double*, int64_t, int32_t, const void*, int, int64_t, const double*,
                     int64_t, const float*, const int64_t*, int32_t, int32_t, int64_t, const float*,
                     const double*, double*, int64_t*, int32_t*, const int*, const float*, void*,
+                    hipStream_t, int64_t list_base);
+int screen_at_local(const double*, const void*, const float*, const float*, int64_t, int64_t,
+                    const void*, int, int64_t, const double*, const void*, const float*, int,
+                    int32_t, int64_t, int32_t, int32_t, int64_t, const int64_t*, const int64_t*,
+                    int32_t, int32_t, int64_t, void*, size_t, float*, int64_t*, const float*,
+                    double, int64_t, const float*, int64_t, const int**, const float**, void*,
                     hipStream_t);
 int pool_kth(const float*, int64_t, int64_t, int64_t, int, int, float*, hipStream_t, float*,
              int64_t*, int, int*, const float*, int64_t, int, uint64_t*, int64_t, int, uint8_t*,
@@ -1105,13 +1111,16 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
   int64_t* lr = (int64_t*)(ws + S.off_lr);
   int32_t* ovf = (int32_t*)(ws + S.off_ovf);
   float* eps = (float*)(ws + S.off_eps);
+  // at the shared threshold the list keeps LOCAL rows and the screen's overflow flags and eps
+  // are read where it wrote them (no export launch); otherwise GLOBAL rows, exported
+  const int* ovf_p = ovf;
+  const float* eps_p = eps;
   if (use_theta)
-    rc = ebt_cosine_screen_at_lead(q64, qimg, qscale, qeps, B, L.B_pad, c.data, c.dtype, c.ld,
-                                   c.gnorm64, c.image, c.cscale, c.img_dtype, c.ld_img, c.n, c.d,
-                                   c.d_pad, c.row_offset, excl_off, excl_rows, L.k_eff, L.kprime,
-                                   L.chunk, 0, ws + S.off_spass, S.screen_bytes, lv, lr, ovf, eps,
-                                   theta, hits, S.lead, (const float*)(ws + S.off_lead),
-                                   S.ld_lead, timer, st);
+    rc = screen_at_local(q64, qimg, qscale, qeps, B, L.B_pad, c.data, c.dtype, c.ld, c.gnorm64,
+                         c.image, c.cscale, c.img_dtype, c.ld_img, c.n, c.d, c.d_pad,
+                         c.row_offset, excl_off, excl_rows, L.k_eff, L.kprime, L.chunk,
+                         ws + S.off_spass, S.screen_bytes, lv, lr, theta, hits, S.lead,
+                         (const float*)(ws + S.off_lead), S.ld_lead, &ovf_p, &eps_p, timer, st);
   else
     rc = ebt_cosine_screen(q64, qimg, qscale, qeps, B, L.B_pad, c.data, c.dtype, c.ld, c.gnorm64,
                            c.image, c.cscale, c.img_dtype, c.ld_img, c.n, c.d, c.d_pad,
@@ -1124,7 +1133,7 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
   float* frecv = (float*)(ws + S.off_frecv);
   double* tfloor = (double*)(ws + S.off_tfloor);
   if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
-  rc = ebt_floor_pack(lv, L.kprime, B, L.k_eff, (int32_t)S.fw, eps, fsend, st);
+  rc = ebt_floor_pack(lv, L.kprime, B, L.k_eff, (int32_t)S.fw, eps_p, fsend, st);
   if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
   if (!rc) rc = sh_gather(cm, fsend, frecv, (size_t)B * (S.fw + 1) * 4, timer, st);
   if (rc) return rc;
@@ -1139,10 +1148,11 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
   double* rs = padded ? (double*)(ws + L.off_res_s) : ls;
   int64_t* rr = padded ? (int64_t*)(ws + L.off_res_r) : lrr;
   int32_t* cert = (int32_t*)(ws + L.off_cert);
-  // (the list's GLOBAL rows read as they are; the certificate with ebt_certify_cut's tests)
+  // (the list's rows read as they are: local at the shared threshold, global otherwise; the
+  // certificate with ebt_certify_cut's tests)
   rc = rescore_sharded(q64, B, c.d, c.data, c.dtype, c.ld, c.gnorm64, c.row_offset, lv, lr,
-                       L.kprime, L.k_eff, c.n, eps, tfloor, rs, rr, cert, ovf,
-                       use_theta ? theta : nullptr, timer, st);
+                       L.kprime, L.k_eff, c.n, eps_p, tfloor, rs, rr, cert, ovf_p,
+                       use_theta ? theta : nullptr, timer, st, use_theta ? 0 : c.row_offset);
   if (rc) return rc;
   if (excl_off) {
     rc = hip_check(hipMemsetAsync(cert + B, 0, 4, st), "hipMemsetAsync");
