@@ -187,6 +187,21 @@ EOF
                      EBERT_LIB=_abl/libebert_grid.so EBT_QP_GRID=240 $G py "r5_overlap_$lay" \
                        tools/overlap_probe.py --tail-cus 2 --layout "$lay"
                    done ;;
+      # (A/B builds: tools/abl_build.sh NAME FLAGS, or the previous commit's libebert.so copied
+      # to _abl/libebert_prev.so before the change)
+      r5_eps)      $G suite r5k; $G ab r5k_ab _abl/libebert_prev.so C3,C2 2 ;;
+      r5_sample16) $G ab r5m_s16 _abl/libebert_s16.so C3 2 ;;          # -DEBT_SPEC_SAMPLE_MIN=16
+      r5_shardlead) $G trace r5m_rs python3 tools/rank_sim_capi.py --config C3 --world 8 --steps 20
+                   EBT_SPEC_LEAD=0 $G py r5m_rs0 tools/rank_sim_capi.py --config C3 --world 8 --steps 20
+                   $G py r5m_rs1 tools/rank_sim_capi.py --config C3 --world 8 --steps 20 ;;
+      r5_segrate)  $G ab r5s_ab _abl/libebert_prev.so C3 3 ;;
+      r5_nr8)      $G ab r5u_ab _abl/libebert_nr8.so C2 3 ;;               # -DEBT_RESCORE_NR_NARROW=8
+      r5_final)    $G suite r5t; $G bench r5t C3 --steps 20
+                   $G py r5t_rs tools/rank_sim_capi.py --config C3 --world 8 --steps 20
+                   $G prof r5t_prof C3 5
+                   $G bench r5r_c4 C4 --steps 10; $G bench r5r_c5 C5 --steps 5 --warmup 2
+                   $G bench r5r_n2 C3 --gpus 2 --share-gpu --steps 5 --warmup 2 --cpu-budget 4
+                   $G bench r5r_n4 C3 --gpus 4 --share-gpu --steps 5 --warmup 2 --cpu-budget 4 ;;
       *) echo "unknown recipe $N" >&2; exit 2 ;;
     esac
     ;;
