@@ -742,7 +742,10 @@ namespace ebt {
 namespace {
 
 constexpr int SH_MERGE_WAVE_KMAX = 512;          // search.py MERGE_WAVE_KMAX
-constexpr int64_t SH_SHARED_MAX_SHARD_ROWS = 200000;  // distributed.py SHARED_MAX_SHARD_ROWS
+#ifndef EBT_SH_SHARED_MAX
+#define EBT_SH_SHARED_MAX 300000  // (build knob for A/B; round 5: 200000 -> 300000, C3/4 -1.6 %)
+#endif
+constexpr int64_t SH_SHARED_MAX_SHARD_ROWS = EBT_SH_SHARED_MAX;  // distributed.py SHARED_MAX_SHARD_ROWS
 constexpr int64_t SH_SAMPLE_TILES_MAX = 64;
 constexpr int SH_K_MAX = 4096;                   // ebt_merge_topk
 

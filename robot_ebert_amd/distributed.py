@@ -41,8 +41,10 @@ from .search import (KPRIME_MAX, MERGE_WAVE_KMAX, _round_up, csr_from_lists, csr
 SAMPLE_TILES_MAX = 64   # per shard, as the single-GPU speculative screen (api.hip spec_params)
 # Larger shards screen at their own sample threshold: there the shard's first segment raises
 # its threshold (list k-th - 2 eps) soon enough, and the shared threshold's uniform hits cost
-# as much as they save (tools/shard_sim.py at C3: 2 ranks +2.5 %, 4 ranks +-0, 8 ranks -3 %).
-SHARED_MAX_SHARD_ROWS = 200_000
+# as much as they save (round 5, tools/rank_sim_capi.py replays of C3, two runs each: 4 ranks
+# 2.689 vs 2.734 ms per step with the shared threshold, 2 ranks 5.251 vs 5.214 ms; round 3's
+# shard_sim: 8 ranks -3 %). driver.hip EBT_SH_SHARED_MAX is the same limit.
+SHARED_MAX_SHARD_ROWS = 300_000
 
 
 def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
