@@ -77,6 +77,10 @@ def main():
     ap.add_argument("--cscale", action="store_true")
     ap.add_argument("--warm", type=int, default=6)
     ap.add_argument("--lib", default=os.path.join(ROOT, "_abl", "libebert_walk.so"))
+    ap.add_argument("--alloc-rows", type=int, default=0,
+                    help="allocate this many catalog rows and screen the --n rows at --offset-rows "
+                         "of it (the bench's C5 parts are 520K-row windows of a 50M-row catalog)")
+    ap.add_argument("--offset-rows", type=int, default=0)
     a = ap.parse_args()
     lib = ctypes.CDLL(a.lib)
     f = lib.ebt_screen_filter
@@ -90,8 +94,17 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     q = torch.randn((B, d), generator=g, device=dev)
     q = (q / q.norm(dim=1, keepdim=True)).to(torch.float16 if a.img == "f16" else torch.bfloat16)
-    c = torch.randn((N, d), generator=g, device=dev)
-    c = (c / c.norm(dim=1, keepdim=True)).to(q.dtype)
+    if a.alloc_rows > N:
+        big = torch.empty((a.alloc_rows, d), dtype=q.dtype, device=dev)
+        for r0 in range(0, a.alloc_rows, 1 << 20):   # filled in 1M-row blocks (bounded temp)
+            r1 = min(a.alloc_rows, r0 + (1 << 20))
+            x = torch.randn((r1 - r0, d), generator=g, device=dev)
+            big[r0:r1] = (x / x.norm(dim=1, keepdim=True)).to(q.dtype)
+            del x
+        c = big[a.offset_rows:a.offset_rows + N]
+    else:
+        c = torch.randn((N, d), generator=g, device=dev)
+        c = (c / c.norm(dim=1, keepdim=True)).to(q.dtype)
     idt = 2 if a.img == "f16" else 1
     qs = torch.ones(B, device=dev)
     cs = torch.ones(N, device=dev) if a.cscale else None
@@ -143,6 +156,7 @@ def main():
     t_all0 = min(t[0][1] for t in wg_tiles.values())
     t_all1 = max(t[-1][2] for t in wg_tiles.values())
     out = {"shape": [B, N, d], "img": a.img, "row_scales": bool(a.cscale), "query_tiles": n_qt,
+           "alloc_rows": a.alloc_rows or N, "offset_rows": a.offset_rows,
            "catalog_tiles": n_ct, "tiles": n_qt * n_ct, "launch_ms": round(ms_plain, 3),
            "launch_ms_stamped": round(ms_stamped, 3),
            "tiles_per_workgroup": round(n_qt * n_ct / max(len(wg_tiles), 1), 1)}
