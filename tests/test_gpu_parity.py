@@ -1224,7 +1224,7 @@ def test_speculative_lead_equals_no_lead(cuda_device, dt):
 
 
 def test_speculative_lead_hits_equal_filter_hits(cuda_device):
-    """The lead tiles' hits (the pool GEMM's stored scores + lead_hits_kernel) are the filter
+    """The lead tiles' hits (the pool GEMM's stored scores, taken by pool_kth_kernel) are the filter
     epilogue's own: a screen with the lead and one without give the same k best approx
     candidates (values and rows) for every query. (Past position k the lists may differ: later
     segments filter at the list's k-th - 2 eps, and the segments start at different rows.)"""
