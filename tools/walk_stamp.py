@@ -81,6 +81,9 @@ def main():
                     help="allocate this many catalog rows and screen the --n rows at --offset-rows "
                          "of it (the bench's C5 parts are 520K-row windows of a 50M-row catalog)")
     ap.add_argument("--offset-rows", type=int, default=0)
+    ap.add_argument("--advance", action="store_true",
+                    help="each warm-up launch screens the next --n rows of the allocation "
+                         "(consecutive windows, as the bench's split parts) instead of the same")
     a = ap.parse_args()
     lib = ctypes.CDLL(a.lib)
     f = lib.ebt_screen_filter
@@ -102,9 +105,12 @@ def main():
             big[r0:r1] = (x / x.norm(dim=1, keepdim=True)).to(q.dtype)
             del x
         c = big[a.offset_rows:a.offset_rows + N]
+        windows = [big[a.offset_rows + i * N:a.offset_rows + (i + 1) * N]
+                   for i in range(max(1, (a.alloc_rows - a.offset_rows) // N))]
     else:
         c = torch.randn((N, d), generator=g, device=dev)
         c = (c / c.norm(dim=1, keepdim=True)).to(q.dtype)
+        windows = [c]
     idt = 2 if a.img == "f16" else 1
     qs = torch.ones(B, device=dev)
     cs = torch.ones(N, device=dev) if a.cscale else None
@@ -117,14 +123,15 @@ def main():
     st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
 
-    def launch():
-        rc = f(P(q), B, P(c), N, d, d, idt, P(qs), P(cs) if cs is not None else None, P(thr),
+    def launch(cc=None):
+        cc = c if cc is None else cc
+        rc = f(P(q), B, P(cc), N, d, d, idt, P(qs), P(cs) if cs is not None else None, P(thr),
                P(cand), groups * slots, slots, P(counts), groups, P(ovf), 0, st)
         if rc:
             raise RuntimeError(lib.ebt_last_error().decode())
     lib.ebt_debug_walk_stamps(None)
-    for _ in range(a.warm):
-        launch()
+    for i in range(a.warm):
+        launch(windows[i % len(windows)] if a.advance else None)
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
