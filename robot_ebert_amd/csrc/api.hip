@@ -840,6 +840,12 @@ struct PipeArgs {
   int64_t lead = 0;
   const float* lead_s = nullptr;
   int64_t ld_lead = 0;
+  // screen_at_local: the threshold as the gs_j-th of the all-gathered sample maxima ([R][B][gj],
+  // rank stride gs_rstride floats, gs_G values per query), taken by the same launch that starts
+  // the list and takes the lead's hits (instead of a caller's theta)
+  const float* gsamp = nullptr;
+  int64_t gs_rstride = 0;
+  int gs_G = 0, gs_gj = 0, gs_j = 0;
 };
 
 static int check_pipe(const PipeArgs& a, const char* who) {
@@ -909,7 +915,8 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
   float* pooled = (float*)(ws + L.off_s);
   float* tspec = (float*)(ws + L.off_tspec);
   const int64_t m = L.head;
-  const bool given = a.theta != nullptr;  // ebt_cosine_screen_at: the caller's threshold
+  // ebt_cosine_screen_at: the caller's threshold (or screen_at_local's gathered samples)
+  const bool given = a.theta != nullptr || a.gsamp != nullptr;
   const double spec_hits = given ? (a.hits > 0.0 ? a.hits : 1.0) : L.spec_hits;
   // hits per group ~ H group_rows / n (per query; its threshold's own spread ~ 1/sqrt(j) on
   // top): slots for 4x that + 4, and at least enough that a group overflow (which costs its
@@ -931,8 +938,13 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
   if (given) {
     // the threshold, the empty list (-inf / -1), no overflow yet: one launch
     // (+ the caller's lead hits at theta into the first groups' slots)
-    rc = spec_given_init(a.theta, B, B_pad, tspec, fv, fi, kprime, ovf, st, a.lead_s, a.ld_lead,
-                         (int)lead, cand, L.ld_cand, slots, counts, L.ld_counts);
+    if (a.gsamp)   // the threshold from the gathered samples, in the same launch
+      rc = pool_kth(a.gsamp, a.gs_G, B, B_pad, a.gs_G, a.gs_j, tspec, st, fv, fi, kprime, ovf,
+                    a.lead_s, a.ld_lead, (int)lead, cand, L.ld_cand, slots, counts, L.ld_counts,
+                    a.gs_gj, a.gs_rstride);
+    else
+      rc = spec_given_init(a.theta, B, B_pad, tspec, fv, fi, kprime, ovf, st, a.lead_s,
+                           a.ld_lead, (int)lead, cand, L.ld_cand, slots, counts, L.ld_counts);
     if (rc) return rc;
   } else {
     {
@@ -1295,24 +1307,31 @@ int screen_at_local(const double* q64, const void* qimg, const float* qscale, co
                     int32_t ld_img, int64_t n_rows, int32_t d, int32_t d_pad, int64_t row_offset,
                     const int64_t* excl_off, const int64_t* excl_rows, int32_t k, int32_t kprime,
                     int64_t chunk_rows, void* workspace, size_t ws_bytes, float* list_vals,
-                    int64_t* list_rows, const float* theta, double hits, int64_t lead,
-                    const float* lead_scores, int64_t ld_lead, const int** ovf_dev,
+                    int64_t* list_rows, const float* gsamp, int64_t gs_rstride, int gs_G,
+                    int gs_gj, int gs_j, double hits, int64_t lead, const float* lead_scores,
+                    int64_t ld_lead, const float** theta_dev, const int** ovf_dev,
                     const float** eps_dev, void* timer, hipStream_t st) {
   const int flags = EBT_FLAG_THETA;
   PipeArgs a{q64, qimg, qscale, eps, B, B_pad, cat, dtype, ld, gnorm64, cimg, cscale,
              img_dtype, ld_img, n_rows, d, d_pad, row_offset, excl_off, excl_rows, k, kprime,
              chunk_rows, flags};
-  a.theta = theta;
   a.hits = hits;
   a.lead = lead;
   a.lead_s = lead_scores;
   a.ld_lead = ld_lead;
+  a.gsamp = gsamp;
+  a.gs_rstride = gs_rstride;
+  a.gs_G = gs_G;
+  a.gs_gj = gs_gj;
+  a.gs_j = gs_j;
   int rc = check_pipe(a, "screen_at_local");
   if (rc) return rc;
-  if (!workspace || !list_vals || !list_rows || !theta || !ovf_dev || !eps_dev ||
-      !merge_wave_fits(kprime) || !(hits >= 0.0) || lead < 0 ||
+  if (!workspace || !list_vals || !list_rows || !gsamp || !theta_dev || !ovf_dev || !eps_dev ||
+      !merge_wave_fits(kprime) || !(hits >= 0.0) || lead < 0 || gs_G < 1 || gs_G > 2048 ||
+      gs_gj < 1 || gs_G % gs_gj != 0 || gs_rstride < B * (int64_t)gs_gj || gs_j < 1 ||
       (lead > 0 && (!lead_scores || ld_lead < 256 * lead || 256 * lead >= n_rows))) {
-    set_error("screen_at_local: bad arguments (kprime=%d, lead=%lld)", kprime, (long long)lead);
+    set_error("screen_at_local: bad arguments (kprime=%d, lead=%lld, G=%d, gj=%d, j=%d)", kprime,
+              (long long)lead, gs_G, gs_gj, gs_j);
     return EBT_EINVAL;
   }
   const WsLayout L = ws_layout(B, B_pad, n_rows, kprime, chunk_rows, flags);
@@ -1325,6 +1344,7 @@ int screen_at_local(const double* q64, const void* qimg, const float* qscale, co
   if (rc) return rc;
   *ovf_dev = so.ovf;
   *eps_dev = so.eps;
+  *theta_dev = (const float*)((char*)workspace + L.off_tspec);
   return EBT_OK;
 }
 }  // namespace ebt

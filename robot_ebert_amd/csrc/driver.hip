@@ -36,8 +36,8 @@ int screen_at_local(const double*, const void*, const float*, const float*, int6
                     const void*, int, int64_t, const double*, const void*, const float*, int,
                     int32_t, int64_t, int32_t, int32_t, int64_t, const int64_t*, const int64_t*,
                     int32_t, int32_t, int64_t, void*, size_t, float*, int64_t*, const float*,
-                    double, int64_t, const float*, int64_t, const int**, const float**, void*,
-                    hipStream_t);
+                    int64_t, int, int, int, double, int64_t, const float*, int64_t, const float**,
+                    const int**, const float**, void*, hipStream_t);
 int pool_kth(const float*, int64_t, int64_t, int64_t, int, int, float*, hipStream_t, float*,
              int64_t*, int, int*, const float*, int64_t, int, uint64_t*, int64_t, int, uint8_t*,
              int64_t, int, int64_t);
@@ -1062,8 +1062,11 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
                               (double*)(ws + S.off_scale), (double*)(ws + S.off_qrecv), timer, st);
   if (timer) (void)ebt_timer_end(timer, EBT_STAGE_PREP, st);
   if (rc) return rc;
-  // 2. the catalog-wide screening threshold from every shard's sample maxima
-  float* theta = nullptr;
+  // 2. the catalog-wide screening threshold from every shard's sample maxima (taken by the
+  // screen's first launch, step 3)
+  bool accept = false;
+  const float* recv_s = nullptr;
+  int j_s = 0;
   double hits = 0.0;
   if (S.tiles) {
     float* pool = (float*)(ws + S.off_pool);
@@ -1097,18 +1100,14 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
     // exact for j <= J; when J was clamped to G every shard sent all of its maxima, and any
     // j <= RG / 2 is (distributed.theta_from_samples decides alike)
     if (j <= S.J || (S.J == S.G && j <= S.RG / 2)) {
-      theta = (float*)(ws + S.off_theta);
-      const int64_t RGJ = (int64_t)R * S.GJ;
-      if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
-      // the j-th of every rank's maxima, read in the gathered [R][B][J + 1] layout
-      rc = pool_kth(recv, RGJ, B, L.B_pad, (int)RGJ, j, theta, st, nullptr, nullptr, 0, nullptr,
-                    nullptr, 0, 0, nullptr, 0, 0, nullptr, 0, (int)S.GJ, B * S.GJ);
-      if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
-      if (rc) return rc;
+      accept = true;
+      recv_s = recv;
+      j_s = j;
       hits = ((double)j + (double)j * j / (2.0 * (double)S.RG)) * (double)c.n / m_total;
     }
   }
-  const bool use_theta = theta && L.flags == 0 && L.kprime <= SH_MERGE_WAVE_KMAX;
+  const bool use_theta = accept && L.flags == 0 && L.kprime <= SH_MERGE_WAVE_KMAX;
+  const float* theta = nullptr;   // the shared threshold, where the screen wrote it
   // 3. the shard's screen: its k' best approx candidates (GLOBAL rows)
   float* lv = (float*)(ws + S.off_lv);
   int64_t* lr = (int64_t*)(ws + S.off_lr);
@@ -1118,12 +1117,16 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
   // are read where it wrote them (no export launch); otherwise GLOBAL rows, exported
   const int* ovf_p = ovf;
   const float* eps_p = eps;
+  // (the j-th of every rank's maxima, read in the gathered [R][B][J + 1] layout, is taken by
+  // the launch that starts the list and takes the lead's hits: one launch for both)
   if (use_theta)
     rc = screen_at_local(q64, qimg, qscale, qeps, B, L.B_pad, c.data, c.dtype, c.ld, c.gnorm64,
                          c.image, c.cscale, c.img_dtype, c.ld_img, c.n, c.d, c.d_pad,
                          c.row_offset, excl_off, excl_rows, L.k_eff, L.kprime, L.chunk,
-                         ws + S.off_spass, S.screen_bytes, lv, lr, theta, hits, S.lead,
-                         (const float*)(ws + S.off_lead), S.ld_lead, &ovf_p, &eps_p, timer, st);
+                         ws + S.off_spass, S.screen_bytes, lv, lr, recv_s, B * S.GJ,
+                         (int)(R * S.GJ), (int)S.GJ, j_s, hits, S.lead,
+                         (const float*)(ws + S.off_lead), S.ld_lead, &theta, &ovf_p, &eps_p,
+                         timer, st);
   else
     rc = ebt_cosine_screen(q64, qimg, qscale, qeps, B, L.B_pad, c.data, c.dtype, c.ld, c.gnorm64,
                            c.image, c.cscale, c.img_dtype, c.ld_img, c.n, c.d, c.d_pad,
