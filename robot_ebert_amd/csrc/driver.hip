@@ -787,7 +787,7 @@ struct ShardLayout {
   size_t screen_bytes;
   int64_t fw, cap;  // floor gather width per shard and query; packed results per rank (0: full)
   size_t pack_bytes;
-  size_t off_spass, off_pool, off_gsamp, off_theta, off_lv, off_lr, off_ovf,
+  size_t off_spass, off_pool, off_gsamp, off_lv, off_lr, off_ovf,
       off_eps, off_fsend, off_frecv, off_tfloor, off_ls, off_lrr, off_gs, off_gr, off_scale,
       off_qrecv, off_psend, off_precv, off_incomplete, off_lead, bytes;
 };
@@ -852,8 +852,6 @@ bool shard_layout(const ebt_catalog& c, const ebt_comm& cm, int64_t B, int32_t k
   o = al(o + (size_t)D.B_pad * L.ld_lead * 4);
   L.off_gsamp = o;
   o = al(o + (size_t)B * L.GJ * 4 * (R + 1));  // this shard's J largest, then every shard's
-  L.off_theta = o;
-  o = al(o + (size_t)D.B_pad * 4);
   L.off_lv = o;
   o = al(o + (size_t)B * kp * 4);
   L.off_lr = o;
