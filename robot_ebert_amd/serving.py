@@ -280,8 +280,8 @@ class ScoreClient:
             rid, res = decode_response(buf)
             with self._plock:
                 fut = self._pending.pop(rid, None)
-            if fut is None:
-                continue
+            if fut is None or not fut.set_running_or_notify_cancel():
+                continue   # unknown id, or the caller cancelled its Future: drop the answer
             if isinstance(res, BaseException):
                 fut.set_exception(res)
             else:
@@ -290,7 +290,7 @@ class ScoreClient:
             left, self._pending = list(self._pending.values()), {}
             self._closed = True
         for f in left:
-            if not f.done():
+            if f.set_running_or_notify_cancel():
                 f.set_exception(err)
 
     def submit(self, liked: Sequence[int], rated: Sequence[int], k: int) -> Future:
@@ -309,8 +309,10 @@ class ScoreClient:
                 self._conn.send_bytes(frame)
         except (OSError, ValueError) as e:
             with self._plock:
-                self._pending.pop(rid, None)
-            fut.set_exception(RuntimeError(f"score server connection failed ({e!r})"))
+                mine = self._pending.pop(rid, None) is not None
+            # (else the reader, ending on the same closed connection, already failed it)
+            if mine and fut.set_running_or_notify_cancel():
+                fut.set_exception(RuntimeError(f"score server connection failed ({e!r})"))
         return fut
 
     def score(self, liked: Sequence[int], rated: Sequence[int], k: int):

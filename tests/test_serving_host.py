@@ -250,3 +250,26 @@ def test_route_through_the_score_server(monkeypatch, tmp_path):
     srv.close()
     b.close()
     direct.close()
+
+
+def test_cancelled_future_does_not_stop_the_client():
+    """A caller that cancels its Future before the answer arrives: the client's reader drops
+    that answer and goes on resolving the others (a set_result on a cancelled Future would raise
+    in the reader and leave every later request hanging)."""
+    x = np.random.default_rng(6).standard_normal((200, 8))
+    gate = threading.Event()
+
+    def slow(cat, k, liked, exclude):
+        gate.wait(10)
+        return _oracle_score([])(cat, k, liked, exclude)
+    b = RecBatcher(_Cat(x), max_batch=8, max_wait_ms=1.0, score_fn=slow)
+    srv = ScoreServer(b)
+    c = ScoreClient(srv.address, timeout=20.0)
+    f1 = c.submit([1], [], 3)
+    assert f1.cancel()
+    gate.set()
+    for i in range(4):
+        assert len(c.score([2 + i], [], 4)[1]) == 4
+    c.close()
+    srv.close()
+    b.close()
