@@ -140,7 +140,7 @@ int64_t ebt_filter_group_rows(int64_t B_pad);
 /* Long filter launches (0.3.0): a fused segment of the pipeline (ebt_cosine_topk*, ebt_cosine_screen*)
  * over more than ~1.5 x T x (CUs / query tiles) tiles of 256 rows is run as consecutive
  * ebt_screen_filter launches of whole rounds, each at most T tiles per workgroup
- * (default T = 512; EBT_FILTER_TPW in the environment), so that the persistent walk's
+ * (default T = 32 since 0.3.1, 512 in 0.3.0; EBT_FILTER_TPW in the environment), so that the persistent walk's
  * workgroups start in step again (screening GEMM). Same tiles, hits and counts.
  * ebt_filter_split(T) sets T for the process (0: never split; T < 0: query) and returns the
  * previous value. */

@@ -1542,7 +1542,7 @@ int64_t filter_group_rows(int64_t B_pad) { return B_pad % QP_TILE == 0 ? QP_TILE
 static std::atomic<int64_t>& filter_tpw_flag() {
   static std::atomic<int64_t> v([] {
     const char* s = getenv("EBT_FILTER_TPW");
-    return s ? (int64_t)atoll(s) : (int64_t)512;
+    return s ? (int64_t)atoll(s) : (int64_t)32;
   }());
   return v;
 }
