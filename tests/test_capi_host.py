@@ -257,3 +257,24 @@ def test_workspace_size_does_not_depend_on_the_lead_knob():
         assert lib.ebt_cosine_topk_spec_lead(1024, 1024, 100_000, 128, 0) == 7   # C2
     finally:
         lib.ebt_spec_lead(prev)
+
+
+def test_filter_split_default_and_set():
+    """ebt_filter_split: long filter launches run as parts of at most 32 tiles per workgroup by
+    default since 0.3.1 (512 before; profiles/r5/ab/tpw/), settable per process, 0 = never split;
+    a negative argument only queries. Host code: no GPU call."""
+    import os
+    from robot_ebert_amd import _lib
+    lib = _lib.load()
+    cur = lib.ebt_filter_split(-1)
+    if "EBT_FILTER_TPW" not in os.environ:
+        assert cur == 32
+    prev = lib.ebt_filter_split(64)
+    try:
+        assert prev == cur
+        assert lib.ebt_filter_split(-1) == 64
+        assert lib.ebt_filter_split(0) == 64
+        assert lib.ebt_filter_split(-1) == 0
+    finally:
+        lib.ebt_filter_split(cur)
+    assert lib.ebt_filter_split(-1) == cur
