@@ -277,7 +277,12 @@ class ScoreClient:
             except (OSError, EOFError) as e:
                 err = RuntimeError(f"score server connection closed ({e!r})")
                 break
-            rid, res = decode_response(buf)
+            try:
+                rid, res = decode_response(buf)
+            except Exception as e:  # noqa: BLE001 -- a garbled frame: the stream is unusable
+                err = RuntimeError(f"score server sent a malformed frame ({e!r})")
+                _shutdown(self._conn)
+                break
             with self._plock:
                 fut = self._pending.pop(rid, None)
             if fut is None or not fut.set_running_or_notify_cancel():

@@ -273,3 +273,36 @@ def test_cancelled_future_does_not_stop_the_client():
     c.close()
     srv.close()
     b.close()
+
+
+def test_garbled_server_frame_fails_pending_callers(tmp_path):
+    """A frame from the server that does not decode ends the client's connection: its pending
+    and later callers get a RuntimeError instead of waiting forever (the reader thread must not
+    die with callers registered)."""
+    from multiprocessing.connection import Listener
+    from robot_ebert_amd.serving import AUTHKEY
+    addr = str(tmp_path / "fake.sock")
+    lst = Listener(addr, family="AF_UNIX", authkey=AUTHKEY)
+    got = {}
+
+    def fake_server():
+        conn = lst.accept()
+        got["req"] = conn.recv_bytes()
+        conn.send_bytes(b"\x01\x02")        # shorter than a response header
+        try:
+            conn.recv_bytes()               # until the client shuts the connection down
+        except (OSError, EOFError):
+            pass
+        conn.close()
+    t = threading.Thread(target=fake_server)
+    t.start()
+    c = ScoreClient(addr, timeout=10.0)
+    f = c.submit([1], [], 3)
+    with pytest.raises(RuntimeError, match="malformed|closed"):
+        f.result(timeout=10.0)
+    with pytest.raises(RuntimeError):
+        c.score([2], [], 3)
+    c.close()
+    t.join(10)
+    lst.close()
+    assert decode_request(got["req"])[0] == 1
