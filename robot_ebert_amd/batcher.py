@@ -163,7 +163,7 @@ class RecBatcher:
                 for r in reqs:
                     groups[k_class(r[2])].append(r)
                 for c in sorted(groups):
-                    self._dispatch(groups[c])
+                    self._dispatch_safe(groups[c])
             if stop:
                 while True:  # drain what was queued before close()
                     try:
@@ -171,7 +171,7 @@ class RecBatcher:
                     except queue.Empty:
                         break
                     if item is not _SENTINEL:
-                        self._dispatch([item])
+                        self._dispatch_safe([item])
                 self._done.put(_SENTINEL)
                 return
 
@@ -180,6 +180,15 @@ class RecBatcher:
         self._n_batches += 1
         self._n_requests += n
         self._hist[max(n, 1).bit_length() - 1] += 1
+
+    def _dispatch_safe(self, reqs: list) -> None:
+        """_dispatch, and if anything in it fails unexpectedly, that error to every caller of the
+        batch not answered yet: the dispatcher thread itself never dies with callers waiting."""
+        try:
+            self._dispatch(reqs)
+        except BaseException as e:  # noqa: BLE001
+            for r in reqs:
+                _answer(r[3], exc=e)
 
     def _dispatch(self, reqs: list) -> None:
         k_max = max(r[2] for r in reqs)
@@ -221,8 +230,9 @@ class RecBatcher:
                         _answer(r[3], exc=e)
                     continue
                 self._deliver(reqs, scores, rows)
-            except BaseException:  # noqa: BLE001 -- never let one batch stop the thread
-                pass
+            except BaseException as e:  # noqa: BLE001 -- never let one batch stop the thread
+                for r in reqs:             # (its callers not answered yet get the error)
+                    _answer(r[3], exc=e)
             finally:
                 self._slots.release()
 

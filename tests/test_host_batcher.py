@@ -180,3 +180,32 @@ def test_pipelined_cancelled_request_does_not_wedge(monkeypatch):
         np.testing.assert_array_equal(r, wr)
     b.close()
     assert b.stats()["requests"] >= 6
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_batcher_malformed_result_fails_callers_not_thread(monkeypatch, pipelined):
+    """A scoring function that returns something the delivery cannot slice (a bug, not a
+    request's error): the batch's callers get that error and the batcher keeps serving."""
+    import robot_ebert_amd.search as S
+    x = np.random.default_rng(12).standard_normal((300, 8))
+    cat = _Cat(x)
+    bad = {"on": True}
+
+    def score(c, k, liked, exclude):
+        if bad["on"]:
+            bad["on"] = False
+            return np.zeros(3), None          # not (scores [B, k], rows [B, k])
+        qs = np.stack([R.mean_cosine_query(c.x[l]) for l in liked])
+        return R.cosine_topk(qs, c.x, k, exclude)
+    if pipelined:
+        monkeypatch.setattr(S, "score_topk_submit", score)
+        monkeypatch.setattr(S, "score_topk_finish", lambda p: p)
+        b = RecBatcher(cat, max_batch=4, max_wait_ms=0.0, max_inflight=1)
+    else:
+        b = RecBatcher(cat, max_batch=4, max_wait_ms=0.0, score_fn=score)
+    first = b.submit([1], [], 3)
+    assert first.exception(timeout=10) is not None
+    for i in range(4):
+        s, r = b.submit([i + 2], [], 3).result(timeout=10)
+        np.testing.assert_array_equal(r, _direct(cat, [i + 2], [], 3)[1])
+    b.close()
