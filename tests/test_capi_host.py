@@ -278,3 +278,22 @@ def test_filter_split_default_and_set():
     finally:
         lib.ebt_filter_split(cur)
     assert lib.ebt_filter_split(-1) == cur
+
+
+def test_sample_lead_argument_checks():
+    """ebt_cosine_sample_lead (0.3.1) refuses, before any GPU call, a lead larger than the sample,
+    sample tiles that run past the catalog, and a lead without its score buffer."""
+    from robot_ebert_amd import _lib
+    lib = _lib.load()
+    n = 256 * 100
+
+    def call(tiles, stride, lead, lead_scores, ld_lead):
+        return lib.ebt_cosine_sample_lead(None, None, 256, None, None, 0, 64, n, 64, tiles,
+                                          stride, None, 4 * tiles, lead, lead_scores, ld_lead,
+                                          None, None)
+    assert call(4, 2, 5, None, 0) == -1                        # lead > tiles
+    assert b"ebt_cosine_sample" in lib.ebt_last_error()
+    assert call(10, 12, 0, None, 0) == -1                      # last tile ends at row 256 * 109
+    assert call(10, 11, 2, None, 512) == -1                    # lead without its scores
+    assert call(0, 1, 0, None, 0) == -1 and call(4, 0, 0, None, 0) == -1
+    assert call(4, 2, -1, None, 0) == -1
