@@ -407,8 +407,6 @@ static int64_t spec_lead_tiles(int64_t B_pad, int64_t n_rows, int64_t sample_til
 }
 
 // A row-sharded catalog's sample lead (ebt_cosine_sample_lead / ebt_cosine_screen_at_lead): the
-// same rule over the shard's rows and its own sample tiles
-// A row-sharded catalog's sample lead (ebt_cosine_sample_lead / ebt_cosine_screen_at_lead): the
 // shard's filter then covers whole rounds too. The shards' samples together spread over the
 // catalog, so a shard's lead may take all but 4 of its sample tiles (C3 on 8 ranks: 489 tiles
 // per shard, 16 sample tiles of which the first 9 are the lead; the filter's 31st round of 9 x 16
