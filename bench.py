@@ -64,6 +64,14 @@ def make_queries(cfg, device) -> torch.Tensor:
     return q.to(TORCH_DT[cfg["dtype"]])
 
 
+def make_exclusions(cfg, r: int) -> list:
+    """Per query, up to r distinct seeded random global rows to exclude (SURVEY section 8d:
+    seed 3; the rated movies that lib.py:48 drops from the candidates), sorted."""
+    rng = np.random.default_rng(3)
+    draw = rng.integers(0, cfg["n"], size=(cfg["b"], r), dtype=np.int64)
+    return [np.unique(x) for x in draw]
+
+
 def host_info() -> dict:
     """The host the CPU baseline ran on: usable cores (affinity), the machine's count, model."""
     try:
@@ -107,7 +115,7 @@ BASE_ROWS_MAX = 1_000_000
 
 def cpu_baseline_and_parity(cfg, blocks, n_all: int, q_gpu: torch.Tensor, s_gpu, r_gpu,
                             budget_s: float, n_parity: int = 0,
-                            what: str = "full catalog, streamed in row blocks"):
+                            what: str = "full catalog, streamed in row blocks", exclude=None):
     """CPU baselines and the parity sample.
 
     (i)  reference-faithful, the value reported: the float64 oracle restatement of lib.py:51-55
@@ -170,7 +178,7 @@ def cpu_baseline_and_parity(cfg, blocks, n_all: int, q_gpu: torch.Tensor, s_gpu,
     # parity sample over the full catalog (>= 64 queries per config; 32 at
     # the multi-GPU-sized catalogs, where the host oracle streams 10M-50M rows)
     n_par = n_parity or (128 if n_all <= BASE_ROWS_MAX else 32)
-    return base, oracle_parity(k, blocks(n_all), Q, s_gpu, r_gpu, n_par, what)
+    return base, oracle_parity(k, blocks(n_all), Q, s_gpu, r_gpu, n_par, what, exclude)
 
 
 def global_blocks(cfg, device, block: int = 1 << 17, rows: int = None):
@@ -183,14 +191,18 @@ def global_blocks(cfg, device, block: int = 1 << 17, rows: int = None):
         yield r0, make_catalog_shard(cfg, r0, r1, device).float().cpu().numpy()
 
 
-def oracle_parity(k: int, blocks, Q: np.ndarray, s_gpu, r_gpu, n_par: int, what: str):
+def oracle_parity(k: int, blocks, Q: np.ndarray, s_gpu, r_gpu, n_par: int, what: str,
+                  exclude=None):
     """n_par evenly spaced queries of the batch against the host float64 oracle streamed over
-    the catalog blocks (oracle.restatement.cosine_topk_stream): rows bit-exact, |ds| <= 1e-5."""
+    the catalog blocks (oracle.restatement.cosine_topk_stream): rows bit-exact, |ds| <= 1e-5.
+    exclude: the batch's per-query excluded rows (the oracle drops them as lib.py:55 does)."""
     from oracle import restatement as R
     n_par = min(Q.shape[0], n_par)
     idx = np.unique(np.linspace(0, Q.shape[0] - 1, n_par).astype(np.int64))
     t0 = time.perf_counter()
     ref_s, ref_r = R.cosine_topk_stream(Q[idx], blocks, k + 1,
+                                        exclude=None if exclude is None else
+                                        [exclude[i] for i in idx],
                                         workers=min(8, max(1, host_info()["nproc"] // 2)))
     t_par = time.perf_counter() - t0
     g_s = s_gpu[torch.from_numpy(idx).to(s_gpu.device)].cpu().numpy()
@@ -199,7 +211,11 @@ def oracle_parity(k: int, blocks, Q: np.ndarray, s_gpu, r_gpu, n_par: int, what:
     max_diff = float(np.max(np.abs(ref_s[:, :k] - g_s)))
     gap = ref_s[:, k - 1] - ref_s[:, k]
     log(f"parity: {len(idx)} queries in {t_par:.1f} s, rows_equal={rows_equal}")
+    hit = None
+    if exclude is not None:   # no excluded row may come back
+        hit = sum(int(np.isin(g_r[j], exclude[i]).sum()) for j, i in enumerate(idx))
     parity = {"queries_checked": int(len(idx)), "rows_bit_exact": rows_equal,
+              "excluded_rows_returned": hit,
               "max_abs_score_diff": max_diff, "tolerance": 1e-5,
               "oracle": "float64 restatement (oracle.restatement.cosine_topk_stream) over the "
                         + what,
@@ -530,6 +546,10 @@ def main() -> None:
                     help="N > 1: the C ABI's pipelined sharded step (ebt_cosine_topk_sharded_*, "
                          "RCCL all-gathers inside libebert) or the Python pipeline "
                          "(distributed.run_sharded_steps over torch.distributed)")
+    ap.add_argument("--exclude", type=int, default=0,
+                    help="(N = 1) exclude up to this many seeded random rows per query (the "
+                         "rated movies of lib.py:48 / :55; SURVEY section 8d's variant: 128); "
+                         "0 = the BASELINE workload, no exclusions")
     ap.add_argument("--skip-collective-rank", type=int, default=-1,
                     help=argparse.SUPPRESS)   # --dry-run test hook (tests/test_bench_launch.py)
     args = ap.parse_args()
@@ -550,6 +570,9 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"error: --gpus {args.gpus} but WORLD_SIZE={world} (launch N ranks for --gpus N)")
+        sys.exit(2)
+    if args.exclude < 0 or (args.exclude and world > 1):
+        log("error: --exclude takes a row count >= 0 and runs at N = 1 only")
         sys.exit(2)
     if args.dry_run:
         return dry_run(args, world, rank)
@@ -586,8 +609,17 @@ def main() -> None:
     # N > 1: per-shard exact top-k with the shared threshold and the floor cut, all-gather,
     # merge; two batches in flight so that each collective runs under the other batch's kernels
     # (distributed.run_sharded_steps).
+    excl, excl_lists = None, None
+    if args.exclude:
+        excl_lists = make_exclusions(cfg, args.exclude)
+        off = np.zeros(len(excl_lists) + 1, dtype=np.int64)
+        off[1:] = np.cumsum([len(e) for e in excl_lists])
+        excl = (torch.from_numpy(off).to(dev),
+                torch.from_numpy(np.concatenate(excl_lists).astype(np.int64)).to(dev))
+        log(f"exclusions: {int(off[-1])} rows over {len(excl_lists)} queries (seed 3)")
+
     def submit():
-        return ebt.score_topk_submit(cat, k, queries=q, timer=timer)
+        return ebt.score_topk_submit(cat, k, queries=q, exclude=excl, timer=timer)
 
     def finish(p):
         return ebt.score_topk_finish(p)
@@ -725,6 +757,7 @@ def main() -> None:
                  " all-gather of each shard's entries above the catalog-wide floor + merge"
                  if world > 1 else ""),
                 "arith": "f16/bf16 MFMA screen (f32 acc) + exact f64 rescore of certified candidates",
+                "exclusions_per_query": (args.exclude or None),
             },
             "roofline": {
                 "bound": "mfma", "kernel": dom_name,
@@ -754,7 +787,7 @@ def main() -> None:
         elif world == 1:
             out["cpu_baseline"], out["parity"] = cpu_baseline_and_parity(
                 cfg, lambda rows: host_blocks(emb, rows), emb.shape[0], q, s, r,
-                args.cpu_budget, args.parity)
+                args.cpu_budget, args.parity, exclude=excl_lists)
         else:
             # N > 1: rank 0 holds only its shard; the CPU baselines and the parity sample (the
             # merged global top-k of the last timed batch) run over the WHOLE catalog,

@@ -87,3 +87,28 @@ def test_traffic_reason_and_stage_breakdown():
     from robot_ebert_amd._lib import STAGES
     for name in ("rescore", "shard_merge", "collective_wait", "prep", "small"):
         assert name in STAGES
+
+
+def test_exclusion_variant_parity():
+    """bench.py --exclude R: seeded per-query exclusions (sorted, distinct, in range); the parity
+    sample drops them in the oracle as lib.py:55 does, accepts an answer without them and counts
+    an excluded row that comes back."""
+    ex = bench.make_exclusions(CFG, 40)
+    assert len(ex) == CFG["b"]
+    for e in ex:
+        assert 0 < len(e) <= 40 and np.all(np.diff(e) > 0) and e[0] >= 0 and e[-1] < CFG["n"]
+    assert all(np.array_equal(a, b) for a, b in zip(ex, bench.make_exclusions(CFG, 40)))
+    cat = _whole().numpy().astype(np.float64)
+    q = np.random.default_rng(7).standard_normal((CFG["b"], CFG["d"]))
+    # the plain top-k's first row of query 0 excluded: the exclusion changes the answer
+    s0, r0 = R.cosine_topk(q, cat, CFG["k"])
+    ex[0] = np.union1d(ex[0], r0[0, :1])
+    s, r = R.cosine_topk(q, cat, CFG["k"], [e.tolist() for e in ex])
+    assert r[0, 0] != r0[0, 0]
+    blocks = lambda: bench.global_blocks(CFG, torch.device("cpu"), block=50_000)  # noqa: E731
+    ok = bench.oracle_parity(CFG["k"], blocks(), q, torch.from_numpy(s), torch.from_numpy(r),
+                             CFG["b"], "test", exclude=ex)
+    assert ok["rows_bit_exact"] and ok["excluded_rows_returned"] == 0
+    bad = bench.oracle_parity(CFG["k"], blocks(), q, torch.from_numpy(s0),
+                              torch.from_numpy(r0), CFG["b"], "test", exclude=ex)
+    assert not bad["rows_bit_exact"] and bad["excluded_rows_returned"] >= 1
