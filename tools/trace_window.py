@@ -1,6 +1,7 @@
 """Per-step kernel time of a repeated step from a rocprofv3 kernel trace (`gpu.sh trace OUT ...`).
 
-The window is the last STEPS steps, each starting at a launch of the anchor kernel (regex, e.g.
+The window is the last STEPS steps (or STEPS steps from the --first-th anchor launch), each
+starting at a launch of the anchor kernel (regex, e.g.
 the sample GEMM 'screen_gemm_qp2_kernel<[^,]*, 2'): per kernel the launches and microseconds per
 step, the busy time (union of kernel intervals) and the idle gaps per step.
 
@@ -18,6 +19,8 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--anchor", required=True)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--first", type=int, default=None,
+                    help="start at this anchor launch (0-based) instead of the last STEPS steps")
     a = ap.parse_args()
     rows = []
     for r in csv.DictReader(open(a.trace)):
@@ -26,7 +29,12 @@ def main():
     starts = [s for s, _, n in rows if re.search(a.anchor, n)]
     if len(starts) < a.steps + 1:
         raise SystemExit(f"only {len(starts)} anchor launches")
-    t0, t1 = starts[-a.steps - 1], starts[-1]   # whole steps: [anchor_i, anchor_{i+1})
+    if a.first is not None:
+        if a.first + a.steps >= len(starts):
+            raise SystemExit(f"only {len(starts)} anchor launches")
+        t0, t1 = starts[a.first], starts[a.first + a.steps]
+    else:
+        t0, t1 = starts[-a.steps - 1], starts[-1]   # whole steps: [anchor_i, anchor_{i+1})
     per = defaultdict(lambda: [0, 0.0])
     busy, end = 0, t0
     for s, e, n in rows:
