@@ -640,10 +640,20 @@ def main() -> None:
             comm = TorchGatherComm(rank, world)
         else:
             try:
-                rccl = comm = RcclComm()
+                rccl = RcclComm()
             except Exception as e:  # noqa: BLE001 -- same collectives through torch.distributed
-                log(f"rank {rank}: libebert's RCCL communicator failed ({e}); all-gathers go "
-                    "through torch.distributed instead")
+                log(f"rank {rank}: libebert's RCCL communicator failed ({e})")
+            # every rank takes the same path: one rank without the library's communicator sends
+            # them all through torch.distributed (mixed paths would wait on each other forever)
+            ok = torch.tensor([1 if rccl is not None else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 1:
+                comm = rccl
+            else:
+                if rccl is not None:
+                    rccl.close()
+                    rccl = None
+                log(f"rank {rank}: all-gathers go through torch.distributed instead")
                 comm = TorchGatherComm(rank, world)
         eng = ShardedTopk(cat, k, cfg["b"], comm, timer=timer)
 
