@@ -19,16 +19,30 @@ namespace {
 
 size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 
-// begin[b] = clamp(off[b]), end[b] = clamp(max(off[b + 1], off[b])): inside [0, nnz]
+// begin[b] = clamp(off[b]), end[b] = clamp(max(off[b + 1], off[b])): inside [0, nnz]. Then
+// end[b] >= begin[b + 1] for every b, so the clamped segments leave no gap between them: the only
+// positions outside every segment are the head [0, begin[0]) and the tail [end[B - 1], nnz),
+// which `keep` (rows_out when it is not rows_in) receives from rows_in here
 __global__ void clamp_offsets_kernel(const int64_t* __restrict__ off, int64_t B, int64_t nnz,
-                                     int64_t* __restrict__ begin, int64_t* __restrict__ end) {
-  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < B;
-       b += (int64_t)gridDim.x * blockDim.x) {
-    int64_t s = off[b], e = off[b + 1];
-    s = s < 0 ? 0 : (s > nnz ? nnz : s);
-    e = e < s ? s : (e > nnz ? nnz : e);
+                                     int64_t* __restrict__ begin, int64_t* __restrict__ end,
+                                     const int64_t* __restrict__ rows_in,
+                                     int64_t* __restrict__ keep) {
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  auto clamp = [&](int64_t x) { return x < 0 ? 0 : (x > nnz ? nnz : x); };
+  for (int64_t b = t0; b < B; b += stride) {
+    const int64_t s = clamp(off[b]), e0 = off[b + 1];
+    const int64_t e = e0 < s ? s : (e0 > nnz ? nnz : e0);
     begin[b] = s;
     end[b] = e;
+  }
+  if (keep) {
+    const int64_t head = clamp(off[0]);
+    int64_t tail = clamp(off[B]);
+    const int64_t lastb = clamp(off[B - 1]);
+    tail = tail < lastb ? lastb : tail;   // end[B - 1]
+    for (int64_t i = t0; i < head; i += stride) keep[i] = rows_in[i];
+    for (int64_t i = tail + t0; i < nnz; i += stride) keep[i] = rows_in[i];
   }
 }
 
@@ -80,23 +94,24 @@ int ebt_sort_exclusions(const int64_t* off, const int64_t* rows_in, int64_t* row
   int64_t* end = (int64_t*)w;
   w += al256((size_t)B * 8);
   size_t temp_bytes = sort_temp_bytes(B, nnz);
-  // the sort reads `keys` and writes rows_out: rows_out first holds the input, so positions
-  // outside every segment keep their value (rows_out == rows_in is allowed)
-  int rc = hip_check(hipMemcpyAsync(keys, rows_in, (size_t)nnz * 8, hipMemcpyDeviceToDevice, st),
-                     "hipMemcpyAsync");
-  if (!rc && rows_out != rows_in)
-    rc = hip_check(hipMemcpyAsync(rows_out, rows_in, (size_t)nnz * 8, hipMemcpyDeviceToDevice, st),
+  // the sort reads its keys from rows_in straight into rows_out when they differ (the clamp
+  // kernel copies the head and tail outside every segment); in place, from a copy in `keys`.
+  // Positions outside every segment keep their value either way.
+  const bool in_place = rows_out == rows_in;
+  int rc = EBT_OK;
+  if (in_place)
+    rc = hip_check(hipMemcpyAsync(keys, rows_in, (size_t)nnz * 8, hipMemcpyDeviceToDevice, st),
                    "hipMemcpyAsync");
   if (rc) return rc;
-  const int64_t blocks = ceil_div(B, 256) < 1024 ? ceil_div(B, 256) : 1024;
+  const int64_t need_thr = B > nnz ? B : nnz;
+  const int64_t blocks = ceil_div(need_thr, 256) < 1024 ? ceil_div(need_thr, 256) : 1024;
   hipLaunchKernelGGL(clamp_offsets_kernel, dim3((unsigned)blocks), dim3(256), 0, st, off, B, nnz,
-                     begin, end);
+                     begin, end, rows_in, in_place ? nullptr : rows_out);
   rc = launch_check("clamp_offsets_kernel");
   if (rc) return rc;
-  return hip_check(hipcub::DeviceSegmentedRadixSort::SortKeys(w, temp_bytes, (const int64_t*)keys,
-                                                              rows_out, (int)nnz, (int)B,
-                                                              (const int64_t*)begin,
-                                                              (const int64_t*)end, 0, 64, st),
+  return hip_check(hipcub::DeviceSegmentedRadixSort::SortKeys(
+                       w, temp_bytes, in_place ? (const int64_t*)keys : rows_in, rows_out,
+                       (int)nnz, (int)B, (const int64_t*)begin, (const int64_t*)end, 0, 64, st),
                    "hipcub segmented radix sort");
 }
 
