@@ -1140,11 +1140,59 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // exclusions (lib.py:48,55): each hit's GLOBAL row looked up in the query's sorted
+      // exclusion segment, a lane's hits 2 at a time in lockstep -- the segment's length sets a
+      // wave-uniform step count, so every step issues those probes together (ceil(log2 L)
+      // dependent loads, not one chain per hit). Branchless lower bound: bs advances by half
+      // while seg[bs + half] < row; the row is excluded iff it sits at the lower bound.
+      constexpr int XE = 2;
+      if (ehi > elo && ehi - elo <= 0x7fffffffLL) {
+        const int32_t L = (int32_t)(ehi - elo);
+        const int64_t* seg = er + elo;
 #pragma unroll
-      for (int u = 0; u < WTOP_E; ++u) {
-        const int h = u * 64 + lane;
-        if (u * 64 < mh && h < mh)
-          U[kprime + h] = (ehi > elo && excluded(comp[u])) ? 0ull : comp[u];
+        for (int c0 = 0; c0 < WTOP_E; c0 += XE) {
+          if (c0 * 64 >= mh) break;  // uniform
+          int64_t gr[XE];
+          int32_t bs[XE];
+#pragma unroll
+          for (int u = 0; u < XE; ++u) {
+            gr[u] = (int64_t)(~(uint32_t)comp[c0 + u]) + row_offset;
+            bs[u] = 0;
+          }
+          for (int32_t n = L; n > 1;) {
+            const int32_t half = n >> 1;
+            int64_t pv[XE];
+#pragma unroll
+            for (int u = 0; u < XE; ++u)
+              if ((c0 + u) * 64 < mh) pv[u] = seg[bs[u] + half];
+#pragma unroll
+            for (int u = 0; u < XE; ++u)
+              if ((c0 + u) * 64 < mh) bs[u] = pv[u] < gr[u] ? bs[u] + half : bs[u];
+            n -= half;
+          }
+          int64_t a[XE], nx[XE];
+#pragma unroll
+          for (int u = 0; u < XE; ++u)
+            if ((c0 + u) * 64 < mh) {
+              a[u] = seg[bs[u]];
+              nx[u] = bs[u] + 1 < L ? seg[bs[u] + 1] : gr[u] - 1;
+            }
+#pragma unroll
+          for (int u = 0; u < XE; ++u) {
+            const int h = (c0 + u) * 64 + lane;
+            if ((c0 + u) * 64 < mh && h < mh) {
+              const bool drop = a[u] < gr[u] ? nx[u] == gr[u] : a[u] == gr[u];
+              U[kprime + h] = drop ? 0ull : comp[c0 + u];
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < WTOP_E; ++u) {
+          const int h = u * 64 + lane;
+          if (u * 64 < mh && h < mh)
+            U[kprime + h] = (ehi > elo && excluded(comp[u])) ? 0ull : comp[u];
+        }
       }
     }
 #else
