@@ -464,6 +464,23 @@ def init_group(backend: str, world: int, rank: int, timeout_s: float, device=Non
     return dist
 
 
+def arith_labels(cfg: dict) -> dict:
+    """The line's `dtype` is the arithmetic of the RESULTS: every returned score is recomputed
+    in float64 from the catalog's own values (rescore.hip), as the reference computes in float64
+    (constants.py:56, lib.py:51). The MFMA screen's operand type (f16 for f32 / f16 catalogs,
+    bf16 for bf16 ones) only picks candidates, certified by a rigorous error bound (DESIGN.md
+    section 3), and is named in config.arith / config.screen_operands."""
+    ops = "bf16" if cfg["dtype"] == "bf16" else "f16"
+    return {
+        "dtype": "f64",
+        "screen_operands": ops,
+        "arith": (f"results f64 (every returned score recomputed in float64 from the catalog's "
+                  f"own {cfg['dtype']} values); candidate screen on MFMA with {ops} operands and "
+                  "f32 accumulation, certified by a rigorous error bound (DESIGN.md section 3); "
+                  "uncertified queries rerun, never approximated"),
+    }
+
+
 def dry_run(args, world: int, rank: int) -> None:
     """--dry-run: the multi-rank protocol of a real run on the CPU (gloo), without the GPU
     path: rendezvous, the world-size check, K barrier-bracketed steps of one small all-gather
@@ -611,12 +628,13 @@ def main() -> None:
     # (distributed.run_sharded_steps).
     excl, excl_lists = None, None
     if args.exclude:
+        # resident in HBM like the queries: the library's device CSR (segments sorted once, as
+        # lib.py:48's rated set arrives from SQL), used as it is on every step; a caller's own
+        # unsorted device CSR would add one ebt_sort_exclusions launch per call
+        from robot_ebert_amd.search import csr_from_lists
         excl_lists = make_exclusions(cfg, args.exclude)
-        off = np.zeros(len(excl_lists) + 1, dtype=np.int64)
-        off[1:] = np.cumsum([len(e) for e in excl_lists])
-        excl = (torch.from_numpy(off).to(dev),
-                torch.from_numpy(np.concatenate(excl_lists).astype(np.int64)).to(dev))
-        log(f"exclusions: {int(off[-1])} rows over {len(excl_lists)} queries (seed 3)")
+        excl = csr_from_lists(excl_lists, dev)
+        log(f"exclusions: {int(excl[1].numel())} rows over {len(excl_lists)} queries (seed 3)")
 
     def submit():
         return ebt.score_topk_submit(cat, k, queries=q, exclude=excl, timer=timer)
@@ -756,7 +774,7 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f16",
+            "dtype": arith_labels(cfg)["dtype"],
             "data": "synthetic (seeded Gaussian catalog and queries, generated on device)",
             "config": {
                 "workload": f"{args.config}: {cfg['n']} items x d={cfg['d']} {cfg['dtype']} catalog, "
@@ -766,7 +784,8 @@ def main() -> None:
                 ((", gloo" if args.share_gpu else ", RCCL") +
                  " all-gather of each shard's entries above the catalog-wide floor + merge"
                  if world > 1 else ""),
-                "arith": "f16/bf16 MFMA screen (f32 acc) + exact f64 rescore of certified candidates",
+                "arith": arith_labels(cfg)["arith"],
+                "screen_operands": arith_labels(cfg)["screen_operands"],
                 "exclusions_per_query": (args.exclude or None),
             },
             "roofline": {

@@ -61,7 +61,12 @@ extern "C" {
  * 0.3.0: ebt_timer_count_rows / ebt_timer_rows (additive).
  * 0.3.1: eps from the measured image errors (ebt_query_image); ebt_catalog_init measures u_cat
  *        and its state holds 256 bytes more for a non-native catalog (ebt_catalog_state_bytes);
- *        ebt_cosine_sample_lead / ebt_cosine_screen_at_lead (additive). */
+ *        ebt_cosine_sample_lead / ebt_cosine_screen_at_lead (additive).
+ * 0.3.2: ebt_sort_exclusions and the full-sort path hand-written (workspace sizes shrink; host
+ *        arithmetic only); the exclusion-order check of ebt_cosine_topk* runs inside the rescore
+ *        (certified = -3 from ebt_cosine_topk_prepared / ebt_rescore's callers for a query whose
+ *        segment is not ascending); ebt_shard_sample_tiles (additive); the row counter of
+ *        ebt_timer_count_rows is device-aware. */
 int ebt_version(void);
 
 /* Message for the last non-zero return on this thread ("" if none). */
@@ -230,7 +235,8 @@ int64_t ebt_merge_block_max_groups(int32_t kprime);
  * the same positions of rows_out; positions outside every segment are copied unchanged; rows_out
  * may equal rows_in. nnz = the length of the rows array. Offsets are clamped into [0, nnz] before
  * use (a malformed CSR is then rejected by the search entry's own check). Workspace: device,
- * ebt_sort_exclusions_bytes(B, nnz) bytes (0 = invalid sizes: B < 1, nnz >= 2^31). */
+ * ebt_sort_exclusions_bytes(B, nnz) bytes (0 = invalid sizes: B < 1 or > 2^24, nnz >= 2^31;
+ * 0.3.2: one hand-written launch, 8 * nnz bytes of workspace). */
 size_t ebt_sort_exclusions_bytes(int64_t B, int64_t nnz);
 int ebt_sort_exclusions(const int64_t* off, const int64_t* rows_in, int64_t* rows_out, int64_t B,
                         int64_t nnz, void* workspace, size_t ws_bytes, void* stream);
@@ -258,6 +264,11 @@ int ebt_merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t
  * the floor all-gather (a shard's widest share of the global top k, with margin; a narrower
  * floor is still a valid lower bound). */
 int64_t ebt_shard_list_width(int32_t k, int32_t world);
+/* The shared screening threshold's sample of the row-sharded step (0.3.2, host arithmetic): the
+ * 256-row tiles each shard samples for this catalog size, world and padded batch (0 = every
+ * shard screens at its own threshold; -1 bad arguments). The same rule as distributed.py
+ * shared_sample_tiles; world * 4 * tiles <= 2048 (ebt_pool_kth's limit). */
+int64_t ebt_shard_sample_tiles(int64_t n_global, int32_t world, int64_t B_pad);
 int64_t ebt_shard_pack_cap(int64_t B, int32_t k, int32_t world, int64_t n_global);
 size_t ebt_shard_pack_bytes(int64_t B, int64_t cap);
 int ebt_shard_pack(const double* scores, const int64_t* rows, int64_t B, int32_t k,
@@ -331,8 +342,10 @@ size_t ebt_cosine_topk_workspace(int64_t B, int64_t B_pad, int64_t n_rows, int32
  * Inputs: the query batch prepared by ebt_query_* (q64, qimg, qscale, eps; B real rows, B_pad
  * image rows), the catalog (cat/dtype/ld with gnorm64; its screening image cimg with cscale or
  * NULL, ld_img, d_pad), exclusions as CSR of GLOBAL rows (NULL = none), k <= kprime.
- * Outputs: out_scores (float64 [B][k]), out_rows (int64 [B][k], global), certified (int32 [B]).
- * timer (NULL or an ebt_timer) collects per-stage GPU time. */
+ * Outputs: out_scores (float64 [B][k]), out_rows (int64 [B][k], global), certified (int32 [B]);
+ * certified[b] = -3 when query b's exclusion segment is not ascending (checked by the rescore,
+ * 0.3.2: its results are then not valid). timer (NULL or an ebt_timer) collects per-stage GPU
+ * time. */
 int ebt_cosine_topk_prepared(const double* q64, const void* qimg, const float* qscale, const float* eps,
                     int64_t B, int64_t B_pad, const void* cat, int dtype, int64_t ld,
                     const double* gnorm64, const void* cimg, const float* cscale, int img_dtype,
@@ -688,8 +701,10 @@ int ebt_timer_begin(void* timer, int stage, void* stream);
 int ebt_timer_end(void* timer, int stage, void* stream);
 /* Row accounting for the top-K roofline (bench.py `roofline_topk`): with on != 0 the timer owns
  * one device counter (allocated on the current device) to which every rescore kernel recorded
- * under EBT_STAGE_RESCORE adds the candidate rows it gathered (one atomic per query);
- * ebt_timer_reset zeroes it, ebt_timer_rows reads it (synchronise the launch streams first).
+ * under EBT_STAGE_RESCORE on a stream of that device adds the candidate rows it gathered (one
+ * atomic per query; launches on another device's streams are not counted, 0.3.2);
+ * ebt_timer_reset zeroes it, ebt_timer_rows reads it (on the counter's device whatever device
+ * is current; synchronise the launch streams first).
  * on = 0 frees it. Costs nothing when off. */
 int ebt_timer_count_rows(void* timer, int on);
 int ebt_timer_rows(void* timer, int64_t* rows);

@@ -105,6 +105,7 @@ _SIGNATURES = {
     "ebt_rccl_all_gather": ([_VP, _VP, _VP, _SZ, _VP], _INT),
     "ebt_rccl_all_reduce_f64": ([_VP, _VP, _SZ, _VP], _INT),
     "ebt_shard_list_width": ([_I32, _I32], _I64),
+    "ebt_shard_sample_tiles": ([_I64, _I32, _I64], _I64),
     "ebt_shard_pack_cap": ([_I64, _I32, _I32, _I64], _I64),
     "ebt_shard_pack_bytes": ([_I64, _I64], _SZ),
     "ebt_shard_pack": ([_VP, _VP, _I64, _I32, _VP, _I64, _VP, _VP], _INT),

@@ -100,15 +100,38 @@ class RecBatcher:
         """Queue one user's request; the Future resolves to (scores [k'], rows [k']) numpy arrays
         (k' <= k: fewer when the catalog has fewer candidates) or raises the request's error."""
         fut: Future = Future()
+        # every request is checked HERE, before it can share a batch: the batch is one library
+        # call, and an argument the library rejects (a liked row outside the catalog, a k whose
+        # workspace cannot exist) would fail every co-batched request, other clients' included
+        try:
+            k = int(k)
+            liked = [int(r) for r in liked_rows]
+            rated = [int(r) for r in exclude_rows]
+        except (TypeError, ValueError, OverflowError) as e:
+            fut.set_exception(ValueError(f"malformed request: {e}"))
+            return fut
         if k < 1:
             fut.set_exception(ValueError("k must be >= 1"))
             return fut
-        if len(liked_rows) == 0:  # lib.py:51 with an empty X -> sklearn check_pairwise_arrays
+        if len(liked) == 0:  # lib.py:51 with an empty X -> sklearn check_pairwise_arrays
             fut.set_exception(ValueError(
                 f"Found array with 0 sample(s) (shape=(0, {self.catalog.d})) while a minimum of 1 "
                 "is required by check_pairwise_arrays."))
             return fut
-        item = (list(liked_rows), sorted(set(int(r) for r in exclude_rows)), int(k), fut)
+        lo = int(getattr(self.catalog, "row_offset", 0))
+        n = int(getattr(self.catalog, "n", 0))
+        hi = lo + n
+        if n > 0 and any(r < lo or r >= hi for r in liked):
+            bad = next(r for r in liked if r < lo or r >= hi)
+            fut.set_exception(ValueError(f"liked row {bad} is not in the catalog rows [{lo}, {hi})"))
+            return fut
+        # rated rows outside the catalog cannot match a candidate: dropped, as lib.py:48's
+        # catalog.index.difference(rated) ignores unknown ids. k past the catalog returns every
+        # candidate (the Future holds at most n rows): the same answer from a k the library can size
+        if n > 0:
+            rated = [r for r in rated if lo <= r < hi]
+            k = min(k, int(getattr(self.catalog, "n_global", n)))
+        item = (liked, sorted(set(rated)), k, fut)
         with self._lock:   # a request is either queued before close()'s sentinel or refused
             if self._closed:
                 fut.set_exception(RuntimeError("batcher is closed"))

@@ -123,7 +123,8 @@ int mask_excluded(float*, int64_t, int64_t, int64_t, int64_t, const int64_t*, co
 int rescore(const double*, int64_t, int32_t, const void*, int, int64_t, const double*, int64_t,
             const float*, const int64_t*, int32_t, int32_t, int64_t, const float*, const double*,
             double*, int64_t*, int32_t*, hipStream_t, const int*, int, unsigned long long*,
-            int64_t list_base = 0, const float* theta = nullptr);
+            int64_t list_base = 0, const float* theta = nullptr,
+            const int64_t* excl_off = nullptr, const int64_t* excl_rows = nullptr);
 int screen_gemm_filter(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
                        const float*, const float*, const float*, uint64_t*, int64_t, int,
                        uint8_t*, int64_t, int*, int64_t, hipStream_t);
@@ -221,11 +222,28 @@ struct Timer {
 
 // 64 row counters 128 bytes apart (the rescore's workgroup b adds to counter b % 64)
 constexpr size_t TIMER_ROW_BYTES = 64 * 128;
-// The row counters the rescore adds to, when counting is on and the rescore stage is recorded
-static unsigned long long* timer_rows(void* timer) {
+// The row counters the rescore adds to, when counting is on, the rescore stage is recorded and
+// the launch goes to the counters' own device (a rescore on another device's stream is not
+// counted: its atomics would land in a peer's memory)
+static unsigned long long* timer_rows(void* timer, hipStream_t st) {
   Timer* t = (Timer*)timer;
   if (!t || !t->d_rows || !((t->mask >> EBT_STAGE_RESCORE) & 1u)) return nullptr;
-  return t->d_rows;
+  int dev = -1;
+  if (st ? hipStreamGetDevice(st, &dev) != hipSuccess : hipGetDevice(&dev) != hipSuccess)
+    return nullptr;
+  return dev == t->rows_dev ? t->d_rows : nullptr;
+}
+
+// runs f with the timer's counter device current (restored afterwards)
+template <class F>
+static int on_rows_dev(const Timer* t, F f) {
+  int cur = -1;
+  int rc = hip_check(hipGetDevice(&cur), "hipGetDevice");
+  if (rc) return rc;
+  if (cur != t->rows_dev && (rc = hip_check(hipSetDevice(t->rows_dev), "hipSetDevice"))) return rc;
+  rc = f();
+  if (cur != t->rows_dev) (void)hipSetDevice(cur);
+  return rc;
 }
 
 struct StageScope {
@@ -502,14 +520,20 @@ static WsLayout ws_layout(int64_t B, int64_t B_pad, int64_t n_rows, int32_t kpri
   size_t o = 0;
   L.off_s = o;
   o = align_up(o + (size_t)B_pad * L.ld_s * 4);
+  // the streaming select's per-segment and per-chunk lists: only head_topk (the unfused path,
+  // the float64 screen and the progressive screen's head) selects from score rows; the
+  // speculative screen's sample writes pooled maxima instead, so its layout has none of them
+  // (round 6: C5's first pass carried 14.7 GiB of unused chunk lists, 16384 queries x 64 sample
+  // "chunks" x k' 1256 x 12 bytes -- 23.2 -> 8.4 GiB per batch)
+  const bool selects = !L.spec;
   L.off_segv = o;
-  if (L.segs > 1) o = align_up(o + (size_t)B * L.segs * kprime * 4);
+  if (selects && L.segs > 1) o = align_up(o + (size_t)B * L.segs * kprime * 4);
   L.off_segi = o;
-  if (L.segs > 1) o = align_up(o + (size_t)B * L.segs * kprime * 8);
+  if (selects && L.segs > 1) o = align_up(o + (size_t)B * L.segs * kprime * 8);
   L.off_chv = o;
-  if (L.n_chunks > 1) o = align_up(o + (size_t)B * L.n_chunks * kprime * 4);
+  if (selects && L.n_chunks > 1) o = align_up(o + (size_t)B * L.n_chunks * kprime * 4);
   L.off_chi = o;
-  if (L.n_chunks > 1) o = align_up(o + (size_t)B * L.n_chunks * kprime * 8);
+  if (selects && L.n_chunks > 1) o = align_up(o + (size_t)B * L.n_chunks * kprime * 8);
   L.off_fv = o;
   o = align_up(o + (size_t)B * kprime * 4);
   L.off_fi = o;
@@ -607,11 +631,12 @@ int rescore_sharded(const double* q64, int64_t B, int32_t d, const void* cat, in
                     const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows,
                     const float* eps, const double* t_floor, double* out_s, int64_t* out_r,
                     int32_t* certified, const int* ovf, const float* theta, void* timer,
-                    hipStream_t st, int64_t list_base) {
+                    hipStream_t st, int64_t list_base, const int64_t* excl_off,
+                    const int64_t* excl_rows) {
   StageScope sc(timer, EBT_STAGE_RESCORE, st);
   return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, cand_vals, cand_rows,
                  kprime, k, n_rows, eps, t_floor, out_s, out_r, certified, st, ovf, 0,
-                 timer_rows(timer), list_base, theta);
+                 timer_rows(timer, st), list_base, theta, excl_off, excl_rows);
 }
 
 }  // namespace ebt
@@ -620,7 +645,7 @@ using namespace ebt;
 
 extern "C" {
 
-int ebt_version(void) { return 301; }  // 0.3.1: measured image errors in eps (see ebert.h)
+int ebt_version(void) { return 302; }  // 0.3.2: hand-written sorts, folded checks (ebert.h)
 
 const char* ebt_last_error(void) { return g_err; }
 
@@ -711,7 +736,7 @@ int ebt_rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dt
   StageScope sc(timer, EBT_STAGE_RESCORE, (hipStream_t)stream);
   return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, cand_vals, cand_rows, kprime, k,
                  n_rows, eps, t_floor, out_scores, out_rows, certified, (hipStream_t)stream,
-                 nullptr, 0, timer_rows(timer));
+                 nullptr, 0, timer_rows(timer, (hipStream_t)stream));
 }
 
 int ebt_screen_exact(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
@@ -1191,9 +1216,11 @@ int ebt_cosine_topk_prepared(const double* q64, const void* qimg, const float* q
   rc = run_screen(a, L, ws, fv, fi, timer, st, &so);
   if (rc) return rc;
   StageScope s(timer, EBT_STAGE_RESCORE, st);
+  // (the rescore also checks each query's exclusion segment: certified = -3 when it is not
+  // sorted ascending -- the check the C entry used to launch on its own, with a flag memset)
   return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, fv, fi, kprime, k, n_rows,
                  so.eps, nullptr, out_scores, out_rows, certified, st, so.ovf, 0,
-                 timer_rows(timer));
+                 timer_rows(timer, st), 0, nullptr, excl_off, excl_rows);
 }
 
 int ebt_cosine_screen(const double* q64, const void* qimg, const float* qscale, const float* eps,
@@ -1418,7 +1445,10 @@ int ebt_timer_reset(void* timer) {
   t->recs.clear();
   t->open.clear();
   t->used = 0;
-  if (t->d_rows) return hip_check(hipMemset(t->d_rows, 0, TIMER_ROW_BYTES), "hipMemset");
+  if (t->d_rows)
+    return on_rows_dev(t, [&] {
+      return hip_check(hipMemset(t->d_rows, 0, TIMER_ROW_BYTES), "hipMemset");
+    });
   return EBT_OK;
 }
 
@@ -1427,7 +1457,7 @@ int ebt_timer_count_rows(void* timer, int on) {
   Timer* t = (Timer*)timer;
   std::lock_guard<std::mutex> g(t->mu);
   if (!on) {
-    if (t->d_rows) (void)hipFree(t->d_rows);
+    if (t->d_rows) (void)on_rows_dev(t, [&] { return hip_check(hipFree(t->d_rows), "hipFree"); });
     t->d_rows = nullptr;
     return EBT_OK;
   }
@@ -1447,7 +1477,9 @@ int ebt_timer_rows(void* timer, int64_t* rows) {
   unsigned long long v[TIMER_ROW_BYTES / 8];
   // hipMemcpy waits for the work before it on the null stream; the caller synchronises the
   // launch streams first (as for ebt_timer_query)
-  int rc = hip_check(hipMemcpy(v, t->d_rows, TIMER_ROW_BYTES, hipMemcpyDeviceToHost), "hipMemcpy");
+  int rc = on_rows_dev(t, [&] {
+    return hip_check(hipMemcpy(v, t->d_rows, TIMER_ROW_BYTES, hipMemcpyDeviceToHost), "hipMemcpy");
+  });
   int64_t tot = 0;
   for (int i = 0; i < 64; ++i) tot += (int64_t)v[i * 16];
   *rows = tot;

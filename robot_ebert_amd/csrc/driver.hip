@@ -31,7 +31,8 @@ int large_topk(const double*, int64_t, int32_t, const void*, int, int64_t, const
 int rescore_sharded(const double*, int64_t, int32_t, const void*, int, int64_t, const double*,
                     int64_t, const float*, const int64_t*, int32_t, int32_t, int64_t, const float*,
                     const double*, double*, int64_t*, int32_t*, const int*, const float*, void*,
-                    hipStream_t, int64_t list_base);
+                    hipStream_t, int64_t list_base, const int64_t* excl_off,
+                    const int64_t* excl_rows);
 int screen_at_local(const double*, const void*, const float*, const float*, int64_t, int64_t,
                     const void*, int, int64_t, const double*, const void*, const float*, int,
                     int32_t, int64_t, int32_t, int32_t, int64_t, const int64_t*, const int64_t*,
@@ -507,9 +508,10 @@ int ebt_cosine_topk_submit(const ebt_catalog* cat, const void* q, int q_dtype, i
                       L.flags, ws + L.off_pass, L.pass_bytes, rs, rr, cert, timer, st);
   }
   if (rc) return rc;
-  // the exclusion check's flag sits right after the certificates: one copy brings both
-  // (without exclusions the flag is neither set nor read)
-  if (excl_off) {
+  // the exclusion check: the rescore's certificate -3 (ebt_cosine_topk_prepared); the full-sort
+  // path has no rescore, so its flag sits right after the certificates, one copy bringing both
+  // (otherwise the flag is neither set nor read)
+  if (excl_off && L.large) {
     rc = hip_check(hipMemsetAsync(cert + B, 0, 4, st), "hipMemsetAsync");
     if (rc) return rc;
     hipLaunchKernelGGL(csr_sorted_kernel, dim3((unsigned)B), dim3(256), 0, st, excl_off,
@@ -517,7 +519,8 @@ int ebt_cosine_topk_submit(const ebt_catalog* cat, const void* q, int q_dtype, i
     rc = launch_check("csr_sorted_kernel");
     if (rc) return rc;
   }
-  rc = hip_check(hipMemcpyAsync(cert_host, cert, (size_t)(B + 1) * 4, hipMemcpyDeviceToHost, st),
+  rc = hip_check(hipMemcpyAsync(cert_host, cert, (size_t)(B + (excl_off && L.large)) * 4,
+                               hipMemcpyDeviceToHost, st),
                  "hipMemcpyAsync");
   if (rc) return rc;
   hipEvent_t ev = event_get(st);
@@ -568,7 +571,12 @@ int ebt_cosine_topk_finish(ebt_pending* p) {
     set_error("ebt_cosine_topk_finish: bad pending batch");
     return EBT_EINVAL;
   }
-  if (p->excl_off && p->cert_host[B] != 0) {
+  const bool unsorted_excl = p->excl_off && (L.large ? p->cert_host[B] != 0 : [&] {
+    for (int64_t b = 0; b < B; ++b)
+      if (p->cert_host[b] == -3) return true;
+    return false;
+  }());
+  if (unsorted_excl) {
     set_error("ebt_cosine_topk: exclusion rows must be sorted ascending within each query");
     return EBT_EINVAL;
   }
@@ -776,7 +784,10 @@ int64_t sh_tiles(int64_t n_global, int world, int64_t B_pad) {
   if (P / per * per >= 8) P = P / per * per;
   // a sample GEMM of less than one round of the persistent grid takes a round's time anyway:
   // fill it (C3 on 8 ranks: 8 -> 16 tiles per shard, room for the lead)
-  if (P < per && per <= full / 6) P = per;
+  // (only while the fill stays within the sample's caps: at B_pad = 512 a round is 128 tiles,
+  // and 8 ranks x 4 x 128 maxima would exceed ebt_pool_kth's 2048 -- distributed.py alike)
+  if (P < per && per <= full / 6 && per <= SH_SAMPLE_TILES_MAX && world * 4 * per <= 2048)
+    P = per;
   return (P >= 1 && world * P >= 8) ? P : 0;
 }
 
@@ -813,7 +824,7 @@ bool shard_layout(const ebt_catalog& c, const ebt_comm& cm, int64_t B, int32_t k
                 : sh_tiles(cm.n_global, cm.world, D.B_pad);
   L.G = 4 * L.tiles;
   L.RG = R * L.G;
-  if (L.RG > 2048) L.tiles = L.G = L.RG = 0;  // ebt_pool_kth's limit (not reached: <= 8 x 32)
+  if (L.RG > 2048) L.tiles = L.G = L.RG = 0;  // ebt_pool_kth's limit (sh_tiles keeps within it)
   // theta = the j-th largest of all R G maxima, j <= J (J from the catalog-wide k', rank-
   // invariant, >= every rank's own j): the j-th of the union of each shard's J largest is the
   // same value, so each shard sends its J largest (+ a -inf column: ebt_floor_pack's layout)
@@ -1154,20 +1165,14 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
   int32_t* cert = (int32_t*)(ws + L.off_cert);
   // (the list's rows read as they are: local at the shared threshold, global otherwise; the
   // certificate with ebt_certify_cut's tests)
+  // (the rescore also checks the exclusion segments' order: certificate -3)
   rc = rescore_sharded(q64, B, c.d, c.data, c.dtype, c.ld, c.gnorm64, c.row_offset, lv, lr,
                        L.kprime, L.k_eff, c.n, eps_p, tfloor, rs, rr, cert, ovf_p,
-                       use_theta ? theta : nullptr, timer, st, use_theta ? 0 : c.row_offset);
+                       use_theta ? theta : nullptr, timer, st, use_theta ? 0 : c.row_offset,
+                       excl_off, excl_rows);
   if (rc) return rc;
-  if (excl_off) {
-    rc = hip_check(hipMemsetAsync(cert + B, 0, 4, st), "hipMemsetAsync");
-    if (rc) return rc;
-    hipLaunchKernelGGL(csr_sorted_kernel, dim3((unsigned)B), dim3(256), 0, st, excl_off,
-                       excl_rows, cert + B);
-    rc = launch_check("csr_sorted_kernel");
-    if (rc) return rc;
-  }
-  // the certificates (and the exclusion flag) to the caller's host buffer; one event for them
-  rc = hip_check(hipMemcpyAsync(host, cert, (size_t)(B + 1) * 4, hipMemcpyDeviceToHost, st),
+  // the certificates to the caller's host buffer; one event for them
+  rc = hip_check(hipMemcpyAsync(host, cert, (size_t)B * 4, hipMemcpyDeviceToHost, st),
                  "hipMemcpyAsync");
   if (rc) return rc;
   hipEvent_t ev = event_get(st);
@@ -1287,6 +1292,11 @@ int ebt_cosine_topk_sharded_wait(ebt_sharded_pending* p) {
   rc = sh_full_merge(S, p->comm, lp.ws, lp.B, lp.k, p->out_scores, p->out_rows, lp.timer, st);
   if (!rc) rc = hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
   return rc;
+}
+
+int64_t ebt_shard_sample_tiles(int64_t n_global, int32_t world, int64_t B_pad) {
+  if (n_global < 1 || world < 1 || B_pad < 1) return -1;
+  return sh_tiles(n_global, world, B_pad);
 }
 
 int ebt_cosine_topk_sharded(const ebt_catalog* cat, const ebt_comm* comm, const void* q,

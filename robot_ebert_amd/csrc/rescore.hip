@@ -156,14 +156,15 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     const float* __restrict__ eps, const double* __restrict__ t_floor, double* __restrict__ out_s,
     int64_t* __restrict__ out_r, int32_t* __restrict__ certified, const int* __restrict__ ovf_cnt,
     int ovf_cap, unsigned long long* __restrict__ gathered, int64_t list_base,
-    const float* __restrict__ theta) {
+    const float* __restrict__ theta, const int64_t* __restrict__ excl_off,
+    const int64_t* __restrict__ excl_rows) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* qs = (double*)smem;                           // d (NU = 0 only)
   double* sc = qs + (NU > 0 ? 0 : ((d + 1) & ~1));      // kpp: approx, then exact
   int64_t* rw = (int64_t*)(sc + kpp);         // kpp
   int* pl = (int*)(rw + kpp);                 // kpp: list position of each kept row
   int* ix = pl + kpp;                         // kpp (NU > 0): the rows of the current pass
-  __shared__ int nvalid, corrupt, nkeep, ntop, nsel, ngath;
+  __shared__ int nvalid, corrupt, nkeep, ntop, nsel, ngath, xbad;
   __shared__ unsigned long long smin_key;
   constexpr int NW = RTHREADS / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -179,10 +180,21 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     ntop = 0;
     nsel = 0;
     ngath = 0;
+    xbad = 0;
     smin_key = ~0ull;
   }
   constexpr int ES = (DT == EBT_F64) ? 8 : (DT == EBT_F32 ? 4 : 2);
   constexpr int PER = 16 / ES;
+  // the query's exclusion segment must be sorted ascending (the merges drop excluded rows by
+  // binary search): checked here, one pass over its few rows, certified = -3 otherwise -- the
+  // C entry's separate check kernel and flag memset folded into the kernel that writes the
+  // certificate (set after the barrier below, read after the next)
+  bool xb = false;
+  if (excl_off) {
+    const int64_t xs = excl_off[b], xe = excl_off[b + 1];
+    xb = xe < xs;
+    for (int64_t t = xs + tid; t + 1 < xe; t += RTHREADS) xb |= excl_rows[t] > excl_rows[t + 1];
+  }
   // NU > 0: the lane's query values of chunks lane + 64 u (0 past the row)
   double qv[NU > 0 ? NU : 1][PER];
   if constexpr (NU > 0) {
@@ -212,6 +224,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
   double cut = (double)cv[k - 1] - 2.0 * (double)eps[b];
   if (t_floor && t_floor[b] - (double)eps[b] > cut) cut = t_floor[b] - (double)eps[b];
   __syncthreads();
+  if (xb) xbad = 1;
   // 1. the whole list at once (no per-candidate load latency): count valid rows, flag corrupt
   //    ones, compact the rows above the cut into rw[0, nkeep)
   for (int c0 = 0; c0 < kprime; c0 += RTHREADS) {
@@ -512,6 +525,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     // global top k (ebt_certify_cut's test, folded in)
     if (theta && t_floor && !((double)theta[b] <= t_floor[b] - (double)eps[b])) ok = -1;
     if (corrupt) ok = -2;                           // internal error: row out of range
+    if (xbad) ok = -3;                              // caller error: unsorted exclusion segment
     certified[b] = ok;
     // rows gathered by the two passes (roofline accounting: ebt_timer_count_rows), spread over
     // 64 counters 128 bytes apart: one address taking every query's atomic serialised them and
@@ -761,7 +775,8 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
             const int64_t* cand_rows, int32_t kprime, int32_t k, int64_t n_rows, const float* eps,
             const double* t_floor, double* out_s, int64_t* out_r, int32_t* certified,
             hipStream_t st, const int* ovf_cnt, int ovf_cap, unsigned long long* gathered,
-            int64_t list_base, const float* theta) {
+            int64_t list_base, const float* theta, const int64_t* excl_off,
+            const int64_t* excl_rows) {
   if (!q64 || !cat || !gnorm || !cand_vals || !cand_rows || !eps || !out_s || !out_r ||
       !certified || B < 0 || d <= 0 || ld < d || k < 1 || kprime < k || kprime > 4096 ||
       dtype < 0 || dtype > 3) {
@@ -782,8 +797,9 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
 #ifdef EBT_RESCORE_LDS
   // Measured and not the default (profiles/r3/rescore_lds_ab.txt): the LDS-DMA batches
   // (16 rows of 1.5 KiB per round trip at C2) took 71-75 us per C2 step against 59-60 us for the
-  // register gather, interleaved on one MI355X; C3 0.616 vs 0.564 ms. Kept for that A/B.
-  if (vec) {
+  // register gather, interleaved on one MI355X; C3 0.616 vs 0.564 ms. Kept for that A/B (it
+  // does not take the exclusion check: a call with exclusions uses the register form).
+  if (vec && !excl_off) {
     const int row_bytes = d * es;
     int R = (24 << 10) / row_bytes;
     R = R > 64 ? 64 : R;
@@ -819,7 +835,7 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
   hipLaunchKernelGGL((rescore_kernel<DT, true, NU>), grid, block, lds_r, st, q64, d, cat, ld,   \
                      gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,      \
                      t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap, gathered, list_base,   \
-                     theta);
+                     theta, excl_off, excl_rows);
 #define EBT_RSR_NU(DT)                                                                          \
   switch (nu) {                                                                                 \
     case 1: EBT_RSR(DT, 1) break;                                                               \
@@ -846,12 +862,12 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
     hipLaunchKernelGGL((rescore_kernel<DT, true>), grid, block, lds, st, q64, d, cat, ld,       \
                        gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,    \
                        t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap, gathered, list_base, \
-                       theta);                                                                  \
+                       theta, excl_off, excl_rows);                                                                  \
   else                                                                                          \
     hipLaunchKernelGGL((rescore_kernel<DT, false>), grid, block, lds, st, q64, d, cat, ld,      \
                        gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,    \
                        t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap, gathered, list_base, \
-                       theta);
+                       theta, excl_off, excl_rows);
   switch (dtype) {
     case EBT_F32: EBT_RS(EBT_F32) break;
     case EBT_BF16: EBT_RS(EBT_BF16) break;

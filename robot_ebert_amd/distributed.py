@@ -270,7 +270,8 @@ def shared_sample_tiles(n_global: int, world: int, B_pad: int) -> int:
     if P // per * per >= 8:
         P = P // per * per
     # less than one round of the persistent grid takes a round's time anyway: fill it
-    if P < per and per <= full // 6:
+    # (only within the sample's caps: ebt_pool_kth takes at most 2048 maxima per query)
+    if P < per and per <= full // 6 and per <= SAMPLE_TILES_MAX and world * 4 * per <= 2048:
         P = per
     return P if P >= 1 and world * P >= 8 else 0
 

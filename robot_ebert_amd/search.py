@@ -71,6 +71,16 @@ class QueryBatch:
         return QueryBatch(self.q64.index_select(0, idx).contiguous(), qimg, qscale, eps, n)
 
 
+class SortedCSR(tuple):
+    """(offsets, rows) of a device CSR the library built with every segment sorted ascending
+    (csr_from_lists, csr_sorted): passed back as `exclude`, it is used as it is -- no re-sort per
+    call. (The rescore checks each segment's order anyway, folded into the kernel that writes the
+    certificates: an unsorted segment fails the call, it is never silently misread.)"""
+
+    def __new__(cls, off: torch.Tensor, rows: torch.Tensor):
+        return super().__new__(cls, (off, rows))
+
+
 def csr_from_lists(lists: Sequence[Sequence[int]], device) -> Tuple[torch.Tensor, torch.Tensor]:
     """Host lists of row ids -> device CSR (offsets int64 [B+1], rows int64 [nnz]), each segment
     sorted (ebt_cosine_topk_prepared binary-searches them). numpy builds it (a batch of a few
@@ -87,15 +97,17 @@ def csr_from_lists(lists: Sequence[Sequence[int]], device) -> Tuple[torch.Tensor
     else:
         both[B + 1] = 0
     t = torch.from_numpy(both).to(device)
-    return t[:B + 1], t[B + 1:]
+    return SortedCSR(t[:B + 1], t[B + 1:])
 
 
-def csr_sorted(off: torch.Tensor, rows: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+def csr_sorted(off, rows: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """A caller's device CSR with every segment sorted ascending (the fused merge drops excluded
     rows by binary search over the segment, so an unsorted segment would silently keep rated
     rows): ebt_sort_exclusions, the library's own segmented sort. Offsets are absolute positions
     into `rows` (off[0] may be > 0); positions outside every segment keep their value. Returns
-    (off, sorted copy of rows)."""
+    (off, sorted copy of rows) as a SortedCSR (a caller may keep it and pass it on every call)."""
+    if isinstance(off, SortedCSR):   # csr_sorted(*sorted_csr) or csr_sorted(sorted_csr)
+        return off
     require_cuda(off, "exclusion offsets")
     require_cuda(rows, "exclusion rows")
     if off.dtype != torch.int64 or rows.dtype != torch.int64:
@@ -104,7 +116,7 @@ def csr_sorted(off: torch.Tensor, rows: torch.Tensor) -> Tuple[torch.Tensor, tor
     nnz = int(rows.numel())
     B = int(off.numel()) - 1
     if nnz <= 1 or B < 1:
-        return off, rows
+        return SortedCSR(off, rows)
     need = _lib.load().ebt_sort_exclusions_bytes(B, nnz)
     if need == 0:
         raise EbertError(f"exclusion CSR of {B} segments / {nnz} rows cannot be sorted")
@@ -112,7 +124,7 @@ def csr_sorted(off: torch.Tensor, rows: torch.Tensor) -> Tuple[torch.Tensor, tor
     out = torch.empty_like(rows)
     call("ebt_sort_exclusions", ptr(off), ptr(rows), ptr(out), B, nnz, ptr(ws), need,
          stream_of(rows.device))
-    return off, out
+    return SortedCSR(off, out)
 
 
 def csr_subset(off: torch.Tensor, rows: torch.Tensor, idx: torch.Tensor):
@@ -449,7 +461,7 @@ def _submit_c(catalog: Catalog, k: int, queries, liked, exclude, kprime, chunk_r
         raise EbertError("pass exactly one of queries= or liked=")
     if exclude is not None:
         exclude = (csr_from_lists(exclude, dev) if not isinstance(exclude, tuple)
-                   else csr_sorted(*exclude))
+                   else exclude if isinstance(exclude, SortedCSR) else csr_sorted(*exclude))
     q_ptr, q_dt, ldq, lo, lr = None, 0, 0, None, None
     if queries is not None:
         require_cuda(queries, "queries")
@@ -512,7 +524,7 @@ def score_topk_stages(catalog: Catalog, k: int, queries: Optional[torch.Tensor] 
         liked = csr_from_lists(liked, dev)
     if exclude is not None:
         exclude = (csr_from_lists(exclude, dev) if not isinstance(exclude, tuple)
-                   else csr_sorted(*exclude))
+                   else exclude if isinstance(exclude, SortedCSR) else csr_sorted(*exclude))
     if theta_hook is not None and t_floor_hook is None:
         raise EbertError("theta_hook needs t_floor_hook (the threshold is verified against it)")
     with region(timer, "prep", dev):
@@ -565,6 +577,8 @@ def score_topk_finish(p) -> Tuple[torch.Tensor, torch.Tensor]:
     while True:
         if flat is None:
             flat = cert.cpu()
+        if bool((flat == -3).any()):   # the rescore's check of the exclusion segments
+            raise EbertError("exclusion rows must be sorted ascending within each query")
         if bool((flat == -2).any()):
             raise EbertError("internal error: candidate row out of range (libebert bug)")
         over = torch.nonzero(flat == -1).flatten().to(dev)

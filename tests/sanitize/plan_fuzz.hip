@@ -99,9 +99,11 @@ int main() {
           for (int32_t k : {1, 10, 100, 1000, 4096, 5000}) {
             ++cases;
             const size_t ws = ebt_workspace_bytes(&c, B, k, nullptr);
+            // min(k, n) <= 4096: the screen; beyond it the full-sort path (large_k.hip), whose
+            // sizing is host arithmetic since round 6 (no device query): every case is valid
             const bool ok = (k < n ? k : n) <= 4096;
-            CHECK((ws > 0) == ok, "driver ws n=%lld B=%lld k=%d -> %zu", (long long)n,
-                  (long long)B, k, ws);
+            CHECK(ws > 0, "driver ws n=%lld B=%lld k=%d -> %zu", (long long)n, (long long)B, k,
+                  ws);
             ebt_options o{};
             o.kprime = 4 * k;
             o.chunk_rows = 4096;

@@ -112,3 +112,14 @@ def test_exclusion_variant_parity():
     bad = bench.oracle_parity(CFG["k"], blocks(), q, torch.from_numpy(s0),
                               torch.from_numpy(r0), CFG["b"], "test", exclude=ex)
     assert not bad["rows_bit_exact"] and bad["excluded_rows_returned"] >= 1
+
+
+def test_line_dtype_is_the_result_arithmetic():
+    """the line's `dtype` names the arithmetic of the returned scores (float64,
+    the reference's own: constants.py:56, lib.py:51), not the screen's operand type, which
+    config.arith / config.screen_operands carry."""
+    for name, ops in (("C2", "bf16"), ("C3", "f16"), ("C4", "bf16"), ("C5", "f16")):
+        lab = bench.arith_labels(bench.CONFIGS[name])
+        assert lab["dtype"] == "f64"
+        assert lab["screen_operands"] == ops
+        assert "f64" in lab["arith"] and ops in lab["arith"] and "certified" in lab["arith"]

@@ -95,7 +95,11 @@ def test_self_contained_sizing_without_gpu():
     ws = lib.ebt_workspace_bytes(ctypes.byref(cat), 4096, 100, None)
     first = lib.ebt_cosine_topk_workspace(4096, 4096, n, 200, (4 << 30) // (4 * 4096) // 128 * 128, 0)
     assert ws > first > 0                            # first pass + retry area + prepared queries
-    assert lib.ebt_workspace_bytes(ctypes.byref(cat), 4096, 5000, None) == 0   # k > 4096 < n
+    # k > 4096 < n: the full-sort path (large_k.hip, hand-written since round 6: its sizing is
+    # host arithmetic too -- the CUB-compatible sort it replaced asked the device for its
+    # temporaries, so without a GPU this used to read 0): two [Bg, n] (key, row) buffers
+    big = lib.ebt_workspace_bytes(ctypes.byref(cat), 4096, 5000, None)
+    assert big >= 2 * 12 * n
     bad = _lib.EbtOptions(kprime=0, flags=0, chunk_rows=100)                   # not % 128
     assert lib.ebt_workspace_bytes(ctypes.byref(cat), 4096, 100, ctypes.byref(bad)) == 0
 
@@ -238,6 +242,26 @@ def test_shared_threshold_plan():
             assert (b - a) // 256 >= P
 
 
+def test_shared_sample_tiles_c_and_python_agree():
+    """the sample's fill to one round of the persistent grid stays within the caps
+    (<= 64 tiles per shard, world * 4 * tiles <= 2048 maxima per query, ebt_pool_kth's limit) in
+    C (driver.hip sh_tiles, through ebt_shard_sample_tiles) and Python
+    (distributed.shared_sample_tiles) alike: the two paths take the same decision for every
+    config, e.g. B_pad = 512 on 8 ranks with 196K-300K-row shards (a round there is 128 tiles)."""
+    from robot_ebert_amd import _lib
+    from robot_ebert_amd.distributed import shared_sample_tiles
+    lib = _lib.load()
+    for world in (1, 2, 3, 4, 8, 16):
+        for B_pad in (128, 256, 512, 1024, 2048, 4096, 16384):
+            for n in (20_000, 100_000, 1_000_000, 1_570_000, 2_000_000, 2_400_000, 10_000_000):
+                c = lib.ebt_shard_sample_tiles(n, world, B_pad)
+                p = shared_sample_tiles(n, world, B_pad)
+                assert c == p, (n, world, B_pad, c, p)
+                assert 0 <= p <= 64 and world * 4 * p <= 2048
+    assert shared_sample_tiles(8 * 250_000, 8, 512) > 0      # still shared, just not filled
+    assert lib.ebt_shard_sample_tiles(0, 8, 512) == -1
+
+
 def test_workspace_size_does_not_depend_on_the_lead_knob():
     """ebt_spec_lead changes whether the speculative sample's lead is used, never the workspace
     layout: a workspace sized with the knob in one state still fits the other (round 5)."""
@@ -297,3 +321,50 @@ def test_sample_lead_argument_checks():
     assert call(10, 11, 2, None, 512) == -1                    # lead without its scores
     assert call(0, 1, 0, None, 0) == -1 and call(4, 0, 0, None, 0) == -1
     assert call(4, 2, -1, None, 0) == -1
+
+
+def _fake_catalog(n, d, dt):
+    from robot_ebert_amd import _lib
+    fake = 1 << 30
+    native = dt in (_lib.EBT_F16, _lib.EBT_BF16)
+    return _lib.EbtCatalog(data=fake, dtype=dt, d=d, n=n, ld=d, row_offset=0, gnorm64=fake,
+                           inv32=fake, image=fake, cscale=fake if native else None,
+                           img_dtype=dt if native else _lib.EBT_F16, ld_img=d, d_pad=d,
+                           native=int(native), u_cat=0.0 if native else 2.0 ** -11)
+
+
+@pytest.mark.parametrize("name,N,d,es,B,k", [("C4", 10_000_000, 768, 2, 8192, 100),
+                                              ("C5", 50_000_000, 1536, 2, 16384, 1000),
+                                              ("C3", 1_000_000, 1536, 4, 4096, 100)])
+@pytest.mark.parametrize("all_reduce", [False, True])
+def test_eight_gpu_memory_budget(name, N, d, es, B, k, all_reduce):
+    """one rank of the 8-GPU step at the BASELINE shapes fits 0.8 x 288 GB by
+    construction -- its shard, the catalog state (norms, inverse norms, image), ShardedTopk's
+    default 3 slots of ebt_sharded_workspace_bytes, each slot's outputs and host buffer, and the
+    query batch -- with or without the comm's float64 all-reduce (without it the liked path's
+    partial sums are all-gathered: R x B x d x 8 more per slot). Host arithmetic only. Also pins
+    the round-6 trim: the speculative screen's layout no longer carries the streaming select's
+    chunk lists (C5/8 27.8 -> 13.0 GiB per slot)."""
+    import ctypes
+    from robot_ebert_amd import _lib
+    lib = _lib.load()
+    R = 8
+    dt = {2: _lib.EBT_BF16 if name == "C4" else _lib.EBT_F16, 4: _lib.EBT_F32}[es]
+    n = -(-N // R)
+    shard = n * d * es
+    state = lib.ebt_catalog_state_bytes(1 << 20, dt, n, d, d)
+    assert state > 0
+    cat = _fake_catalog(n, d, dt)
+    cb = _lib.ALLGATHER_FN(lambda *a: 0)
+    ar = _lib.ALLREDUCE_F64_FN(lambda *a: 0) if all_reduce else _lib.ALLREDUCE_F64_FN()
+    comm = _lib.EbtComm(rank=0, world=R, n_global=N, all_gather=cb, all_reduce_f64=ar)
+    ws = lib.ebt_sharded_workspace_bytes(ctypes.byref(cat), ctypes.byref(comm), B, k, None)
+    assert ws > 0
+    slots = 3
+    outputs = slots * B * k * 16
+    queries = B * d * es
+    total = shard + state + slots * ws + outputs + queries
+    assert total <= 0.8 * 288e9, (name, total / 1e9)
+    if name == "C5":
+        assert ws < 14 * 2 ** 30, ws / 2 ** 30          # was 27.76 GiB per slot (round 5)
+        assert total < 70e9, total / 1e9

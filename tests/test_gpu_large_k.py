@@ -1,5 +1,5 @@
 """k beyond the screen's k' range (min(k, n) > 4096): the full-sort path (large_k.hip) --
-every score in float64, a stable descending radix sort, the first k -- against the float64
+every score in float64, a descending (score, row) merge sort cut at k, the first k -- against the float64
 oracle (oracle/restatement.py: lib.py:51-55 restated): rows bit-exact in (score desc, row asc)
 order, scores within 1e-12, NaN / -1 past the valid rows (k > n, exclusions), exact duplicate
 rows ordered by row, dense / liked queries, f32 / bf16 catalogs. The reference's pandas [:k]
@@ -61,3 +61,29 @@ def test_large_k_liked_bf16(cuda_device):
     s, r = ebt.score_topk(cat, k, liked=liked, exclude=excl)
     s_ref, r_ref = R.liked_topk(c64, liked, k, exclude=excl)
     _check(s.cpu().numpy(), r.cpu().numpy(), s_ref, r_ref)
+
+
+def test_large_k_many_runs_and_groups(cuda_device):
+    """The hand-written sort (round 6) past one LDS run and one query group: n = 70 000 rows are
+    35 sorted runs and 6 merge passes, the later ones cut at k; 70 queries are two groups of the
+    key budget's at most 64; many exact duplicates (tied scores across runs) ordered by row;
+    an all-excluded-but-few query leaves NaN / -1 slots."""
+    import robot_ebert_amd as ebt
+    n, d, B, k = 70_000, 16, 70, 4500
+    rng = np.random.default_rng(11)
+    c = rng.standard_normal((n, d))
+    src = rng.integers(0, n, size=3000)
+    dst = rng.integers(0, n, size=3000)
+    c[dst] = c[src]                                   # ties spread over every run
+    q = rng.standard_normal((B, d))
+    q[3] = c[src[0]]
+    excl = [sorted(rng.choice(n, 50, replace=False).tolist()) for _ in range(B)]
+    excl[7] = list(range(0, n - 1000))                # only 1000 candidates left
+    cat = ebt.Catalog(torch.tensor(c, dtype=torch.float32, device=cuda_device))
+    c32 = c.astype(np.float32).astype(np.float64)
+    q32 = q.astype(np.float32).astype(np.float64)
+    s, r = ebt.score_topk(cat, k, queries=torch.tensor(q32, dtype=torch.float32,
+                                                       device=cuda_device), exclude=excl)
+    s_ref, r_ref = R.cosine_topk(q32, c32, k, exclude=excl)
+    _check(s.cpu().numpy(), r.cpu().numpy(), s_ref, r_ref)
+    assert (r.cpu().numpy()[7] >= 0).sum() == 1000

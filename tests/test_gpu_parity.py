@@ -1072,6 +1072,77 @@ def test_sort_exclusions_entry(cuda_device):
                L.stream_of(cuda_device))
 
 
+def test_sort_exclusions_out_of_place_head_tail(cuda_device):
+    """out of place, with off[0] > 0, off[B] < nnz and a decreasing offset, the rows
+    outside every clamped segment are copied from rows_in (the sort's copy blocks), the
+    well-formed segments come out sorted, and rows_in is not modified. Also: segments beyond one
+    LDS run (4096 rows) out of place, sorted and already-sorted (copied)."""
+    ebt, L = _ebt()
+    rng = np.random.default_rng(39)
+    nnz = 30_000
+    flat = rng.integers(-1000, 1 << 40, size=nnz).astype(np.int64)
+    # segments: [100, 600) [600, 5000) [5000, 5000) [4000, 9000) (overlaps: off decreases)
+    # [9000, 9000) ... [9000, 20000) (long, sorted); tail [20000, 30000) untouched
+    flat[9000:20000] = np.sort(flat[9000:20000])
+    off = np.array([100, 600, 5000, 4000, 9000, 9000, 20000], dtype=np.int64)
+    B = len(off) - 1
+    er = torch.tensor(flat, device=cuda_device)
+    eo = torch.tensor(off, device=cuda_device)
+    out = torch.full_like(er, 7)
+    need = L.load().ebt_sort_exclusions_bytes(B, nnz)
+    ws = torch.empty(need, dtype=torch.uint8, device=cuda_device)
+    L.call("ebt_sort_exclusions", L.ptr(eo), L.ptr(er), L.ptr(out), B, nnz, L.ptr(ws), need,
+           L.stream_of(cuda_device))
+    got = out.cpu().numpy()
+    assert np.array_equal(er.cpu().numpy(), flat)           # the input is not modified
+    assert np.array_equal(got[:100], flat[:100])            # head
+    assert np.array_equal(got[20000:], flat[20000:])        # tail
+    assert np.array_equal(got[100:600], np.sort(flat[100:600]))
+    assert np.array_equal(got[9000:20000], flat[9000:20000])  # already sorted: copied
+    # a long unsorted segment out of place, then in place: both sorted, same result
+    off2 = np.array([5, 25_000], dtype=np.int64)
+    eo2 = torch.tensor(off2, device=cuda_device)
+    out2 = torch.full_like(er, 7)
+    need2 = L.load().ebt_sort_exclusions_bytes(1, nnz)
+    ws2 = torch.empty(need2, dtype=torch.uint8, device=cuda_device)
+    L.call("ebt_sort_exclusions", L.ptr(eo2), L.ptr(er), L.ptr(out2), 1, nnz, L.ptr(ws2), need2,
+           L.stream_of(cuda_device))
+    g2 = out2.cpu().numpy()
+    assert np.array_equal(g2[:5], flat[:5]) and np.array_equal(g2[25_000:], flat[25_000:])
+    assert np.array_equal(g2[5:25_000], np.sort(flat[5:25_000]))
+    er3 = er.clone()
+    L.call("ebt_sort_exclusions", L.ptr(eo2), L.ptr(er3), L.ptr(er3), 1, nnz, L.ptr(ws2), need2,
+           L.stream_of(cuda_device))
+    assert np.array_equal(er3.cpu().numpy(), g2)
+
+
+def test_unsorted_exclusions_rejected_by_the_rescore_check(cuda_device):
+    """Round 6: the C entry's exclusion-order check is folded into the rescore (certificate -3
+    for a query whose segment is not ascending): an unsorted device CSR handed straight to
+    ebt_cosine_topk fails with the same message; the same CSR sorted passes; a SortedCSR from
+    csr_sorted / csr_from_lists is used as it is."""
+    ebt, L = _ebt()
+    from robot_ebert_amd.search import SortedCSR, csr_from_lists, csr_sorted
+    n, d, B, k = 20_000, 64, 300, 10
+    cat = ebt.Catalog(torch.randn((n, d), generator=torch.Generator().manual_seed(1)).to(cuda_device))
+    q = torch.randn((B, d), generator=torch.Generator().manual_seed(2)).to(cuda_device)
+    lists = [[5, 3, 9]] * B
+    lists[17] = [1, 2, 3]
+    sc = csr_from_lists(lists, cuda_device)
+    assert isinstance(sc, SortedCSR)
+    assert csr_sorted(sc) is sc
+    s_ok, r_ok = ebt.score_topk(cat, k, queries=q, exclude=sc)
+    raw_off = torch.tensor(np.arange(B + 1) * 3, dtype=torch.int64, device=cuda_device)
+    raw_rows = torch.tensor(np.concatenate(lists), dtype=torch.int64, device=cuda_device)
+    # through the Python layer a plain tuple is sorted first (ebt_sort_exclusions)
+    s2, r2 = ebt.score_topk(cat, k, queries=q, exclude=(raw_off, raw_rows))
+    assert torch.equal(r2, r_ok)
+    # handed to the C entry unsorted: rejected by the rescore's check
+    bad = SortedCSR(raw_off, raw_rows)     # a false claim: the rescore still checks
+    with pytest.raises(L.EbertError, match="sorted ascending"):
+        ebt.score_topk(cat, k, queries=q, exclude=bad)
+
+
 @pytest.mark.parametrize("k", [20, 5999])
 def test_non_finite_catalog_rows_never_candidates(cuda_device, k):
     """include/ebert.h "Non-finite catalog rows": a row with a NaN or an inf element scores NaN

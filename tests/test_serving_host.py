@@ -306,3 +306,53 @@ def test_garbled_server_frame_fails_pending_callers(tmp_path):
     t.join(10)
     lst.close()
     assert decode_request(got["req"])[0] == 1
+
+
+def test_bad_request_fails_only_itself():
+    """a request is checked before it can share a batch. One client's liked row past
+    the catalog fails only that request (the library would reject the whole batch: a liked row
+    out of range is EBT_EINVAL for the call), while another client's request coalesced in the
+    same window is answered; a huge k is clamped to the catalog (same answer), rated rows outside
+    the catalog are ignored (lib.py:48's index.difference ignores unknown ids)."""
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((300, 8))
+
+    class Cat(_Cat):
+        n, n_global, row_offset = 300, 300, 0
+
+    calls = []
+    inner = _oracle_score(calls)
+
+    def strict(cat, k, liked, exclude):     # the library's own argument checks
+        if any(r < 0 or r >= cat.n for l in liked for r in l) or k > 100_000:
+            raise ValueError("the whole batch was rejected")
+        return inner(cat, k, liked, exclude)
+    b = RecBatcher(Cat(x), max_batch=64, max_wait_ms=200.0, score_fn=strict)
+    srv = ScoreServer(b)
+    ca, cb = ScoreClient(srv.address), ScoreClient(srv.address)
+    res = {}
+
+    def run(name, c, args):
+        try:
+            res[name] = c.score(*args)
+        except Exception as e:  # noqa: BLE001
+            res[name] = e
+    good = ([3, 7], [1, 2, 5000], (1 << 31) - 1)     # the wire's largest k
+    ts = [threading.Thread(target=run, args=("bad", ca, ([3, 300], [], 5))),
+          threading.Thread(target=run, args=("good", cb, good)),
+          threading.Thread(target=run, args=("neg", ca, ([-1], [], 5)))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(30)
+    assert isinstance(res["bad"], ValueError) and "not in the catalog" in str(res["bad"])
+    assert isinstance(res["neg"], ValueError)
+    ws, wr = _direct(x, [3, 7], [1, 2], 300)
+    s, r = res["good"]
+    np.testing.assert_array_equal(r, wr)
+    assert len(r) == 298
+    assert sum(calls) == 1
+    ca.close()
+    cb.close()
+    srv.close()
+    b.close()
