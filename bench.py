@@ -329,27 +329,53 @@ def device_f64_check(emb: torch.Tensor, q: torch.Tensor, s, r, nq: int, chunk: i
                       "restatement"}
 
 
-def host_boundary(cat, k, q, timer, steps=3):
-    """Untimed for `value`: the same step with the queries handed over in pinned host memory
-    and the results copied back (PCIe-inclusive; steps not overlapped)."""
+def host_boundary(cat, k, q, timer, steps=12):
+    """Untimed for `value`: the same step with the queries handed over in host memory and the
+    results copied back (PCIe-inclusive). Overlapped (robot_ebert_amd/hostio.py): batch i+1's
+    H2D and batch i's D2H run on a copy stream under batch i / i+1's kernels, batches submitted
+    before the previous one is finished, as the resident loop does; also the same steps one at
+    a time with the copies in line (`serial_ms_per_step`), the round-5 form."""
     import robot_ebert_amd as ebt
+    from robot_ebert_amd.hostio import HostStager, run_pipelined
     dev = q.device
     qh = q.cpu().pin_memory()
     timer.only()
-    outs = None
+    stager = HostStager(dev)
+
+    def submit(qd):
+        return ebt.score_topk_submit(cat, k, queries=qd, timer=timer)
+
+    def finish(p):
+        return ebt.score_topk_finish(p)
+
+    def overlapped(n):
+        outs = None
+        for h in run_pipelined(stager, [qh] * n, submit, finish):
+            outs = h
+        return outs.result()
+
+    overlapped(2)                                   # warm the pinned pools and the copy stream
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        qd = qh.to(dev, non_blocking=True)
-        s, r = ebt.score_topk_finish(ebt.score_topk_submit(cat, k, queries=qd, timer=timer))
-        outs = (s.to("cpu", non_blocking=True), r.to("cpu", non_blocking=True))
-        torch.cuda.synchronize(dev)
+    outs = overlapped(steps)
+    torch.cuda.synchronize(dev)
     el = (time.perf_counter() - t0) / steps
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    for _ in range(3):
+        qd = qh.to(dev, non_blocking=True)
+        s, r = finish(submit(qd))
+        (s.to("cpu", non_blocking=True), r.to("cpu", non_blocking=True))
+        torch.cuda.synchronize(dev)
+    el_serial = (time.perf_counter() - t1) / 3
     return {"ms_per_step": round(1e3 * el, 3), "queries_per_s": round(q.shape[0] / el, 1),
+            "serial_ms_per_step": round(1e3 * el_serial, 3),
             "h2d_bytes": qh.numel() * qh.element_size(),
-            "d2h_bytes": sum(t.numel() * t.element_size() for t in outs), "steps": steps,
-            "note": "queries from pinned host memory, results back to host memory, "
-                    "one step at a time (no overlap); never `value`"}
+            "d2h_bytes": sum(int(a.nbytes) for a in outs), "steps": steps,
+            "note": "queries from pinned host memory, results back to host memory; H2D of the "
+                    "next batch and D2H of the previous one on a copy stream under the current "
+                    "batch's kernels (hostio.run_pipelined); serial_ms_per_step: one step at a "
+                    "time, copies in line; never `value`"}
 
 
 def stage_breakdown(st: dict, ms_per_step: float, world: int) -> dict:

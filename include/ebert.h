@@ -391,7 +391,14 @@ int ebt_catalog_init(ebt_catalog* cat, const void* data, int dtype, int64_t n, i
 /* Optional knobs (NULL = defaults; a zero field = its default): kprime = the screen's candidate
  * count k' (default: k + slack for the image's error band), chunk_rows = catalog rows per
  * materialised score chunk of the unfused path (default: 4 GiB of f32 scores),
- * flags = EBT_FLAG_NO_FUSE to disable the fused screen. Results do not depend on them. */
+ * flags = EBT_FLAG_NO_FUSE to disable the fused screen. Results do not depend on them.
+ * flags |= EBT_FLAG_LIKED_CHECKED (0.3.2, ebt_cosine_topk / _submit only): the caller has
+ * checked its liked CSR on the host -- every user has >= 1 liked row and every row lies in the
+ * catalog's [row_offset, row_offset + n) -- so _submit does not read the CSR back (no stream
+ * synchronisation: the liked path enqueues asynchronously, as the dense one; the 1/L scales
+ * are taken from the offsets on the device, the same float64 values). An unchecked CSR with
+ * this flag is undefined behaviour (rows out of range are read). */
+#define EBT_FLAG_LIKED_CHECKED 8
 typedef struct ebt_options {
   int32_t kprime;
   int32_t flags;

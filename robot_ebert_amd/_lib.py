@@ -24,6 +24,7 @@ STAGES = {"gemm": 0, "mask": 1, "select": 2, "merge_select": 3, "rescore": 4, "g
 EBT_FLAG_NO_FUSE = 1
 EBT_FLAG_EXACT = 2
 EBT_FLAG_THETA = 4
+EBT_FLAG_LIKED_CHECKED = 8   # ebert.h: the liked CSR was checked on the host (no read-back)
 EBT_FILTER_SLOTS_MAX = 128
 
 

@@ -66,13 +66,25 @@ def k_class(k: int) -> int:
 class RecBatcher:
     def __init__(self, catalog, max_batch: int = 4096, max_wait_ms: float = 2.0,
                  score_fn: Optional[Callable] = None, history: int = 1024,
-                 max_inflight: int = 2) -> None:
+                 max_inflight: int = 2, stager="auto", submit_fn: Optional[Callable] = None,
+                 finish_fn: Optional[Callable] = None) -> None:
         """catalog: the ``Catalog`` every request scores against. score_fn(catalog, k, liked=,
         exclude=) -> (scores [B, k], rows [B, k]); default: ``search.score_topk_submit`` /
-        ``score_topk_finish`` with up to ``max_inflight`` batches on the GPU."""
+        ``score_topk_finish`` (or submit_fn / finish_fn) with up to ``max_inflight`` batches on
+        the GPU. stager: the host boundary's copy stream (hostio.HostStager; "auto" = one on the
+        catalog's GPU, None = copies in line): a batch's liked / rated CSR goes to the device
+        under the previous batch's kernels and its results come back under the next one's."""
         if max_batch < 1:
             raise ValueError("max_batch must be >= 1")
         self.catalog = catalog
+        self._submit_fn, self._finish_fn = submit_fn, finish_fn
+        if stager == "auto":
+            dev = getattr(catalog, "device", None)
+            stager = None
+            if score_fn is None and dev is not None and getattr(dev, "type", None) == "cuda":
+                from .hostio import HostStager
+                stager = HostStager(dev)
+        self.stager = stager
         self.max_batch = int(max_batch)
         self.max_wait = float(max_wait_ms) / 1e3
         self._score = score_fn
@@ -225,29 +237,51 @@ class RecBatcher:
                 return
             self._deliver(reqs, scores, rows)
             return
-        from .search import score_topk_submit
+        submit = self._submit_fn
+        if submit is None:
+            from .search import score_topk_submit as submit
         self._slots.acquire()            # released by the completion thread
         try:
-            p = score_topk_submit(self.catalog, k_max, liked=liked, exclude=excl)
+            ev = None
+            if self.stager is not None:
+                # the batch's CSRs through the copy stream (pinned staging), then its kernels;
+                # an event right after them for its results' D2H
+                from .search import csr_from_lists
+                dev = self.catalog.device
+                liked = csr_from_lists(liked, dev, self.stager)
+                excl = csr_from_lists(excl, dev, self.stager)
+                p = submit(self.catalog, k_max, liked=liked, exclude=excl)
+                ev = self.stager.record()
+            else:
+                p = submit(self.catalog, k_max, liked=liked, exclude=excl)
         except BaseException as e:
             self._slots.release()
             for r in reqs:
                 _answer(r[3], exc=e)
             return
-        self._done.put((p, reqs))
+        self._done.put((p, reqs, ev))
 
     def _complete(self) -> None:
         """Completion thread: finish the submitted batches in order and answer their callers."""
-        from .search import score_topk_finish
+        finish = self._finish_fn
+        if finish is None:
+            from .search import score_topk_finish as finish
+        from .hostio import retried
         self._bind_device()
         while True:
             item = self._done.get()
             if item is _SENTINEL:
                 return
-            p, reqs = item
+            p, reqs, ev = item
             try:   # the slot is released whatever happens to this batch's callers
                 try:
-                    scores, rows = score_topk_finish(p)
+                    scores, rows = finish(p)
+                    if self.stager is not None:
+                        # D2H on the copy stream after this batch's kernels only (a fresh event
+                        # when its retries ran behind later batches), under the next batch
+                        if retried(p):
+                            ev = self.stager.record()
+                        scores, rows = self.stager.to_host((scores, rows), ev).result()
                 except BaseException as e:  # noqa: BLE001
                     for r in reqs:
                         _answer(r[3], exc=e)

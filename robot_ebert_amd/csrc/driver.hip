@@ -120,7 +120,8 @@ struct DriverLayout {
 bool driver_layout(const ebt_catalog& c, int64_t B, int32_t k, const ebt_options& opt,
                    DriverLayout* L) {
   if (B < 1 || k < 1 || c.n < 1 || opt.kprime < 0 || opt.chunk_rows < 0 ||
-      (opt.chunk_rows && opt.chunk_rows % 128) || (opt.flags & ~EBT_FLAG_NO_FUSE))
+      (opt.chunk_rows && opt.chunk_rows % 128) ||
+      (opt.flags & ~(EBT_FLAG_NO_FUSE | EBT_FLAG_LIKED_CHECKED)))
     return false;
   DriverLayout& D = *L;
   D = DriverLayout{};
@@ -131,7 +132,7 @@ bool driver_layout(const ebt_catalog& c, int64_t B, int32_t k, const ebt_options
     const size_t big = large_topk_bytes(B, c.n, nullptr);
     if (big == 0) return false;
     D.large = true;
-    D.flags = opt.flags;
+    D.flags = opt.flags & EBT_FLAG_NO_FUSE;  // (LIKED_CHECKED: the submit's, not the screen's)
     D.prep = prep_layout(c, B);
     size_t o = 0;
     D.off_prep = o;
@@ -151,7 +152,7 @@ bool driver_layout(const ebt_catalog& c, int64_t B, int32_t k, const ebt_options
     kp = kp < KPRIME_MAX ? kp : KPRIME_MAX;
     D.kprime = (int32_t)(kp > lo ? kp : lo);
   }
-  D.flags = opt.flags;
+  D.flags = opt.flags & EBT_FLAG_NO_FUSE;  // (LIKED_CHECKED: the submit's, not the screen's)
   D.chunk = opt.chunk_rows ? opt.chunk_rows : chunk_rows(c, D.B_pad, SCORE_BUDGET);
   D.R = B < RETRY_GROUP ? B : RETRY_GROUP;
   const int64_t R_pad = pad_batch(D.R);
@@ -279,10 +280,38 @@ int prep_dense(const ebt_catalog& c, const void* q, int q_dtype, int64_t B, int6
                          native_q ? ldq : 0, native_q, c.u_cat, qimg, c.ld_img, qscale, eps, st);
 }
 
-// liked path: validated on the host (counts >= 1 with sklearn's message, rows in the catalog)
+// q64[b] *= 1 / (off[b+1] - off[b]): the 1/L of lib.py:52 from the liked CSR's offsets (the
+// same float64 scale the host computes, then the same product as scale_rows_kernel)
+__global__ void scale_by_count_kernel(double* __restrict__ q64, int64_t total, int d,
+                                      const int64_t* __restrict__ off) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = t / d;
+    const double s = 1.0 / (double)(off[b + 1] - off[b]);
+    q64[t] *= s;
+  }
+}
+
+// liked path: validated on the host (counts >= 1 with sklearn's message, rows in the catalog),
+// unless the caller did (EBT_FLAG_LIKED_CHECKED): then nothing is read back
 int prep_liked(const ebt_catalog& c, const int64_t* off, const int64_t* rows, int64_t B,
                const PrepLayout& P, char* base, char* scratch, size_t scratch_bytes,
-               hipStream_t st) {
+               hipStream_t st, bool checked) {
+  if (checked) {
+    double* q64 = (double*)(base + P.q64);
+    int rc = query_liked_sum(c.data, c.dtype, c.d, c.ld, c.gnorm64, B, off, rows, q64, st,
+                             c.row_offset, 0);
+    if (rc) return rc;
+    int64_t blocks = ceil_div(B * c.d, 256);
+    blocks = blocks > 8192 ? 8192 : blocks;
+    hipLaunchKernelGGL(scale_by_count_kernel, dim3((unsigned)blocks), dim3(256), 0, st, q64,
+                       B * c.d, c.d, off);
+    rc = launch_check("scale_by_count_kernel");
+    if (rc) return rc;
+    return ebt_query_image(q64, B, pad_batch(B), c.d, c.img_dtype, nullptr, 0, 0, c.u_cat,
+                           base + P.qimg, c.ld_img, (float*)(base + P.qscale),
+                           (float*)(base + P.eps), st);
+  }
   std::vector<int64_t> h_off(B + 1);
   int rc = hip_check(hipMemcpyAsync(h_off.data(), off, (B + 1) * 8, hipMemcpyDeviceToHost, st),
                      "hipMemcpyAsync");
@@ -491,7 +520,8 @@ int ebt_cosine_topk_submit(const ebt_catalog* cat, const void* q, int q_dtype, i
   int rc = q ? prep_dense(*cat, q, q_dtype, B, ldq, L.prep, prep, st)
              : prep_liked(*cat, liked_off, liked_rows, B, L.prep, prep,
                           ws + (L.large ? L.off_big : L.off_pass),
-                          L.large ? L.big_bytes : L.pass_bytes, st);
+                          L.large ? L.big_bytes : L.pass_bytes, st,
+                          (o.flags & EBT_FLAG_LIKED_CHECKED) != 0);
   if (rc) return rc;
   int32_t* cert = (int32_t*)(ws + L.off_cert);
   if (L.large) {  // exact: every certificate is 1, the results are final

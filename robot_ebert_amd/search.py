@@ -77,11 +77,26 @@ class SortedCSR(tuple):
     call. (The rescore checks each segment's order anyway, folded into the kernel that writes the
     certificates: an unsorted segment fails the call, it is never silently misread.)"""
 
-    def __new__(cls, off: torch.Tensor, rows: torch.Tensor):
-        return super().__new__(cls, (off, rows))
+    # host facts of a CSR built from host lists (None when unknown): the shortest segment and
+    # the row range, so that a liked CSR can be passed with EBT_FLAG_LIKED_CHECKED
+    min_len = None
+    row_min = None
+    row_max = None
+
+    def __new__(cls, off: torch.Tensor, rows: torch.Tensor, min_len=None, row_min=None,
+                row_max=None):
+        t = super().__new__(cls, (off, rows))
+        t.min_len, t.row_min, t.row_max = min_len, row_min, row_max
+        return t
+
+    def checked_for(self, lo: int, hi: int) -> bool:
+        """Every segment non-empty and every row in [lo, hi) (known from the host build)."""
+        return (self.min_len is not None and self.min_len >= 1 and self.row_min is not None
+                and self.row_min >= lo and self.row_max < hi)
 
 
-def csr_from_lists(lists: Sequence[Sequence[int]], device) -> Tuple[torch.Tensor, torch.Tensor]:
+def csr_from_lists(lists: Sequence[Sequence[int]], device,
+                   stager=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Host lists of row ids -> device CSR (offsets int64 [B+1], rows int64 [nnz]), each segment
     sorted (ebt_cosine_topk_prepared binary-searches them). numpy builds it (a batch of a few
     thousand users' lists costs the interpreter ~1 ms as Python loops, on the serving path's
@@ -96,8 +111,14 @@ def csr_from_lists(lists: Sequence[Sequence[int]], device) -> Tuple[torch.Tensor
         np.concatenate(segs, out=both[B + 1:])
     else:
         both[B + 1] = 0
-    t = torch.from_numpy(both).to(device)
-    return SortedCSR(t[:B + 1], t[B + 1:])
+    # (with a hostio.HostStager the copy runs on its copy stream from pinned memory, under the
+    # kernels of the batch before; the compute stream waits for it)
+    t = stager.to_device(both) if stager is not None else torch.from_numpy(both).to(device)
+    nnz = int(lens.sum())
+    rows = both[B + 1:B + 1 + nnz]
+    return SortedCSR(t[:B + 1], t[B + 1:], min_len=int(lens.min()) if B else 0,
+                     row_min=int(rows.min()) if nnz else None,
+                     row_max=int(rows.max()) if nnz else None)
 
 
 def csr_sorted(off, rows: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -462,7 +483,7 @@ def _submit_c(catalog: Catalog, k: int, queries, liked, exclude, kprime, chunk_r
     if exclude is not None:
         exclude = (csr_from_lists(exclude, dev) if not isinstance(exclude, tuple)
                    else exclude if isinstance(exclude, SortedCSR) else csr_sorted(*exclude))
-    q_ptr, q_dt, ldq, lo, lr = None, 0, 0, None, None
+    q_ptr, q_dt, ldq, lo, lr, lo_csr = None, 0, 0, None, None, None
     if queries is not None:
         require_cuda(queries, "queries")
         if queries.dim() != 2 or queries.shape[1] != catalog.d:
@@ -474,12 +495,17 @@ def _submit_c(catalog: Catalog, k: int, queries, liked, exclude, kprime, chunk_r
         B = int(queries.shape[0])
         q_ptr, q_dt, ldq = ptr(queries), DTYPE_CODE[queries.dtype], int(queries.stride(0))
     else:
-        lo, lr = liked if isinstance(liked, tuple) else csr_from_lists(liked, dev)
+        lo_csr = liked if isinstance(liked, tuple) else csr_from_lists(liked, dev)
+        lo, lr = lo_csr
         B = int(lo.numel()) - 1
     if B < 1:
         raise EbertError("empty query batch")
-    opt = _lib.EbtOptions(kprime=int(kprime or 0), flags=0 if fuse else _lib.EBT_FLAG_NO_FUSE,
-                          chunk_rows=int(chunk_rows or 0))
+    flags = 0 if fuse else _lib.EBT_FLAG_NO_FUSE
+    if liked is not None and isinstance(lo_csr, SortedCSR) and lo_csr.checked_for(
+            catalog.row_offset, catalog.row_offset + catalog.n):
+        # checked on the host while building it: the C entry reads nothing back (no stream sync)
+        flags |= _lib.EBT_FLAG_LIKED_CHECKED
+    opt = _lib.EbtOptions(kprime=int(kprime or 0), flags=flags, chunk_rows=int(chunk_rows or 0))
     lib = _lib.load()
     need = lib.ebt_workspace_bytes(ctypes.byref(catalog.cstruct), B, k, ctypes.byref(opt))
     if need == 0:
