@@ -251,9 +251,11 @@ int ebt_merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t
  * best exact score over the WHOLE catalog -- cannot enter the global top k. ebt_shard_pack keeps
  * of each sorted list (scores/rows [B][k], row < 0 = padding; t_floor NULL = keep every real
  * entry) the prefix with score >= t_floor[b] and packs it into `send`
- * (ebt_shard_pack_bytes(B, cap) bytes, device): u32 starts[B + 1] (query b's entries are
- * [starts[b], starts[b + 1])) and block totals, then f64 scores[cap], then i32 GLOBAL rows[cap].
- * Entries at positions >= cap are counted but not sent. After an all-gather of the R buffers
+ * (ebt_shard_pack_bytes(B, cap) bytes, device): u32 start[B], u32 len[B] (query b's entries are
+ * [start[b], start[b] + len[b]); 0.3.2 -- ebt_shard_pack writes the starts in query order, the
+ * sharded C entry's rescore reserves each query's range by an atomic, so any order is valid)
+ * and block totals, then f64 scores[cap], then i32 GLOBAL rows[cap]. Entries at positions
+ * >= cap are counted but not sent. After an all-gather of the R buffers
  * (recv, R * ebt_shard_pack_bytes bytes, rank order), ebt_merge_packed writes the same global
  * top-k as ebt_merge_topk over the full lists, and sets *incomplete (device int32; set to 1,
  * never cleared) when some rank's entries did not all fit its cap: the caller must then merge

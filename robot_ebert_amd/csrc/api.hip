@@ -124,7 +124,8 @@ int rescore(const double*, int64_t, int32_t, const void*, int, int64_t, const do
             const float*, const int64_t*, int32_t, int32_t, int64_t, const float*, const double*,
             double*, int64_t*, int32_t*, hipStream_t, const int*, int, unsigned long long*,
             int64_t list_base = 0, const float* theta = nullptr,
-            const int64_t* excl_off = nullptr, const int64_t* excl_rows = nullptr);
+            const int64_t* excl_off = nullptr, const int64_t* excl_rows = nullptr,
+            const ShardPackOut* pack = nullptr);
 int screen_gemm_filter(const void*, int64_t, const void*, int64_t, int32_t, int32_t, int,
                        const float*, const float*, const float*, uint64_t*, int64_t, int,
                        uint8_t*, int64_t, int*, int64_t, hipStream_t);
@@ -160,7 +161,8 @@ int64_t merge_block_max_groups(int);
 int merge_segment_wave(float*, int64_t*, int64_t, int, int, const uint64_t*, int64_t, int,
                        const uint8_t*, int64_t, int64_t, int64_t, const int64_t*, const int64_t*,
                        int*, hipStream_t, const float* veps = nullptr,
-                       const float* vspec = nullptr);
+                       const float* vspec = nullptr, float* fout = nullptr, int fw = 0,
+                       const float* feps = nullptr);
 int pilot_topk(const float*, int64_t, int64_t, int, int64_t, int, int, float*, int64_t*,
                hipStream_t);
 constexpr int64_t PILOT_ROWS = 1024;  // = WMERGE_H (select_topk.hip)
@@ -632,11 +634,11 @@ int rescore_sharded(const double* q64, int64_t B, int32_t d, const void* cat, in
                     const float* eps, const double* t_floor, double* out_s, int64_t* out_r,
                     int32_t* certified, const int* ovf, const float* theta, void* timer,
                     hipStream_t st, int64_t list_base, const int64_t* excl_off,
-                    const int64_t* excl_rows) {
+                    const int64_t* excl_rows, const ShardPackOut* pack) {
   StageScope sc(timer, EBT_STAGE_RESCORE, st);
   return rescore(q64, B, d, cat, dtype, ld, gnorm64, row_offset, cand_vals, cand_rows,
                  kprime, k, n_rows, eps, t_floor, out_s, out_r, certified, st, ovf, 0,
-                 timer_rows(timer, st), list_base, theta, excl_off, excl_rows);
+                 timer_rows(timer, st), list_base, theta, excl_off, excl_rows, pack);
 }
 
 }  // namespace ebt
@@ -869,6 +871,10 @@ struct PipeArgs {
   const float* gsamp = nullptr;
   int64_t gs_rstride = 0;
   int gs_G = 0, gs_gj = 0, gs_j = 0;
+  // screen_at_local: the row-sharded step's floor entries ([B][floor_w + 1], ebt_floor_pack's
+  // layout) written by the screen's last wave merge
+  float* floor_out = nullptr;
+  int floor_w = 0;
 };
 
 static int check_pipe(const PipeArgs& a, const char* who) {
@@ -1060,10 +1066,12 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
     const int64_t groups = g0 + ceil_div(seg, L.group_rows);
     {
       StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
+      const bool last = r0 + seg == n_rows;
       if (wave)
         rc = merge_segment_wave(fv, fi, B, kprime, k, cand, L.ld_cand, slots, counts,
                                 L.ld_counts, groups, a.row_offset, a.excl_off, a.excl_rows, ovf,
-                                st, fuse_verify ? a.eps : nullptr, fuse_verify ? tspec : nullptr);
+                                st, fuse_verify ? a.eps : nullptr, fuse_verify ? tspec : nullptr,
+                                last ? a.floor_out : nullptr, a.floor_w, a.eps);
       else  // sorted lists (the block merge sorts the union)
         rc = merge_segment(fv, fi, B, kprime, cand, L.ld_cand, slots, counts, L.ld_counts,
                            groups, a.row_offset, a.excl_off, a.excl_rows, ovf, st,
@@ -1335,7 +1343,8 @@ int screen_at_local(const double* q64, const void* qimg, const float* qscale, co
                     int64_t* list_rows, const float* gsamp, int64_t gs_rstride, int gs_G,
                     int gs_gj, int gs_j, double hits, int64_t lead, const float* lead_scores,
                     int64_t ld_lead, const float** theta_dev, const int** ovf_dev,
-                    const float** eps_dev, void* timer, hipStream_t st) {
+                    const float** eps_dev, void* timer, hipStream_t st, float* floor_out,
+                    int floor_w) {
   const int flags = EBT_FLAG_THETA;
   PipeArgs a{q64, qimg, qscale, eps, B, B_pad, cat, dtype, ld, gnorm64, cimg, cscale,
              img_dtype, ld_img, n_rows, d, d_pad, row_offset, excl_off, excl_rows, k, kprime,
@@ -1349,10 +1358,13 @@ int screen_at_local(const double* q64, const void* qimg, const float* qscale, co
   a.gs_G = gs_G;
   a.gs_gj = gs_gj;
   a.gs_j = gs_j;
+  a.floor_out = floor_out;
+  a.floor_w = floor_w;
   int rc = check_pipe(a, "screen_at_local");
   if (rc) return rc;
   if (!workspace || !list_vals || !list_rows || !gsamp || !theta_dev || !ovf_dev || !eps_dev ||
       !merge_wave_fits(kprime) || !(hits >= 0.0) || lead < 0 || gs_G < 1 || gs_G > 2048 ||
+      (floor_out && (floor_w < 1 || floor_w > k)) ||
       gs_gj < 1 || gs_G % gs_gj != 0 || gs_rstride < B * (int64_t)gs_gj || gs_j < 1 ||
       (lead > 0 && (!lead_scores || ld_lead < 256 * lead || 256 * lead >= n_rows))) {
     set_error("screen_at_local: bad arguments (kprime=%d, lead=%lld, G=%d, gj=%d, j=%d)", kprime,

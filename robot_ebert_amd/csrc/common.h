@@ -242,11 +242,21 @@ __device__ __forceinline__ double guard_norm(double nrm) {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// ebt_shard_pack's buffer: u32 starts[B + 1], u32 block totals[ceil(B / SHARD_PACK_QPB)] (scratch of the
+// ebt_shard_pack's buffer (0.3.2): u32 start[B], u32 len[B] (query b's entries are
+// [start[b], start[b] + len[b]) -- in any order of b: the sharded rescore reserves each query's
+// range by an atomic), u32 block totals[ceil(B / SHARD_PACK_QPB)] (scratch of the two-launch
 // pack, sent along), 16-byte aligned; then f64 scores[cap]; then i32 rows[cap]
 constexpr int SHARD_PACK_QPB = 64;  // queries per pack workgroup (one wave counts them)
 __host__ __device__ inline int64_t shard_pack_hdr_bytes(int64_t B) {
-  return ((B + 1 + (B + SHARD_PACK_QPB - 1) / SHARD_PACK_QPB) * 4 + 15) & ~(int64_t)15;
+  return ((2 * B + (B + SHARD_PACK_QPB - 1) / SHARD_PACK_QPB) * 4 + 15) & ~(int64_t)15;
 }
+
+// The sharded rescore's share of the pack (rescore_sharded): each query's workgroup counts its
+// entries >= t_floor from the exact scores it holds in LDS and writes len[b] into the send
+// buffer's header; one launch (shard_pack_lens) then places and copies them -- ebt_shard_pack's
+// counting launch folded into the rescore
+struct ShardPackOut {
+  uint32_t* len;       // NULL: no count
+};
 
 }  // namespace ebt

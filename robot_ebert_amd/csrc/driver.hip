@@ -32,13 +32,18 @@ int rescore_sharded(const double*, int64_t, int32_t, const void*, int, int64_t, 
                     int64_t, const float*, const int64_t*, int32_t, int32_t, int64_t, const float*,
                     const double*, double*, int64_t*, int32_t*, const int*, const float*, void*,
                     hipStream_t, int64_t list_base, const int64_t* excl_off,
-                    const int64_t* excl_rows);
+                    const int64_t* excl_rows, const ShardPackOut* pack);
+int union_floor(const float* gathered, int32_t R, int64_t B, int32_t ld, int32_t k,
+                double* t_floor, hipStream_t stream, uint32_t* zero2);
+int shard_pack_lens(const double* scores, const int64_t* rows, int64_t B, int32_t k,
+                    int64_t cap, void* send, hipStream_t st);
 int screen_at_local(const double*, const void*, const float*, const float*, int64_t, int64_t,
                     const void*, int, int64_t, const double*, const void*, const float*, int,
                     int32_t, int64_t, int32_t, int32_t, int64_t, const int64_t*, const int64_t*,
                     int32_t, int32_t, int64_t, void*, size_t, float*, int64_t*, const float*,
                     int64_t, int, int, int, double, int64_t, const float*, int64_t, const float**,
-                    const int**, const float**, void*, hipStream_t);
+                    const int**, const float**, void*, hipStream_t, float* floor_out,
+                    int floor_w);
 int pool_kth(const float*, int64_t, int64_t, int64_t, int, int, float*, hipStream_t, float*,
              int64_t*, int, int*, const float*, int64_t, int, uint64_t*, int64_t, int, uint8_t*,
              int64_t, int, int64_t);
@@ -929,8 +934,8 @@ bool shard_layout(const ebt_catalog& c, const ebt_comm& cm, int64_t B, int32_t k
   o = al(o + L.pack_bytes);
   L.off_precv = o;
   o = al(o + (size_t)R * L.pack_bytes);
-  L.off_incomplete = o;
-  o = al(o + 4);
+  L.off_incomplete = o;   // int32 "incomplete" flag, then the rescore's pack counter (u32)
+  o = al(o + 8);
   L.bytes = o;
   return true;
 }
@@ -1157,7 +1162,10 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
   const int* ovf_p = ovf;
   const float* eps_p = eps;
   // (the j-th of every rank's maxima, read in the gathered [R][B][J + 1] layout, is taken by
-  // the launch that starts the list and takes the lead's hits: one launch for both)
+  // the launch that starts the list and takes the lead's hits: one launch for both; and at the
+  // shared threshold the screen's last wave merge also writes this shard's floor entries,
+  // step 4's send buffer: no ebt_floor_pack launch)
+  float* fsend = (float*)(ws + S.off_fsend);
   if (use_theta)
     rc = screen_at_local(q64, qimg, qscale, qeps, B, L.B_pad, c.data, c.dtype, c.ld, c.gnorm64,
                          c.image, c.cscale, c.img_dtype, c.ld_img, c.n, c.d, c.d_pad,
@@ -1165,7 +1173,7 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
                          ws + S.off_spass, S.screen_bytes, lv, lr, recv_s, B * S.GJ,
                          (int)(R * S.GJ), (int)S.GJ, j_s, hits, S.lead,
                          (const float*)(ws + S.off_lead), S.ld_lead, &theta, &ovf_p, &eps_p,
-                         timer, st);
+                         timer, st, fsend, (int)S.fw);
   else
     rc = ebt_cosine_screen(q64, qimg, qscale, qeps, B, L.B_pad, c.data, c.dtype, c.ld, c.gnorm64,
                            c.image, c.cscale, c.img_dtype, c.ld_img, c.n, c.d, c.d_pad,
@@ -1174,16 +1182,20 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
                            st);
   if (rc) return rc;
   // 4. the catalog-wide floor: the k-th largest (approx - eps) over every shard's fw best
-  float* fsend = (float*)(ws + S.off_fsend);
   float* frecv = (float*)(ws + S.off_frecv);
   double* tfloor = (double*)(ws + S.off_tfloor);
-  if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
-  rc = ebt_floor_pack(lv, L.kprime, B, L.k_eff, (int32_t)S.fw, eps_p, fsend, st);
-  if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
+  if (!use_theta) {
+    if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
+    rc = ebt_floor_pack(lv, L.kprime, B, L.k_eff, (int32_t)S.fw, eps_p, fsend, st);
+    if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
+  }
   if (!rc) rc = sh_gather(cm, fsend, frecv, (size_t)B * (S.fw + 1) * 4, timer, st);
   if (rc) return rc;
+  // (the floor's launch also zeroes the merge's "incomplete" flag and the pack counter that
+  // the rescore and the finish use: no memset launch)
+  uint32_t* zero2 = (uint32_t*)(ws + S.off_incomplete);
   if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
-  rc = ebt_union_floor(frecv, R, B, (int32_t)S.fw + 1, k, tfloor, st);
+  rc = union_floor(frecv, R, B, (int32_t)S.fw + 1, k, tfloor, st, zero2);
   if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
   if (rc) return rc;
   // 5. the rescore of the rows that can enter the global top k, the certificate
@@ -1195,11 +1207,14 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
   int32_t* cert = (int32_t*)(ws + L.off_cert);
   // (the list's rows read as they are: local at the shared threshold, global otherwise; the
   // certificate with ebt_certify_cut's tests)
-  // (the rescore also checks the exclusion segments' order: certificate -3)
+  // (the rescore also checks the exclusion segments' order -- certificate -3 -- and packs the
+  // shard's entries above the floor for the results exchange: ebt_shard_pack's two launches
+  // folded in; the finish packs again only for a batch whose retries changed lists)
+  const ShardPackOut pack{S.cap && !padded ? (uint32_t*)(ws + S.off_psend) + B : nullptr};
   rc = rescore_sharded(q64, B, c.d, c.data, c.dtype, c.ld, c.gnorm64, c.row_offset, lv, lr,
                        L.kprime, L.k_eff, c.n, eps_p, tfloor, rs, rr, cert, ovf_p,
                        use_theta ? theta : nullptr, timer, st, use_theta ? 0 : c.row_offset,
-                       excl_off, excl_rows);
+                       excl_off, excl_rows, &pack);
   if (rc) return rc;
   // the certificates to the caller's host buffer; one event for them
   rc = hip_check(hipMemcpyAsync(host, cert, (size_t)B * 4, hipMemcpyDeviceToHost, st),
@@ -1266,13 +1281,21 @@ int ebt_cosine_topk_sharded_finish(ebt_sharded_pending* p) {
   void* timer = lp.timer;
   p->host[B + 1] = 0;
   if (S.cap) {
-    // 6. every shard's entries above the floor, packed (int32 rows), ONE all-gather, the merge
+    // 6. every shard's entries above the floor, packed (int32 rows), ONE all-gather, the merge.
+    // The rescore counted them already (len[b] in the header; the "incomplete" flag was zeroed
+    // in the submit): one launch places and copies them. Counted again (ebt_shard_pack) only when
+    // retries rewrote some query's list (its first-pass certificate was not 1) or the list was
+    // padded to k in the finish
     int32_t* incomplete = (int32_t*)(ws + S.off_incomplete);
-    rc = hip_check(hipMemsetAsync(incomplete, 0, 4, st), "hipMemsetAsync");
+    bool repack = lp.k_eff < k;
+    for (int64_t b = 0; b < B && !repack; ++b) repack = lp.cert_host[b] != 1;
     if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SMALL, st);
-    if (!rc)
-      rc = ebt_shard_pack((const double*)(ws + S.off_ls), (const int64_t*)(ws + S.off_lrr), B, k,
-                          (const double*)(ws + S.off_tfloor), S.cap, ws + S.off_psend, st);
+    rc = repack ? ebt_shard_pack((const double*)(ws + S.off_ls), (const int64_t*)(ws + S.off_lrr),
+                                 B, k, (const double*)(ws + S.off_tfloor), S.cap,
+                                 ws + S.off_psend, st)
+                : shard_pack_lens((const double*)(ws + S.off_ls),
+                                  (const int64_t*)(ws + S.off_lrr), B, k, S.cap,
+                                  ws + S.off_psend, st);
     if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SMALL, st);
     if (!rc) rc = sh_gather(p->comm, ws + S.off_psend, ws + S.off_precv, S.pack_bytes, timer, st);
     if (rc) return rc;

@@ -157,14 +157,14 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     int64_t* __restrict__ out_r, int32_t* __restrict__ certified, const int* __restrict__ ovf_cnt,
     int ovf_cap, unsigned long long* __restrict__ gathered, int64_t list_base,
     const float* __restrict__ theta, const int64_t* __restrict__ excl_off,
-    const int64_t* __restrict__ excl_rows) {
+    const int64_t* __restrict__ excl_rows, const ShardPackOut pack) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* qs = (double*)smem;                           // d (NU = 0 only)
   double* sc = qs + (NU > 0 ? 0 : ((d + 1) & ~1));      // kpp: approx, then exact
   int64_t* rw = (int64_t*)(sc + kpp);         // kpp
   int* pl = (int*)(rw + kpp);                 // kpp: list position of each kept row
   int* ix = pl + kpp;                         // kpp (NU > 0): the rows of the current pass
-  __shared__ int nvalid, corrupt, nkeep, ntop, nsel, ngath, xbad;
+  __shared__ int nvalid, corrupt, nkeep, ntop, nsel, ngath, xbad, npk;
   __shared__ unsigned long long smin_key;
   constexpr int NW = RTHREADS / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -181,6 +181,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     nsel = 0;
     ngath = 0;
     xbad = 0;
+    npk = 0;
     smin_key = ~0ull;
   }
   constexpr int ES = (DT == EBT_F64) ? 8 : (DT == EBT_F32 ? 4 : 2);
@@ -435,6 +436,19 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     exact_pass(false, cut2);
   }
   RST(4);
+  if (pack.len) {
+    // the sharded step's pack count: the entries of this query's top k with score >= t_floor
+    // (ebt_shard_pack's prefix) are min(k, the kept rows scoring >= t_floor) -- those rank
+    // before every other kept row; read from the exact scores in LDS, no second pass over the
+    // written list. (A barrier first: the last pass's scores come from other waves.)
+    __syncthreads();
+    const double tf = t_floor ? t_floor[b] : -__builtin_inf();
+    int c = 0;
+    for (int j = tid; j < nk; j += RTHREADS) c += sc[j] >= tf ? 1 : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (lane == 0 && c) atomicAdd(&npk, c);   // read after the ordering's barriers
+  }
   // 3. order the kept rows (score desc, row asc); positions past them read NaN / -1
   if (nk <= RESCORE_RANK_MAX) {
     // few rows (C2 / C3: ~120-150): each row's position is the number of rows before it,
@@ -527,6 +541,7 @@ __global__ __launch_bounds__(RTHREADS) void rescore_kernel(
     if (corrupt) ok = -2;                           // internal error: row out of range
     if (xbad) ok = -3;                              // caller error: unsorted exclusion segment
     certified[b] = ok;
+    if (pack.len) pack.len[b] = (uint32_t)(npk < k ? npk : k);
     // rows gathered by the two passes (roofline accounting: ebt_timer_count_rows), spread over
     // 64 counters 128 bytes apart: one address taking every query's atomic serialised them and
     // slowed the measured kernel by ~9 % at C3
@@ -776,7 +791,8 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
             const double* t_floor, double* out_s, int64_t* out_r, int32_t* certified,
             hipStream_t st, const int* ovf_cnt, int ovf_cap, unsigned long long* gathered,
             int64_t list_base, const float* theta, const int64_t* excl_off,
-            const int64_t* excl_rows) {
+            const int64_t* excl_rows, const ShardPackOut* pack) {
+  const ShardPackOut po = pack ? *pack : ShardPackOut{};
   if (!q64 || !cat || !gnorm || !cand_vals || !cand_rows || !eps || !out_s || !out_r ||
       !certified || B < 0 || d <= 0 || ld < d || k < 1 || kprime < k || kprime > 4096 ||
       dtype < 0 || dtype > 3) {
@@ -798,8 +814,8 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
   // Measured and not the default (profiles/r3/rescore_lds_ab.txt): the LDS-DMA batches
   // (16 rows of 1.5 KiB per round trip at C2) took 71-75 us per C2 step against 59-60 us for the
   // register gather, interleaved on one MI355X; C3 0.616 vs 0.564 ms. Kept for that A/B (it
-  // does not take the exclusion check: a call with exclusions uses the register form).
-  if (vec && !excl_off) {
+  // takes neither the exclusion check nor the pack count: such calls use the register form).
+  if (vec && !excl_off && !po.len) {
     const int row_bytes = d * es;
     int R = (24 << 10) / row_bytes;
     R = R > 64 ? 64 : R;
@@ -835,7 +851,7 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
   hipLaunchKernelGGL((rescore_kernel<DT, true, NU>), grid, block, lds_r, st, q64, d, cat, ld,   \
                      gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,      \
                      t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap, gathered, list_base,   \
-                     theta, excl_off, excl_rows);
+                     theta, excl_off, excl_rows, po);
 #define EBT_RSR_NU(DT)                                                                          \
   switch (nu) {                                                                                 \
     case 1: EBT_RSR(DT, 1) break;                                                               \
@@ -862,12 +878,12 @@ int rescore(const double* q64, int64_t B, int32_t d, const void* cat, int dtype,
     hipLaunchKernelGGL((rescore_kernel<DT, true>), grid, block, lds, st, q64, d, cat, ld,       \
                        gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,    \
                        t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap, gathered, list_base, \
-                       theta, excl_off, excl_rows);                                                                  \
+                       theta, excl_off, excl_rows, po);                                                                  \
   else                                                                                          \
     hipLaunchKernelGGL((rescore_kernel<DT, false>), grid, block, lds, st, q64, d, cat, ld,      \
                        gnorm, row_offset, cand_vals, cand_rows, kprime, kpp, k, n_rows, eps,    \
                        t_floor, out_s, out_r, certified, ovf_cnt, ovf_cap, gathered, list_base, \
-                       theta, excl_off, excl_rows);
+                       theta, excl_off, excl_rows, po);
   switch (dtype) {
     case EBT_F32: EBT_RS(EBT_F32) break;
     case EBT_BF16: EBT_RS(EBT_BF16) break;
@@ -956,9 +972,9 @@ size_t merge_corank_lds(int R, int P) {
 
 // The lists' sources. DenseSrc (merge_topk_corank_kernel): [R][B][k] f64 scores + i64 rows
 // (row < 0 = padding). PackedSrc (merge_packed_kernel): every rank's packed list of
-// ebt_shard_pack (one all-gathered byte buffer, `stride` bytes per rank): u32 starts[B + 1], then
-// f64 scores[cap], then i32 rows[cap]; query b's entries are [starts[b], starts[b + 1]) clipped
-// to cap (the rest was not sent).
+// ebt_shard_pack (one all-gathered byte buffer, `stride` bytes per rank): u32 start[B], u32
+// len[B] (+ scratch), then f64 scores[cap], then i32 rows[cap]; query b's entries are
+// [start[b], start[b] + len[b]) clipped to cap (the rest was not sent).
 struct DenseSrc {
   const double* scores;
   const int64_t* rows;
@@ -970,6 +986,9 @@ struct PackedSrc {
 
 __device__ __forceinline__ const uint32_t* pk_starts(const PackedSrc& p, int r) {
   return (const uint32_t*)(p.recv + (int64_t)r * p.stride);
+}
+__device__ __forceinline__ const uint32_t* pk_lens(const PackedSrc& p, int r, int64_t B) {
+  return (const uint32_t*)(p.recv + (int64_t)r * p.stride) + B;
 }
 __device__ __forceinline__ const double* pk_scores(const PackedSrc& p, int r, int64_t B) {
   return (const double*)(p.recv + (int64_t)r * p.stride + shard_pack_hdr_bytes(B));
@@ -1232,8 +1251,7 @@ __global__ __launch_bounds__(MP_THREADS) void merge_packed_kernel(
     const int r = r0 + tid;
     int v = 0;
     if (r < R) {
-      const uint32_t* st = pk_starts(src, r);
-      const int64_t s0 = st[b], s1 = st[b + 1];
+      const int64_t s0 = pk_starts(src, r)[b], s1 = s0 + pk_lens(src, r, B)[b];
       const int64_t a = s0 < src.cap ? s0 : src.cap, e = s1 < src.cap ? s1 : src.cap;
       v = (int)(e - a < k ? e - a : k);
       pst[r] = (int)a;
@@ -1418,7 +1436,7 @@ __global__ __launch_bounds__(SHARD_PACK_QPB) void shard_pack_count_kernel(
     total += wsum[w];
   }
   if (b < B) hdr[b] = (uint32_t)(base + incl - cnt);  // start within the workgroup
-  if (tid == 0) hdr[B + 1 + blockIdx.x] = (uint32_t)total;
+  if (tid == 0) hdr[2 * B + blockIdx.x] = (uint32_t)total;
 }
 
 // (64 queries per workgroup -- 64 workgroups at B = 4096, not 16 -- and SHARD_PACK_COPY_THREADS
@@ -1435,7 +1453,7 @@ __global__ __launch_bounds__(SHARD_PACK_COPY_THREADS) void shard_pack_copy_kerne
   const int tid = threadIdx.x;
   const int64_t q0 = (int64_t)blockIdx.x * SHARD_PACK_QPB;
   const int nq = B - q0 < SHARD_PACK_QPB ? (int)(B - q0) : SHARD_PACK_QPB;
-  const uint32_t* tot = hdr + B + 1;
+  const uint32_t* tot = hdr + 2 * B;
   if (tid < 64) {  // the totals of the workgroups before this one
     uint32_t s = 0;
     for (int i = tid; i < (int)blockIdx.x; i += 64) s += tot[i];
@@ -1447,8 +1465,10 @@ __global__ __launch_bounds__(SHARD_PACK_COPY_THREADS) void shard_pack_copy_kerne
   if (tid == 0) lst[nq] = tot[blockIdx.x];
   __syncthreads();
   const uint32_t g0 = gbase, n = lst[nq];
-  if (tid < nq) hdr[q0 + tid] = g0 + lst[tid];
-  if (blockIdx.x == gridDim.x - 1 && tid == 0) hdr[B] = g0 + n;
+  if (tid < nq) {
+    hdr[q0 + tid] = g0 + lst[tid];                // start
+    hdr[B + q0 + tid] = lst[tid + 1] - lst[tid];  // len
+  }
   for (uint32_t t = tid; t < n; t += SHARD_PACK_COPY_THREADS) {
     int lo = 0, hi = nq - 1;  // the last query whose start <= t
     while (lo < hi) {
@@ -1462,6 +1482,60 @@ __global__ __launch_bounds__(SHARD_PACK_COPY_THREADS) void shard_pack_copy_kerne
       orow[pos] = (int32_t)rows[b * k + j];
     }
   }
+}
+
+// The pack's second half when the sharded rescore counted already (len[b] in the header): each
+// workgroup's base is the sum of len over the queries before it (at most B values, L2-resident:
+// no block totals, so no counting launch), then the starts and the copy as shard_pack_copy_kernel.
+__global__ __launch_bounds__(SHARD_PACK_COPY_THREADS) void shard_pack_lens_kernel(
+    const double* __restrict__ scores, const int64_t* __restrict__ rows, int64_t B, int k,
+    int64_t cap, char* __restrict__ send) {
+  __shared__ uint32_t lst[SHARD_PACK_QPB + 1];
+  __shared__ uint32_t part[SHARD_PACK_COPY_THREADS / 64];
+  uint32_t* hdr = (uint32_t*)send;
+  const uint32_t* len = hdr + B;
+  double* os = (double*)(send + shard_pack_hdr_bytes(B));
+  int32_t* orow = (int32_t*)(send + shard_pack_hdr_bytes(B) + cap * 8);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t q0 = (int64_t)blockIdx.x * SHARD_PACK_QPB;
+  const int nq = B - q0 < SHARD_PACK_QPB ? (int)(B - q0) : SHARD_PACK_QPB;
+  uint32_t sum = 0;   // the queries before this workgroup's
+  for (int64_t i = tid; i < q0; i += SHARD_PACK_COPY_THREADS) sum += len[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  if (lane == 0) part[wave] = sum;
+  if (wave == 0) {    // this workgroup's queries: an inclusive scan of their lens
+    uint32_t v = lane < nq ? len[q0 + lane] : 0u;
+    const uint32_t incl = wave_scan_add_u32(v);
+    lst[lane + 1] = incl;
+    if (lane == 0) lst[0] = 0u;
+  }
+  __syncthreads();
+  uint32_t g0 = 0;
+#pragma unroll
+  for (int w = 0; w < SHARD_PACK_COPY_THREADS / 64; ++w) g0 += part[w];
+  const uint32_t n = lst[nq];
+  if (tid < nq) hdr[q0 + tid] = g0 + lst[tid];   // start
+  for (uint32_t t = tid; t < n; t += SHARD_PACK_COPY_THREADS) {
+    int lo = 0, hi = nq - 1;  // the last query whose start <= t (an empty one is skipped)
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (lst[mid] <= t) lo = mid;
+      else hi = mid - 1;
+    }
+    const int64_t b = q0 + lo, j = t - lst[lo], pos = (int64_t)g0 + t;
+    if (pos < cap) {
+      os[pos] = scores[b * k + j];
+      orow[pos] = (int32_t)rows[b * k + j];
+    }
+  }
+}
+
+int shard_pack_lens(const double* scores, const int64_t* rows, int64_t B, int32_t k,
+                    int64_t cap, void* send, hipStream_t st) {
+  hipLaunchKernelGGL(shard_pack_lens_kernel, dim3((unsigned)ceil_div(B, SHARD_PACK_QPB)),
+                     dim3(SHARD_PACK_COPY_THREADS), 0, st, scores, rows, B, k, cap, (char*)send);
+  return launch_check("shard_pack_lens_kernel");
 }
 
 int64_t shard_list_width(int32_t k, int32_t world) {
@@ -1788,7 +1862,9 @@ __device__ __forceinline__ double key2d(uint64_t k) {
 
 __global__ __launch_bounds__(256) void union_floor_kernel(const float* __restrict__ g, int R,
                                                           int64_t B, int ld, int k,
-                                                          double* __restrict__ t_floor) {
+                                                          double* __restrict__ t_floor,
+                                                          uint32_t* __restrict__ zero2) {
+  if (zero2 && blockIdx.x == 0 && threadIdx.x < 2) zero2[threadIdx.x] = 0u;
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
@@ -1826,7 +1902,11 @@ constexpr int UF_PL = 32;
 template <int W, int PL>
 __global__ __launch_bounds__(256) void union_floor_reg_kernel(const float* __restrict__ g, int R,
                                                               int64_t B, int ld, int k,
-                                                              double* __restrict__ t_floor) {
+                                                              double* __restrict__ t_floor,
+                                                              uint32_t* __restrict__ zero2) {
+  // (zero2: two words the caller needs zeroed before its next kernel -- the sharded step's pack
+  // counter and "incomplete" flag, one memset launch less per step)
+  if (zero2 && blockIdx.x == 0 && threadIdx.x < 2) zero2[threadIdx.x] = 0u;
   __shared__ int wc[2][4];
   __shared__ uint64_t wmm[2][4];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1920,9 +2000,16 @@ __global__ void certify_cut_kernel(int32_t* __restrict__ cert, const int32_t* __
 
 }  // namespace ebt
 
+namespace ebt {
+int union_floor(const float* gathered, int32_t R, int64_t B, int32_t ld, int32_t k,
+                double* t_floor, hipStream_t stream, uint32_t* zero2);
+}
 extern "C" int ebt_union_floor(const float* gathered, int32_t R, int64_t B, int32_t ld, int32_t k,
                                double* t_floor, void* stream) {
-  using namespace ebt;
+  return ebt::union_floor(gathered, R, B, ld, k, t_floor, (hipStream_t)stream, nullptr);
+}
+int ebt::union_floor(const float* gathered, int32_t R, int64_t B, int32_t ld, int32_t k,
+                     double* t_floor, hipStream_t stream, uint32_t* zero2) {
   if (!gathered || !t_floor || R < 1 || B < 0 || ld < 2 || k < 1 || (int64_t)R * (ld - 1) > (1 << 30)) {
     set_error("ebt_union_floor: bad arguments (R=%d B=%lld ld=%d k=%d)", R, (long long)B, ld, k);
     return EBT_EINVAL;
@@ -1934,7 +2021,7 @@ extern "C" int ebt_union_floor(const float* gathered, int32_t R, int64_t B, int3
 #define EBT_UF(W, PL, G)                                                                       \
   {                                                                                           \
     hipLaunchKernelGGL((union_floor_reg_kernel<W, PL>), G, blk, 0, st, gathered, R, B, ld, k, \
-                       t_floor);                                                              \
+                       t_floor, zero2);                                                       \
     return launch_check("union_floor_reg_kernel");                                            \
   }
   if (n <= 64 * 4) EBT_UF(1, 4, g1)
@@ -1945,7 +2032,7 @@ extern "C" int ebt_union_floor(const float* gathered, int32_t R, int64_t B, int3
   if (n <= 256 * UF_PL) EBT_UF(4, 32, g4)
 #undef EBT_UF
   hipLaunchKernelGGL(union_floor_kernel, dim3((unsigned)ceil_div(B, 4)), dim3(256), 0,
-                     (hipStream_t)stream, gathered, R, B, ld, k, t_floor);
+                     (hipStream_t)stream, gathered, R, B, ld, k, t_floor, zero2);
   return launch_check("union_floor_kernel");
 }
 

@@ -962,6 +962,58 @@ __device__ float wave_topk_write(const uint64_t (&x)[WTOP_E], int kprime, int k,
   return kth;
 }
 
+// The row-sharded step's floor entries (ebt_floor_pack's [w + 1] layout) from the wave merge's
+// union, fused into the screen's last merge: the w largest keys of the union (= the w largest
+// of the final list's k best, w <= k <= k'), keys above the w-th first, then as many equal to it
+// as fit, -inf past them, then eps. The w-th key by bisection on ballot counts, as floor_pack.
+template <int E>
+__device__ void wave_floor_write(const uint64_t (&x)[WTOP_E], int w, float* dst, int lane,
+                                 float eps) {
+  uint32_t kx[E];
+  int nvalid = 0;
+  uint32_t kmax = 0u, kmin = 0xffffffffu;
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    kx[j] = (uint32_t)(x[j] >> 32);
+    nvalid += __popcll(__ballot(kx[j] != 0u));
+    kmax = max(kmax, kx[j]);
+    if (kx[j] != 0u) kmin = min(kmin, kx[j]);
+  }
+  kmax = wave_max_u32(kmax);
+  kmin = wave_min_u32(kmin);
+  uint32_t t = 0u;
+  if (nvalid > w) {
+    auto count_ge = [&](uint32_t v) {
+      int c = 0;
+#pragma unroll
+      for (int j = 0; j < E; ++j) c += __popcll(__ballot(kx[j] >= v));
+      return c;
+    };
+    uint32_t lo = kmin, hi = kmax;  // count_ge(kmin) = nvalid >= w
+    while (lo < hi) {
+      const uint32_t mid = lo + ((hi - lo) >> 1) + 1u;
+      if (count_ge(mid) >= w) lo = mid;
+      else hi = mid - 1u;
+    }
+    t = lo;
+  }
+  int base = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const bool pick = kx[j] != 0u && (pass == 0 ? (nvalid <= w || kx[j] > t)
+                                                  : (nvalid > w && kx[j] == t));
+      const uint64_t m = __ballot(pick);
+      const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (pick && pos < w) dst[pos] = key2f(kx[j]);
+      base += __popcll(m);
+    }
+  }
+  for (int j = (base < w ? base : w) + lane; j < w; j += 64) dst[j] = -__builtin_inff();
+  if (lane == 0) dst[w] = eps;
+}
+
 // (double)kth - 2 eps rounded down to a float (the segment threshold / speculative check value)
 __device__ __forceinline__ float kth_minus_2eps_down(float kth, float eps) {
   const double t = (double)kth - 2.0 * (double)eps;
@@ -992,7 +1044,8 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
     const uint8_t* __restrict__ counts, int64_t ld_counts, int n_groups,
     const float* __restrict__ dense, int64_t ld_dense, int n_dense, int64_t idx_base,
     int64_t row_offset, const int64_t* __restrict__ eo, const int64_t* __restrict__ er,
-    int* __restrict__ ovf, const float* __restrict__ veps, const float* __restrict__ vspec) {
+    int* __restrict__ ovf, const float* __restrict__ veps, const float* __restrict__ vspec,
+    float* __restrict__ fout, int fw, const float* __restrict__ feps) {
   __shared__ uint64_t stage[WMERGE_Q][WTOP_N];  // the union
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t b = (int64_t)blockIdx.x * WMERGE_Q + w;
@@ -1250,6 +1303,11 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
   const float kth =
       ne <= 8 ? wave_topk_write<8>(x, kprime, k, fv + b * kprime, fi + b * kprime, lane, key_lo)
               : wave_topk_write<WTOP_E>(x, kprime, k, fv + b * kprime, fi + b * kprime, lane, key_lo);
+  if (fout) {  // the floor entries of the row-sharded step (ebt_floor_pack folded in)
+    const float fe = feps ? feps[b] : -__builtin_inff();
+    if (ne <= 8) wave_floor_write<8>(x, fw, fout + b * (fw + 1), lane, fe);
+    else wave_floor_write<WTOP_E>(x, fw, fout + b * (fw + 1), lane, fe);
+  }
   const bool any_over = __ballot(over) != 0ull;
 #ifdef EBT_MERGE_STAMP
   MST(3);
@@ -1284,8 +1342,9 @@ int merge_segment_wave(float* fv, int64_t* fi, int64_t B, int kprime, int k, con
                        int64_t ld_cand, int slots, const uint8_t* counts, int64_t ld_counts,
                        int64_t n_groups, int64_t row_offset, const int64_t* eo,
                        const int64_t* er, int* ovf, hipStream_t st, const float* veps,
-                       const float* vspec) {
+                       const float* vspec, float* fout, int fw, const float* feps) {
   if (B < 0 || kprime < 1 || kprime > WMERGE_K || k < 1 || k > kprime || n_groups < 1 ||
+      (fout && (fw < 1 || fw > k)) ||
       n_groups > 64 * 16 * WCNT ||
       ld_counts < n_groups || ld_counts % 16 != 0 || ((uintptr_t)counts & 15) ||
       ld_cand < n_groups * slots) {
@@ -1295,7 +1354,7 @@ int merge_segment_wave(float* fv, int64_t* fi, int64_t B, int kprime, int k, con
   if (B == 0) return EBT_OK;
   hipLaunchKernelGGL(merge_wave_kernel<false>, dim3((unsigned)ceil_div(B, WMERGE_Q)),
                      dim3(STHREADS), 0, st, fv, fi, B, kprime, k, cand, ld_cand, slots, counts, ld_counts, (int)n_groups, nullptr,
-                     0, 0, 0, row_offset, eo, er, ovf, veps, vspec);
+                     0, 0, 0, row_offset, eo, er, ovf, veps, vspec, fout, fw, feps);
   return launch_check("merge_wave_kernel");
 }
 
@@ -1311,7 +1370,7 @@ int pilot_topk(const float* S, int64_t ld_s, int64_t B, int n, int64_t idx_base,
   if (B == 0) return EBT_OK;
   hipLaunchKernelGGL(merge_wave_kernel<true>, dim3((unsigned)ceil_div(B, WMERGE_Q)),
                      dim3(STHREADS), 0, st, fv, fi, B, kprime, k, nullptr, 0, 1, nullptr, 0, 0, S, ld_s, n, idx_base, 0, nullptr,
-                     nullptr, nullptr, nullptr, nullptr);
+                     nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr);
   return launch_check("merge_wave_kernel");
 }
 

@@ -64,11 +64,13 @@ def test_pack_merge_equals_full_merge(cuda_device, R, B, k, ties):
     for a in range(R):
         L.call("ebt_shard_pack", L.ptr(gs[a].contiguous()), L.ptr(gr[a].contiguous()), B, k,
                L.ptr(tf), cap, L.ptr(recv[a * nbytes:]), st)
-        hdr = recv[a * nbytes:a * nbytes + 4 * (B + 1)].view(torch.int32).cpu().numpy()
+        # header (0.3.2): u32 start[B], u32 len[B]; ebt_shard_pack's starts are the prefix sum
+        hdr = recv[a * nbytes:a * nbytes + 8 * B].view(torch.int32).cpu().numpy()
+        start, ln = hdr[:B], hdr[B:]
         want = ((r[a] >= 0) & (s[a] >= floor[:, None])).sum(1)
-        np.testing.assert_array_equal(np.diff(hdr), want)
-        assert hdr[0] == 0
-        counts.append(hdr[-1])
+        np.testing.assert_array_equal(ln, want)
+        np.testing.assert_array_equal(start, np.concatenate([[0], np.cumsum(want)[:-1]]))
+        counts.append(int(want.sum()))
     out_s = torch.empty((B, k), dtype=torch.float64, device=dev)
     out_r = torch.empty((B, k), dtype=torch.int64, device=dev)
     inc = torch.zeros(1, dtype=torch.int32, device=dev)

@@ -160,3 +160,33 @@ def test_c5_small_batch_many_groups(cuda_device):
     indexes (16383 at k' = 1256, select_topk.hip merge_block_max_groups); the segment is
     clamped / merged in parts instead of failing."""
     run_workload(cuda_device, "C5", n_sample=16, n=4_500_000, b=1024, full_device_check=False)
+
+
+@pytest.mark.parametrize("spread", [0.02, 0.2])
+def test_clustered_catalog_reruns_stay_exact(cuda_device, spread):
+    """the speculative screen's later segments are sized for (k + k') / 2 kept rows
+    per r0 rows (api.hip run_screen_spec); on a clustered, near-duplicate-heavy catalog a
+    segment's hits may overflow the merge, and each overflowed query is rerun unfused. Here:
+    64 tight clusters of ~3100 rows each (row = center + spread x noise), queries drawn at the
+    centers, so every query has thousands of rows in its k-th score's neighbourhood. The
+    answers stay bit-exact against the float64 oracle whatever the rerun rate, which is
+    reported (the first pass's certificates: 1 exact, 0 widened, -1 rerun unfused)."""
+    import robot_ebert_amd as ebt
+    from robot_ebert_amd.search import score_topk_finish, score_topk_submit
+    n, d, B, k, C = 200_000, 128, 512, 100, 64
+    rng = np.random.default_rng(17)
+    centers = rng.standard_normal((C, d))
+    x = centers[rng.integers(0, C, n)] + spread * rng.standard_normal((n, d))
+    q = centers[rng.integers(0, C, B)] + spread * 0.5 * rng.standard_normal((B, d))
+    x32 = x.astype(np.float32)
+    q32 = q.astype(np.float32)
+    cat = ebt.Catalog(torch.from_numpy(x32).to(cuda_device))
+    p = score_topk_submit(cat, k, queries=torch.from_numpy(q32).to(cuda_device))
+    s, r = score_topk_finish(p)
+    first = p.cert_host[:B].clone()   # the first pass's (the finish waited for them)
+    s_ref, r_ref = R.cosine_topk(q32.astype(np.float64), x32.astype(np.float64), k)
+    np.testing.assert_array_equal(r.cpu().numpy(), r_ref)
+    np.testing.assert_allclose(s.cpu().numpy(), s_ref, rtol=0, atol=1e-12)
+    rates = {c: int((first == c).sum()) for c in (1, 0, -1)}
+    print(f"\nclustered spread={spread}: first-pass certificates {rates} of {B}")
+    assert sum(rates.values()) == B
