@@ -13,6 +13,7 @@
 //   v_4x8_half  the same MFMA stream, fragments re-read from LDS every 2nd k step: 192 B/MFMA
 //   v_4x8_none  the same MFMA stream, operands rotated in registers, no LDS reads: 0 B/MFMA
 //   v_8x8_w4    8 x 8 blocks, 4 waves per CU (1 per SIMD), 256 B/MFMA  -- the larger tile
+//   v_8x8_w4_pipe  the same with the next step's fragments read under the current MFMAs
 //   v_4x4_w8    4 x 4 blocks, 8 waves, 512 B/MFMA
 //
 // Each variant runs back to back for ~2.5 s (the clock settles, MI355X_MICROARCH.md "DVFS
@@ -112,15 +113,78 @@ __global__ __launch_bounds__(64 * WAVES) void lever_kernel(const half8* __restri
   }
 }
 
-template <int FA, int FB, int WAVES, int RE>
+// The 8 x 8 register tile with the next k step's fragments read under the current step's MFMAs
+// (double-buffered operand registers: 2 x 16 fragments = 128 VGPRs beside 256 AGPR
+// accumulators): one wave per SIMD has no second wave to hide the ds_read latency behind, so
+// its own pipeline must.
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void lever_pipe_kernel(const half8* __restrict__ src,
+                                                                int iters, float* __restrict__ out,
+                                                                unsigned long long* __restrict__ st) {
+  constexpr int FA = 8, FB = 8;
+  __shared__ half8 lds[NFRAG * 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int i = tid; i < NFRAG * 64; i += 64 * WAVES) lds[i] = src[(blockIdx.x * 7 + i) % (NFRAG * 64 * 8)];
+  __syncthreads();
+  unsigned long long c0 = 0, r0 = 0;
+  if (tid == 0) {
+    c0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  f32x4 acc[FA][FB];
+#pragma unroll
+  for (int i = 0; i < FA; ++i)
+#pragma unroll
+    for (int j = 0; j < FB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wv = tid >> 6;
+  half8 a[FA], b[FB], an[FA], bn[FB];
+#pragma unroll
+  for (int i = 0; i < FA; ++i) a[i] = lds[(i & (NFRAG - 1)) * 64 + lane];
+#pragma unroll
+  for (int j = 0; j < FB; ++j) b[j] = lds[((FA + j) & (NFRAG - 1)) * 64 + lane];
+  for (int it = 0; it < iters; ++it) {
+    const int base = (it + 1 + wv) & (NFRAG - 1);
+#pragma unroll
+    for (int i = 0; i < FA; ++i) an[i] = lds[((base + i) & (NFRAG - 1)) * 64 + lane];
+#pragma unroll
+    for (int j = 0; j < FB; ++j) bn[j] = lds[((base + FA + j) & (NFRAG - 1)) * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < FA; ++i)
+#pragma unroll
+      for (int j = 0; j < FB; ++j)
+        asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[i]), "v"(b[j]));
+#pragma unroll
+    for (int i = 0; i < FA; ++i) a[i] = an[i];
+#pragma unroll
+    for (int j = 0; j < FB; ++j) b[j] = bn[j];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < FA; ++i)
+#pragma unroll
+    for (int j = 0; j < FB; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+  out[(size_t)blockIdx.x * 64 * WAVES + tid] = s;
+  if (tid == 0) {
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    st[2 * blockIdx.x] = c1 - c0;
+    st[2 * blockIdx.x + 1] = r1 - r0;
+  }
+}
+
+template <int FA, int FB, int WAVES, int RE, bool PIPE = false>
 void run(const char* name, const half8* src, float* out, unsigned long long* st, int cus,
          double settle_s) {
   const double bytes_per_mfma = RE == 0 ? 0.0 : (double)(FA + FB) * 1024.0 / (FA * FB) / RE;
   // ~2 ms per launch
   const int iters = (int)(2.0e-3 * 1.9e15 / ((double)cus * WAVES * FA * FB * 16384.0));
   auto launch = [&] {
-    hipLaunchKernelGGL((lever_kernel<FA, FB, WAVES, RE>), dim3(cus), dim3(64 * WAVES), 0, 0, src,
-                       iters, out, st);
+    if constexpr (PIPE)
+      hipLaunchKernelGGL((lever_pipe_kernel<WAVES>), dim3(cus), dim3(64 * WAVES), 0, 0, src,
+                         iters, out, st);
+    else
+      hipLaunchKernelGGL((lever_kernel<FA, FB, WAVES, RE>), dim3(cus), dim3(64 * WAVES), 0, 0,
+                         src, iters, out, st);
   };
   launch();
   CHECK(hipDeviceSynchronize());
@@ -182,6 +246,7 @@ int main(int argc, char** argv) {
     run<4, 8, 8, 2>("v_4x8_half", src, out, st, cus, settle);
     run<4, 8, 8, 0>("v_4x8_none", src, out, st, cus, settle);
     run<8, 8, 4, 1>("v_8x8_w4", src, out, st, cus, settle);
+    run<8, 8, 4, 1, true>("v_8x8_w4_pipe", src, out, st, cus, settle);
     run<4, 4, 8, 1>("v_4x4_w8", src, out, st, cus, settle);
   }
   return 0;
