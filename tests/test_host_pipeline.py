@@ -184,3 +184,38 @@ def test_batcher_two_streams_order_and_answers():
                 assert after > ev_of[1] and ("record", after) in log[f:]
             else:
                 assert after == ev_of[bi]
+
+
+def test_sorted_csr_host_facts_and_retried():
+    """csr_from_lists' SortedCSR carries the host facts that let the C entry skip reading the
+    liked CSR back (EBT_FLAG_LIKED_CHECKED only when every segment is non-empty and every row in
+    the catalog's range); hostio.retried reads a finished batch's first-pass certificates (and
+    the C entry's k > n padding) to decide whether its results' D2H needs a fresh event."""
+    from robot_ebert_amd.hostio import retried
+    from robot_ebert_amd.search import SortedCSR, csr_from_lists, csr_sorted
+    c = csr_from_lists([[5, 1, 3], [7], [2, 2]], torch.device("cpu"))
+    assert isinstance(c, SortedCSR) and c.min_len == 1 and (c.row_min, c.row_max) == (1, 7)
+    assert c[0].tolist() == [0, 3, 4, 6] and c[1].tolist() == [1, 3, 5, 7, 2, 2]
+    assert c.checked_for(0, 8) and not c.checked_for(0, 7) and not c.checked_for(2, 100)
+    e = csr_from_lists([[4], []], torch.device("cpu"))
+    assert e.min_len == 0 and not e.checked_for(0, 100)
+    z = csr_from_lists([[], []], torch.device("cpu"))
+    assert z.row_min is None and not z.checked_for(0, 100)
+    assert not SortedCSR(c[0], c[1]).checked_for(0, 100)   # facts unknown: not checked
+    assert csr_sorted(c) is c
+
+    class Rec:
+        def __init__(self, B, k, k_eff):
+            self.B, self.k, self.k_eff = B, k, k_eff
+
+    class P:
+        def __init__(self, cert, rec=None):
+            self.cert_host = torch.tensor(cert, dtype=torch.int32)
+            if rec is not None:
+                self.pending = rec
+    assert not retried(P([1, 1, 1, 77], Rec(3, 10, 10)))    # slot B is the C entry's flag
+    assert retried(P([1, 0, 1, 0], Rec(3, 10, 10)))
+    assert retried(P([1, 1, 1, 0], Rec(3, 10, 5)))          # k > n: padded in the finish
+    assert not retried(P([1, 1]))                           # the Python path: B entries
+    assert retried(P([1, -1]))
+    assert retried(object())                                # unknown: a fresh event
