@@ -5,6 +5,7 @@
 #               interleaved: _abl/libebert_r6base.so (round-6 tree before the sharded-step
 #               fusions), the current build, twice each
 #   lever OUT   the LDS-read-bytes-per-MFMA clock lab (tools/gemm_lab/lds_lever.hip)
+#   c5full OUT  C5 on 8 thread ranks at the real 6.25M-row shard size (tools/c5_full_shards.py)
 export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 MODE=$1
@@ -26,6 +27,12 @@ case "$MODE" in
         python3 -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; print(sys.argv[2], {k: d[k] for k in d if 'ms' in k})" "$O/rs_${v}_$i.json" "$v$i"
       done
     done
+    ;;
+  c5full)
+    # C5 on 8 thread ranks of 6.25M-row shards, one batch through the C ABI's sharded step
+    timeout -k 10 1000 python -u tools/c5_full_shards.py --sample 16 --replay 4 > "$O/c5full.json" \
+      2> "$O/c5full.log" || { tail -20 "$O/c5full.log"; exit 1; }
+    cat "$O/c5full.json"
     ;;
   lever)
     # tools/gemm_lab/lds_lever.hip built as _abl/lds_lever: LDS-read bytes per MFMA vs clock

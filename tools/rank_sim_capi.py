@@ -85,7 +85,8 @@ def main():
     per_step = len(record) // a.steps
     sizes = sorted(set(int(g.numel()) for g in record))
     recv_total = sum(int(g.numel()) for g in record)
-    # the packed results' gathers: every rank's starts[B] = its entries above the floor
+    # the packed results' gathers: every rank's entries above the floor = the sum of its
+    # per-query len[B] (header u32 start[B], u32 len[B] since ABI 0.3.2)
     lib = _lib.load()
     w = int(lib.ebt_shard_list_width(k, W))
     cap = int(lib.ebt_shard_pack_cap(B, k, W, cfg["n"]))
@@ -93,8 +94,8 @@ def main():
     counts = []
     for g in record:
         if pb and g.numel() == W * pb:
-            v = g.view(W, pb)[:, :4 * (B + 1)].contiguous().view(torch.int32)
-            counts.append(v[:, B].double().cpu())
+            v = g.view(W, pb)[:, :8 * B].contiguous().view(torch.int32)
+            counts.append(v[:, B:2 * B].double().sum(1).cpu())
     sent = torch.stack(counts) if counts else None
     ref = outs[0]
     cat0 = cats[0]
