@@ -151,21 +151,24 @@ def main():
     if a.replay:
         # rank 0 alone: the other shards freed, three workspaces, every all-gather replayed
         record = shared["record"]
+        by_size = {}
+        for g in record:   # one batch's gathers, by size: with batches in flight the floor
+            by_size.setdefault(g.numel(), []).append(g)   # and results gathers interleave
         cat0 = cats[0]
         del cats[1:]
         torch.cuda.empty_cache()
-        state = {"i": 0}
+        state = {"i": 0, "n": {}}
 
         def rgather(recv, send):
-            g = record[state["i"] % len(record)]
-            state["i"] += 1
-            recv.copy_(g)
+            lst = by_size[recv.numel()]
+            j = state["n"].get(recv.numel(), 0)
+            state["n"][recv.numel()] = j + 1
+            recv.copy_(lst[j % len(lst)])
         timer = ebt.Timer()
         eng = ShardedTopk(cat0, k, B, _AllReduceSlot(0, W, gather=rgather), slots=3, timer=timer)
-        state["i"] = 0
         eng.run(1, q)                      # warm
         torch.cuda.synchronize()
-        state["i"] = 0
+        state["n"] = {}
         timer.reset()
         t3 = time.perf_counter()
         s1, r1 = eng.run(a.replay, q)
