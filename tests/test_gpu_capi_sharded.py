@@ -92,7 +92,7 @@ REDUCE = ctypes.CFUNCTYPE(ctypes.c_int, VP, VP, SZ, VP)
 
 
 def run_ranks(lib, hip, full, world, k, q=None, liked=None, excl=None, fail_rank=-1,
-              allreduce=False):
+              allreduce=False, opt=None):
     """ebt_cosine_topk_sharded on `world` thread ranks; returns per-rank (rc, message, s, r).
     allreduce: the comm also offers all_reduce_f64 (a barrier exchange summing in rank order)."""
     dev = full.device
@@ -148,7 +148,8 @@ def run_ranks(lib, hip, full, world, k, q=None, liked=None, excl=None, fail_rank
         comm = Comm(rank, world, n, cb, None, ctypes.cast(rcb, VP) if allreduce else None)
         cat = cats[rank][0]
         B = q.shape[0] if q is not None else liked[0].numel() - 1
-        need = lib.ebt_sharded_workspace_bytes(ctypes.byref(cat), ctypes.byref(comm), B, k, None)
+        optp = ctypes.byref(opt) if opt is not None else None
+        need = lib.ebt_sharded_workspace_bytes(ctypes.byref(cat), ctypes.byref(comm), B, k, optp)
         assert need > 0
         ws = torch.empty(need, dtype=torch.uint8, device=dev)
         s = torch.full((B, k), float("nan"), dtype=torch.float64, device=dev)
@@ -157,7 +158,7 @@ def run_ranks(lib, hip, full, world, k, q=None, liked=None, excl=None, fail_rank
         eo, er = excl if excl is not None else (None, None)
         rc = lib.ebt_cosine_topk_sharded(
             ctypes.byref(cat), ctypes.byref(comm), P(q), CODE[q.dtype] if q is not None else 0, B,
-            q.stride(0) if q is not None else 0, P(lo), P(lr), k, P(eo), P(er), None, P(ws), need,
+            q.stride(0) if q is not None else 0, P(lo), P(lr), k, P(eo), P(er), optp, P(ws), need,
             P(s), P(rr), None, torch.cuda.current_stream(dev).cuda_stream)
         msg = lib.ebt_last_error().decode() if rc else ""
         out[rank] = (rc, msg, s.cpu().numpy(), rr.cpu().numpy())
@@ -207,6 +208,26 @@ def test_sharded_capi_shared_threshold_exclusions(cuda_device, lib, hip):
                                  [excl[i] for i in sample])
     np.testing.assert_array_equal(r1[sample], r_ref)
     np.testing.assert_allclose(s1[sample], s_ref, rtol=0, atol=1e-12)
+
+
+def test_sharded_capi_local_retries_repack(cuda_device, lib, hip):
+    """Round 6: the sharded rescore counts each query's packed entries and one launch places
+    them -- unless the shard's local retries rewrote some list, when the finish packs again with
+    the two-launch ebt_shard_pack. Forced here: k' = k on 2 ranks of 350K rows (no shared
+    threshold: every shard's list holds k' candidates, so no query is certified at k' = k and
+    every query is retried at k' x 4); the answer equals the single-GPU path's at default
+    options and the float64 oracle."""
+    n, d, B, k, world = 700_000, 64, 256, 20, 2
+    c = gaussian(221, n, d, "f32")
+    qv = gaussian(222, B, d, "f32")
+    full = torch.from_numpy(c.astype(np.float32)).to(cuda_device)
+    q = torch.from_numpy(qv.astype(np.float32)).to(cuda_device)
+    res, calls = run_ranks(lib, hip, full, world, k, q=q, opt=Options(k, 0, 0))
+    assert calls == [2] * world          # floor, packed results (no threshold at 350K rows)
+    s1, r1 = check_equal_single(lib, full, res, k, q=q)
+    s_ref, r_ref = R.cosine_topk(qv[[0, 255]].astype(np.float32).astype(np.float64),
+                                 c.astype(np.float32).astype(np.float64), k)
+    np.testing.assert_array_equal(r1[[0, 255]], r_ref)
 
 
 def test_sharded_capi_large_k_block_merge(cuda_device, lib, hip):
