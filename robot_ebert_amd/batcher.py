@@ -29,6 +29,7 @@ with sklearn's ValueError (alone -- the rest of its batch is unaffected), result
 from __future__ import annotations
 
 import collections
+import os
 import queue
 import threading
 import time
@@ -67,13 +68,19 @@ class RecBatcher:
     def __init__(self, catalog, max_batch: int = 4096, max_wait_ms: float = 2.0,
                  score_fn: Optional[Callable] = None, history: int = 1024,
                  max_inflight: int = 2, stager="auto", submit_fn: Optional[Callable] = None,
-                 finish_fn: Optional[Callable] = None) -> None:
+                 finish_fn: Optional[Callable] = None,
+                 stage_min_bytes: Optional[int] = None) -> None:
         """catalog: the ``Catalog`` every request scores against. score_fn(catalog, k, liked=,
         exclude=) -> (scores [B, k], rows [B, k]); default: ``search.score_topk_submit`` /
         ``score_topk_finish`` (or submit_fn / finish_fn) with up to ``max_inflight`` batches on
         the GPU. stager: the host boundary's copy stream (hostio.HostStager; "auto" = one on the
         catalog's GPU, None = copies in line): a batch's liked / rated CSR goes to the device
-        under the previous batch's kernels and its results come back under the next one's."""
+        under the previous batch's kernels and its results come back under the next one's --
+        for batches whose CSRs reach `stage_min_bytes` (default 1 MiB, EBERT_STAGE_MIN_BYTES).
+        A route-sized batch (tens of users, tens of KB) goes in line: its copies take
+        microseconds, and the staging's dozen host-side stream / event / pinned-buffer calls per
+        batch cost more than they hide (round 6, tools/route_bench.py with and without: batched
+        scoring 10.1-11.0K requests/s staged vs 15.0-15.7K in line, profiles/r6/route/)."""
         if max_batch < 1:
             raise ValueError("max_batch must be >= 1")
         self.catalog = catalog
@@ -81,10 +88,13 @@ class RecBatcher:
         if stager == "auto":
             dev = getattr(catalog, "device", None)
             stager = None
-            if score_fn is None and dev is not None and getattr(dev, "type", None) == "cuda":
+            if (score_fn is None and dev is not None and getattr(dev, "type", None) == "cuda"
+                    and os.environ.get("EBERT_HOST_STAGER", "1") != "0"):   # "0": A/B knob
                 from .hostio import HostStager
                 stager = HostStager(dev)
         self.stager = stager
+        self.stage_min_bytes = int(stage_min_bytes if stage_min_bytes is not None
+                                   else os.environ.get("EBERT_STAGE_MIN_BYTES", 1 << 20))
         self.max_batch = int(max_batch)
         self.max_wait = float(max_wait_ms) / 1e3
         self._score = score_fn
@@ -243,7 +253,10 @@ class RecBatcher:
         self._slots.acquire()            # released by the completion thread
         try:
             ev = None
-            if self.stager is not None:
+            # the batch's CSR bytes (offsets + rows, liked and rated)
+            nbytes = 8 * (2 * (len(liked) + 1) + sum(len(x) for x in liked) +
+                          sum(len(x) for x in excl))
+            if self.stager is not None and nbytes >= self.stage_min_bytes:
                 # the batch's CSRs through the copy stream (pinned staging), then its kernels;
                 # an event right after them for its results' D2H
                 from .search import csr_from_lists
@@ -276,7 +289,7 @@ class RecBatcher:
             try:   # the slot is released whatever happens to this batch's callers
                 try:
                     scores, rows = finish(p)
-                    if self.stager is not None:
+                    if ev is not None:
                         # D2H on the copy stream after this batch's kernels only (a fresh event
                         # when its retries ran behind later batches), under the next batch
                         if retried(p):
