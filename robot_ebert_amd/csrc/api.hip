@@ -162,7 +162,9 @@ int merge_segment_wave(float*, int64_t*, int64_t, int, int, const uint64_t*, int
                        const uint8_t*, int64_t, int64_t, int64_t, const int64_t*, const int64_t*,
                        int*, hipStream_t, const float* veps = nullptr,
                        const float* vspec = nullptr, float* fout = nullptr, int fw = 0,
-                       const float* feps = nullptr);
+                       const float* feps = nullptr, float* tout = nullptr,
+                       const float* tin = nullptr, const float* teps = nullptr,
+                       int64_t B_pad = 0);
 int pilot_topk(const float*, int64_t, int64_t, int, int64_t, int, int, float*, int64_t*,
                hipStream_t);
 constexpr int64_t PILOT_ROWS = 1024;  // = WMERGE_H (select_topk.hip)
@@ -1020,7 +1022,7 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
     f_spread = f_spread < 2.5 ? 2.5 : f_spread;
   }
   int64_t r0 = 256 * lead;
-  bool first = true, verified = false;
+  bool first = true, verified = false, thr_raised = false;
   while (r0 < n_rows) {
     // expected hits <= 1 / f_spread of the merge's room beside the list. Hits per row: at
     // theta_spec H / n; after r0 rows the raised threshold (the list's k-th - 2 eps) keeps at
@@ -1053,8 +1055,10 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
     }
     const float* t = tspec;
     if (!first) {
-      rc = spec_threshold(fv, kprime, B, B_pad, k, a.eps, tspec, thr, ovf, 0, st);
-      if (rc) return rc;
+      if (!thr_raised) {  // (the previous wave merge wrote it: no launch)
+        rc = spec_threshold(fv, kprime, B, B_pad, k, a.eps, tspec, thr, ovf, 0, st);
+        if (rc) return rc;
+      }
       t = thr;
     }
     rc = filter_screen(a, r0, seg, t, cand + g0 * slots, L.ld_cand, slots, counts + g0,
@@ -1064,14 +1068,18 @@ static int run_screen_spec(const PipeArgs& a, const WsLayout& L, char* ws, float
     const bool fuse_verify = wave && !given && r0 + seg == n_rows;
     verified |= fuse_verify;
     const int64_t groups = g0 + ceil_div(seg, L.group_rows);
+    const bool last = r0 + seg == n_rows;
+    // the wave merge of a segment that is not the last also writes the next one's threshold
+    // (spec_threshold's RAISE folded in)
+    thr_raised = wave && !last;
     {
       StageScope s(timer, EBT_STAGE_MERGE_SELECT, st);
-      const bool last = r0 + seg == n_rows;
       if (wave)
         rc = merge_segment_wave(fv, fi, B, kprime, k, cand, L.ld_cand, slots, counts,
                                 L.ld_counts, groups, a.row_offset, a.excl_off, a.excl_rows, ovf,
                                 st, fuse_verify ? a.eps : nullptr, fuse_verify ? tspec : nullptr,
-                                last ? a.floor_out : nullptr, a.floor_w, a.eps);
+                                last ? a.floor_out : nullptr, a.floor_w, a.eps,
+                                thr_raised ? thr : nullptr, tspec, a.eps, B_pad);
       else  // sorted lists (the block merge sorts the union)
         rc = merge_segment(fv, fi, B, kprime, cand, L.ld_cand, slots, counts, L.ld_counts,
                            groups, a.row_offset, a.excl_off, a.excl_rows, ovf, st,

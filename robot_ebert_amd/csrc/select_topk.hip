@@ -1045,11 +1045,15 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
     const float* __restrict__ dense, int64_t ld_dense, int n_dense, int64_t idx_base,
     int64_t row_offset, const int64_t* __restrict__ eo, const int64_t* __restrict__ er,
     int* __restrict__ ovf, const float* __restrict__ veps, const float* __restrict__ vspec,
-    float* __restrict__ fout, int fw, const float* __restrict__ feps) {
+    float* __restrict__ fout, int fw, const float* __restrict__ feps, float* __restrict__ tout,
+    const float* __restrict__ tin, const float* __restrict__ teps, int64_t B_pad) {
   __shared__ uint64_t stage[WMERGE_Q][WTOP_N];  // the union
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t b = (int64_t)blockIdx.x * WMERGE_Q + w;
-  if (b >= B) return;
+  if (b >= B) {
+    if (tout && b < B_pad && lane == 0) tout[b] = __builtin_inff();  // padding: no hits
+    return;
+  }
   uint64_t* U = stage[w];
 #ifdef EBT_MERGE_STAMP
   unsigned long long ms[5] = {0, 0, 0, 0, 0};
@@ -1319,6 +1323,12 @@ __global__ __launch_bounds__(STHREADS, 4) void merge_wave_kernel(
   }
 #endif
   if (lane == 0) {
+    // tout: the next segment's threshold from the list just written (spec_threshold_kernel's
+    // RAISE with tin = theta_spec, kth_threshold_kernel's value without), no launch of its own
+    if (tout) {
+      const float f = kth_minus_2eps_down(kth, teps[b]);
+      tout[b] = tin ? (f > tin[b] ? f : tin[b]) : f;  // NaN f keeps theta_spec
+    }
     // vspec: the speculative screen's VERIFY on the final list (spec_threshold_kernel,
     // SPEC_VERIFY) fused into the last merge: theta_spec > the k-th - 2 eps (rounded down), a
     // NaN or fewer than k entries fail with 2, as the separate launch would set after the merge
@@ -1342,19 +1352,22 @@ int merge_segment_wave(float* fv, int64_t* fi, int64_t B, int kprime, int k, con
                        int64_t ld_cand, int slots, const uint8_t* counts, int64_t ld_counts,
                        int64_t n_groups, int64_t row_offset, const int64_t* eo,
                        const int64_t* er, int* ovf, hipStream_t st, const float* veps,
-                       const float* vspec, float* fout, int fw, const float* feps) {
+                       const float* vspec, float* fout, int fw, const float* feps,
+                       float* tout, const float* tin, const float* teps, int64_t B_pad) {
   if (B < 0 || kprime < 1 || kprime > WMERGE_K || k < 1 || k > kprime || n_groups < 1 ||
-      (fout && (fw < 1 || fw > k)) ||
+      (fout && (fw < 1 || fw > k)) || (tout && (!teps || B_pad < B)) ||
       n_groups > 64 * 16 * WCNT ||
       ld_counts < n_groups || ld_counts % 16 != 0 || ((uintptr_t)counts & 15) ||
       ld_cand < n_groups * slots) {
     set_error("merge_segment_wave: bad arguments");
     return EBT_EINVAL;
   }
-  if (B == 0) return EBT_OK;
-  hipLaunchKernelGGL(merge_wave_kernel<false>, dim3((unsigned)ceil_div(B, WMERGE_Q)),
+  const int64_t nq = tout ? B_pad : B;  // waves past B only write the padding's threshold
+  if (nq == 0) return EBT_OK;
+  hipLaunchKernelGGL(merge_wave_kernel<false>, dim3((unsigned)ceil_div(nq, WMERGE_Q)),
                      dim3(STHREADS), 0, st, fv, fi, B, kprime, k, cand, ld_cand, slots, counts, ld_counts, (int)n_groups, nullptr,
-                     0, 0, 0, row_offset, eo, er, ovf, veps, vspec, fout, fw, feps);
+                     0, 0, 0, row_offset, eo, er, ovf, veps, vspec, fout, fw, feps, tout, tin, teps,
+                     B_pad);
   return launch_check("merge_wave_kernel");
 }
 
@@ -1370,7 +1383,8 @@ int pilot_topk(const float* S, int64_t ld_s, int64_t B, int n, int64_t idx_base,
   if (B == 0) return EBT_OK;
   hipLaunchKernelGGL(merge_wave_kernel<true>, dim3((unsigned)ceil_div(B, WMERGE_Q)),
                      dim3(STHREADS), 0, st, fv, fi, B, kprime, k, nullptr, 0, 1, nullptr, 0, 0, S, ld_s, n, idx_base, 0, nullptr,
-                     nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr);
+                     nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+                     nullptr, B);
   return launch_check("merge_wave_kernel");
 }
 
@@ -1448,28 +1462,52 @@ struct LeadArgs {
   uint8_t* counts;
   int64_t ld_counts;
 };
-__device__ __forceinline__ void lead_hits_wave(const LeadArgs& la, int64_t b, float th, int* ovf) {
+// The lead tiles' scores are loaded LEAD_LB tiles at a time (4 x LEAD_LB floats per lane), every
+// load of a batch issued before the first is used: one memory round trip per batch instead of
+// one per tile. The first batch can be issued earlier still (lead_load, before pool_kth's
+// bisection, whose ballot loop then hides its latency).
+constexpr int LEAD_LB = 8;
+struct LeadBatch {
+  float v[LEAD_LB][4];
+};
+__device__ __forceinline__ void lead_load(const LeadArgs& la, int64_t b, int p0, LeadBatch& lb) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int q = 0; q < LEAD_LB; ++q) {
+    if (p0 + q < la.lead) {  // uniform
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        lb.v[q][e] = la.s[b * la.ld + (int64_t)(p0 + q) * 256 + e * 64 + lane];
+    }
+  }
+}
+__device__ __forceinline__ void lead_hits_wave(const LeadArgs& la, int64_t b, float th, int* ovf,
+                                               LeadBatch& lb) {
   const int lane = threadIdx.x & 63;
   int over = 0;
-  for (int p = 0; p < la.lead; ++p) {
-    float v[4];
+  for (int p0 = 0; p0 < la.lead; p0 += LEAD_LB) {
+    if (p0 > 0) lead_load(la, b, p0, lb);  // (batch 0: the caller's lead_load)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = la.s[b * la.ld + (int64_t)p * 256 + e * 64 + lane];
-    uint32_t base = 0;
+    for (int q = 0; q < LEAD_LB; ++q) {
+      const int p = p0 + q;
+      if (p >= la.lead) break;  // uniform
+      uint32_t base = 0;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const bool hit = v[e] >= th;
-      const uint64_t bm = __ballot(hit);
-      const uint32_t pp = base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
-      if (hit && pp < (uint32_t)la.slots) {
-        const uint32_t row = (uint32_t)(p * 256 + e * 64 + lane);
-        la.cand[b * la.ld_cand + (int64_t)p * la.slots + pp] =
-            ((uint64_t)f2key(v[e]) << 32) | (uint64_t)(~row);
+      for (int e = 0; e < 4; ++e) {
+        const float v = lb.v[q][e];
+        const bool hit = v >= th;
+        const uint64_t bm = __ballot(hit);
+        const uint32_t pp = base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+        if (hit && pp < (uint32_t)la.slots) {
+          const uint32_t row = (uint32_t)(p * 256 + e * 64 + lane);
+          la.cand[b * la.ld_cand + (int64_t)p * la.slots + pp] =
+              ((uint64_t)f2key(v) << 32) | (uint64_t)(~row);
+        }
+        base += (uint32_t)__popcll(bm);
       }
-      base += (uint32_t)__popcll(bm);
+      if (lane == 0) la.counts[b * la.ld_counts + p] = (uint8_t)(base < 255u ? base : 255u);
+      over |= base > (uint32_t)la.slots ? 1 : 0;
     }
-    if (lane == 0) la.counts[b * la.ld_counts + p] = (uint8_t)(base < 255u ? base : 255u);
-    over |= base > (uint32_t)la.slots ? 1 : 0;
   }
   if (lane == 0 && over) ovf[b] = 1;
 }
@@ -1492,11 +1530,16 @@ __global__ __launch_bounds__(256) void pool_kth_kernel(const float* __restrict__
         fi[b * kprime + i] = -1;
       }
   }
+  LeadBatch lb;
   if (b >= B) {
     if (lane == 0) thr[b] = __builtin_inff();
-    if (la.lead > 0) lead_hits_wave(la, b, __builtin_inff(), ovf);   // zero counts
+    if (la.lead > 0) {   // zero counts
+      lead_load(la, b, 0, lb);
+      lead_hits_wave(la, b, __builtin_inff(), ovf, lb);
+    }
     return;
   }
+  if (la.lead > 0) lead_load(la, b, 0, lb);  // in flight during the bisection
   // gj > 0: the all-gathered [R][B][gj] layout of a row-sharded catalog's samples, read in place
   // (value g of query b at rank g / gj), instead of a [B][ld] row
   uint32_t kx[E];
@@ -1525,7 +1568,7 @@ __global__ __launch_bounds__(256) void pool_kth_kernel(const float* __restrict__
     th = key2f((uint32_t)lo);
   }
   if (lane == 0) thr[b] = th;
-  if (la.lead > 0) lead_hits_wave(la, b, th, ovf);
+  if (la.lead > 0) lead_hits_wave(la, b, th, ovf, lb);
 }
 int pool_kth(const float* pool, int64_t ld, int64_t B, int64_t B_pad, int G, int j, float* thr,
              hipStream_t st, float* fv, int64_t* fi, int kprime, int* ovf,
@@ -1591,7 +1634,9 @@ __global__ __launch_bounds__(256) void spec_given_lead_kernel(const float* __res
       fv[b * kprime + i] = -__builtin_inff();
       fi[b * kprime + i] = -1;
     }
-  lead_hits_wave(la, b, th, ovf);   // padding rows: +inf, zero counts
+  LeadBatch lb;
+  lead_load(la, b, 0, lb);
+  lead_hits_wave(la, b, th, ovf, lb);   // padding rows: +inf, zero counts
 }
 
 int spec_given_init(const float* theta, int64_t B, int64_t B_pad, float* tspec, float* fv,
