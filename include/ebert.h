@@ -66,7 +66,10 @@ extern "C" {
  *        arithmetic only); the exclusion-order check of ebt_cosine_topk* runs inside the rescore
  *        (certified = -3 from ebt_cosine_topk_prepared / ebt_rescore's callers for a query whose
  *        segment is not ascending); ebt_shard_sample_tiles (additive); the row counter of
- *        ebt_timer_count_rows is device-aware. */
+ *        ebt_timer_count_rows is device-aware.
+ * 0.3.3: a pinned certificate buffer of ebt_cosine_topk_submit / ebt_cosine_topk_sharded_submit
+ *        is written by the kernels themselves (no copy launch; EBT_EHIP from _finish if one was
+ *        not delivered); the speculative screen's segment thresholds come from its wave merges. */
 int ebt_version(void);
 
 /* Message for the last non-zero return on this thread ("" if none). */
@@ -426,9 +429,13 @@ size_t ebt_workspace_bytes(const ebt_catalog* cat, int64_t B, int32_t k, const e
  * are final. The two halves let a caller overlap batches: _submit enqueues the first pass
  * (no synchronisation for dense queries; the liked path reads its CSR offsets on the host) and
  * fills the caller's ebt_pending; _finish waits for THAT batch only (an event), reads its
- * certificates from cert_host (host memory, B + 1 int32; pinned memory keeps the copy
- * asynchronous) and runs the retries. Workspace, outputs and cert_host stay in use until
- * _finish returns. timer: NULL or an ebt_timer. */
+ * certificates from cert_host (host memory, B + 1 int32) and runs the retries. Pinned
+ * cert_host (hipHostMalloc / hipHostRegister, e.g. torch pin_memory) is written by the rescore
+ * kernel itself, one store per query across the host link (0.3.3: no copy launch; _submit
+ * marks the entries unset first and _finish fails with EBT_EHIP on one that was not
+ * delivered); pageable memory gets a copy from the workspace (EBT_HOST_DIRECT=0 forces the
+ * copy). Workspace, outputs and cert_host stay in use until _finish returns. timer: NULL or
+ * an ebt_timer. */
 typedef struct ebt_pending {
   const ebt_catalog* cat;
   ebt_options opt;
@@ -525,12 +532,12 @@ size_t ebt_sharded_workspace_bytes(const ebt_catalog* cat, const ebt_comm* comm,
 /* The same in three calls, so that a caller can keep batches in flight (the collectives and
  * the host's waits of one batch behind the GPU work of the next):
  *   _submit enqueues query prep, the threshold and floor all-gathers, the screen, the rescore
- *     and the certificates' copy to host[0 .. B] (caller's host memory, B + 2 int32; pinned
- *     keeps the copy asynchronous) and fills *pending;
+ *     and the certificates into host[0 .. B] (caller's host memory, B + 2 int32; pinned: the
+ *     rescore's own stores, else a copy -- as ebt_cosine_topk_submit) and fills *pending;
  *   _finish waits for THAT batch's certificates, runs the shard's local retries, packs the
  *     shard's entries above the catalog-wide floor (ebt_shard_pack), all-gathers them, merges
- *     (ebt_merge_packed) into out_scores / out_rows on the stream and copies the merge's
- *     "incomplete" flag to host[B + 1];
+ *     (ebt_merge_packed) into out_scores / out_rows on the stream and brings the merge's
+ *     "incomplete" flag to host[B + 1] (pinned: written by the merge itself);
  *   _wait waits for that flag (an event) and, when a rank's entries did not fit its packed
  *     capacity, re-merges from the full lists (two more all-gathers: every rank sees the same
  *     flag). The results are final when _wait returns.

@@ -649,7 +649,7 @@ using namespace ebt;
 
 extern "C" {
 
-int ebt_version(void) { return 302; }  // 0.3.2: hand-written sorts, folded checks (ebert.h)
+int ebt_version(void) { return 303; }  // 0.3.3: certificates into pinned host buffers (ebert.h)
 
 const char* ebt_last_error(void) { return g_err; }
 

@@ -60,6 +60,30 @@ constexpr int64_t RETRY_EXCL_MAX = 1LL << 20; // gathered exclusion rows per ret
 int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 size_t al(size_t v) { return (v + 255) & ~(size_t)255; }
 
+// The caller's certificate buffer, seen from the device when it is pinned host memory
+// (hipHostMalloc / hipHostRegister, e.g. a torch pin_memory tensor): the rescore then stores each
+// query's certificate straight into it -- one 4-byte store per query across the host link, no
+// copy launch behind the kernels (a D2H copy is a blit kernel here: ~4 us plus its boundary, 2 %
+// of a C2 batch). Anything else (pageable memory) -> nullptr: the workspace's certificates and
+// one hipMemcpyAsync, as before. EBT_HOST_DIRECT=0 keeps the copy (A/B).
+int32_t* host_mapped(int32_t* host) {
+  static const bool on = [] {
+    const char* v = getenv("EBT_HOST_DIRECT");
+    return !(v && v[0] == '0');
+  }();
+  void* dp = nullptr;
+  if (!on || !host) return nullptr;
+  if (hipHostGetDevicePointer(&dp, host, 0) != hipSuccess || !dp) {
+    (void)hipGetLastError();  // (pageable memory: clear the query's error for later checks)
+    return nullptr;
+  }
+  return (int32_t*)dp;
+}
+// written by the host into a directly delivered certificate buffer before the kernels run: a
+// value that is still there when the batch's event has passed was never delivered (the finish
+// fails loudly instead of reading a previous batch's leftovers as certificates)
+constexpr int32_t CERT_UNSET = 0x7fffffff;
+
 int64_t pad_batch(int64_t B) {
   B = B < 1 ? 1 : B;
   return B <= 128 ? round_up(B, 128) : round_up(B, 256);
@@ -529,6 +553,12 @@ int ebt_cosine_topk_submit(const ebt_catalog* cat, const void* q, int q_dtype, i
                           (o.flags & EBT_FLAG_LIKED_CHECKED) != 0);
   if (rc) return rc;
   int32_t* cert = (int32_t*)(ws + L.off_cert);
+  // the full-sort path fills its certificates by a memset and adds the exclusion flag: copied
+  int32_t* direct = L.large ? nullptr : host_mapped(cert_host);
+  if (direct) {
+    for (int64_t b = 0; b < B; ++b) cert_host[b] = CERT_UNSET;
+    cert = direct;
+  }
   if (L.large) {  // exact: every certificate is 1, the results are final
     rc = large_topk((const double*)(prep + L.prep.q64), B, cat->d, cat->data, cat->dtype,
                     cat->ld, cat->gnorm64, cat->n, cat->row_offset, excl_off, excl_rows, k,
@@ -554,10 +584,12 @@ int ebt_cosine_topk_submit(const ebt_catalog* cat, const void* q, int q_dtype, i
     rc = launch_check("csr_sorted_kernel");
     if (rc) return rc;
   }
-  rc = hip_check(hipMemcpyAsync(cert_host, cert, (size_t)(B + (excl_off && L.large)) * 4,
-                               hipMemcpyDeviceToHost, st),
-                 "hipMemcpyAsync");
-  if (rc) return rc;
+  if (!direct) {
+    rc = hip_check(hipMemcpyAsync(cert_host, cert, (size_t)(B + (excl_off && L.large)) * 4,
+                                 hipMemcpyDeviceToHost, st),
+                   "hipMemcpyAsync");
+    if (rc) return rc;
+  }
   hipEvent_t ev = event_get(st);
   if (!ev) return hip_check(hipErrorOutOfMemory, "hipEventCreate");
   rc = hip_check(hipEventRecord(ev, st), "hipEventRecord");
@@ -611,6 +643,12 @@ int ebt_cosine_topk_finish(ebt_pending* p) {
       if (p->cert_host[b] == -3) return true;
     return false;
   }());
+  for (int64_t b = 0; b < B; ++b)
+    if (p->cert_host[b] < -3 || p->cert_host[b] > 1) {
+      set_error("ebt_cosine_topk_finish: query %lld's certificate %d was not delivered",
+                (long long)b, p->cert_host[b]);
+      return EBT_EHIP;
+    }
   if (unsorted_excl) {
     set_error("ebt_cosine_topk: exclusion rows must be sorted ascending within each query");
     return EBT_EINVAL;
@@ -1205,6 +1243,11 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
   double* rs = padded ? (double*)(ws + L.off_res_s) : ls;
   int64_t* rr = padded ? (int64_t*)(ws + L.off_res_r) : lrr;
   int32_t* cert = (int32_t*)(ws + L.off_cert);
+  int32_t* direct = host_mapped(host);  // (see the dense submit)
+  if (direct) {
+    for (int64_t b = 0; b < B; ++b) host[b] = CERT_UNSET;
+    cert = direct;
+  }
   // (the list's rows read as they are: local at the shared threshold, global otherwise; the
   // certificate with ebt_certify_cut's tests)
   // (the rescore also checks the exclusion segments' order -- certificate -3 -- and packs the
@@ -1216,10 +1259,13 @@ int ebt_cosine_topk_sharded_submit(const ebt_catalog* cat, const ebt_comm* comm,
                        use_theta ? theta : nullptr, timer, st, use_theta ? 0 : c.row_offset,
                        excl_off, excl_rows, &pack);
   if (rc) return rc;
-  // the certificates to the caller's host buffer; one event for them
-  rc = hip_check(hipMemcpyAsync(host, cert, (size_t)B * 4, hipMemcpyDeviceToHost, st),
-                 "hipMemcpyAsync");
-  if (rc) return rc;
+  // the certificates to the caller's host buffer (unless the rescore wrote them there); one
+  // event for them
+  if (!direct) {
+    rc = hip_check(hipMemcpyAsync(host, cert, (size_t)B * 4, hipMemcpyDeviceToHost, st),
+                   "hipMemcpyAsync");
+    if (rc) return rc;
+  }
   hipEvent_t ev = event_get(st);
   if (!ev) return hip_check(hipErrorOutOfMemory, "hipEventCreate");
   rc = hip_check(hipEventRecord(ev, st), "hipEventRecord");
@@ -1300,10 +1346,13 @@ int ebt_cosine_topk_sharded_finish(ebt_sharded_pending* p) {
     if (!rc) rc = sh_gather(p->comm, ws + S.off_psend, ws + S.off_precv, S.pack_bytes, timer, st);
     if (rc) return rc;
     if (timer) (void)ebt_timer_begin(timer, EBT_STAGE_SHARD_MERGE, st);
+    // (the flag straight into the host buffer when it is pinned: zeroed above, only ever set
+    // to 1 by the merge's stores; else the workspace's flag and one copy)
+    int32_t* direct = host_mapped(p->host + B + 1);
     rc = ebt_merge_packed(ws + S.off_precv, p->comm.world, B, k, S.cap, p->out_scores,
-                          p->out_rows, incomplete, st);
+                          p->out_rows, direct ? direct : incomplete, st);
     if (timer) (void)ebt_timer_end(timer, EBT_STAGE_SHARD_MERGE, st);
-    if (!rc)
+    if (!rc && !direct)
       rc = hip_check(hipMemcpyAsync(p->host + B + 1, incomplete, 4, hipMemcpyDeviceToHost, st),
                      "hipMemcpyAsync");
   } else {
