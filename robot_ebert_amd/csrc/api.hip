@@ -274,6 +274,58 @@ struct StageScope {
   }
 };
 
+// A stage that is exactly one kernel launch (the filter GEMM's, the roofline's dominant kernel):
+// its event pair is handed to the launch (take_launch_events -> hipExtLaunchKernelGGL), which
+// binds the events to the dispatch -- no marker packets between the launches of the timed
+// region, where StageScope's two hipEventRecords cost the stream gaps of their own. A launch that
+// does not take them (an argument error before it) records nothing. EBT_TIMER_MARKERS=1: the
+// StageScope form (A/B).
+static thread_local hipEvent_t tl_launch_ev[2] = {nullptr, nullptr};
+bool take_launch_events(hipEvent_t* start, hipEvent_t* stop) {
+  *start = tl_launch_ev[0];
+  *stop = tl_launch_ev[1];
+  tl_launch_ev[0] = tl_launch_ev[1] = nullptr;
+  return *start != nullptr;
+}
+static bool timer_markers() {
+  static const bool on = [] {
+    const char* v = getenv("EBT_TIMER_MARKERS");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+struct KernelStage {
+  Timer* t;
+  int stage;
+  hipEvent_t a = nullptr, b = nullptr;
+  StageScope* markers = nullptr;
+  KernelStage(void* timer, int s, hipStream_t stream) : t((Timer*)timer), stage(s) {
+    if (t && !((t->mask >> s) & 1u)) t = nullptr;
+    if (!t) return;
+    if (timer_markers()) {
+      markers = new StageScope(timer, s, stream);
+      t = nullptr;
+      return;
+    }
+    std::lock_guard<std::mutex> g(t->mu);
+    a = t->get();
+    b = t->get();
+    if (a && b) {
+      tl_launch_ev[0] = a;
+      tl_launch_ev[1] = b;
+    }
+  }
+  ~KernelStage() {
+    delete markers;
+    if (!t || !a || !b) return;
+    const bool taken = tl_launch_ev[0] == nullptr;
+    tl_launch_ev[0] = tl_launch_ev[1] = nullptr;
+    if (!taken) return;
+    std::lock_guard<std::mutex> g(t->mu);
+    t->recs.push_back({stage, a, b});
+  }
+};
+
 // --------------------------------------------------------------------- workspace layout ----
 // Unfused:  [S: B_pad x chunk f32][seg tmp][per-chunk candidates][final candidates]
 // Fused:    the same for the HEAD rows [0, H) (chunked), plus the candidate rows
@@ -924,7 +976,7 @@ static int filter_screen(const PipeArgs& a, int64_t r0, int64_t seg, const float
   for (int64_t p0 = 0; p0 < seg; p0 += step) {
     const int64_t nr = seg - p0 < step ? seg - p0 : step;
     const int64_t r = r0 + p0, g = p0 / 256;  // part boundaries are whole 256-row groups
-    StageScope s(timer, EBT_STAGE_GEMM_FILTER, st);
+    KernelStage s(timer, EBT_STAGE_GEMM_FILTER, st);
     const int rc = screen_gemm_filter(a.qimg, a.B_pad, (const char*)a.cimg + r * a.ld_img * 2, nr,
                                       a.d_pad, a.ld_img, a.img_dtype, a.qscale,
                                       a.cscale ? a.cscale + r : nullptr, thr, cand + g * slots,

@@ -29,6 +29,10 @@ hipEvent_t event_get(hipStream_t st);
 void event_put(hipEvent_t e, hipStream_t st);
 std::mutex& event_pool_mutex();
 std::vector<hipEvent_t>* event_pool();
+// A timed stage that is ONE kernel launch (api.hip KernelStage): the launch site takes the
+// stage's event pair and passes it to hipExtLaunchKernelGGL, which binds the events to the
+// dispatch itself instead of two marker packets around it (take: returns false when none).
+bool take_launch_events(hipEvent_t* start, hipEvent_t* stop);
 
 // ---- element conversion --------------------------------------------------------------------
 __device__ __forceinline__ double bf16_bits_to_f64(uint16_t h) {

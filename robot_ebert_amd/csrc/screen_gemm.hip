@@ -20,6 +20,8 @@
 // Block order: XCD-bijective remap (blocks sharing an XCD get a contiguous logical range), then
 // groups of 8 (128-kernel) / 4 (256-kernel) catalog tiles walked query-tile-major, so a catalog
 // tile is fetched from HBM about once per XCD and re-read from L2 by the query tiles that use it.
+#include <hip/hip_ext.h>
+
 #include <atomic>
 #include <cstdlib>
 #include <type_traits>
@@ -1444,7 +1446,11 @@ static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_
     a.S2 = S2;
     a.ld_s2 = ld_s2;
     a.e = e;
-    hipLaunchKernelGGL(k, grid, block, QP_LDS_TOTAL, stream, a);
+    hipEvent_t ev0, ev1;
+    if (take_launch_events(&ev0, &ev1))   // a timed launch: the events ride on the dispatch
+      hipExtLaunchKernelGGL(k, grid, block, QP_LDS_TOTAL, stream, ev0, ev1, 0, a);
+    else
+      hipLaunchKernelGGL(k, grid, block, QP_LDS_TOTAL, stream, a);
     return launch_check("screen_gemm_qp2_kernel");
   }
   if (cstride != GBM || EPI == EPI_POOL) {
@@ -1457,8 +1463,13 @@ static int launch_gemm(const void* qimg, int64_t B_pad, const void* cimg, int64_
                                  : screen_gemm_kernel<false, FILTER>;
   const int lds = GLDS_BYTES + (FILTER ? GBN * 4 : 0);
   set_max_lds((const void*)k, lds);
-  hipLaunchKernelGGL(k, grid, block, lds, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
-                     n_ctiles, d_pad / GBK, qscale, cscale, e);
+  hipEvent_t ev0, ev1;
+  if (take_launch_events(&ev0, &ev1))
+    hipExtLaunchKernelGGL(k, grid, block, lds, stream, ev0, ev1, 0, Q, C, (int64_t)ld_img,
+                          n_rows, n_qtiles, n_ctiles, d_pad / GBK, qscale, cscale, e);
+  else
+    hipLaunchKernelGGL(k, grid, block, lds, stream, Q, C, (int64_t)ld_img, n_rows, n_qtiles,
+                       n_ctiles, d_pad / GBK, qscale, cscale, e);
   return launch_check("screen_gemm_kernel");
 }
 

@@ -116,7 +116,7 @@ EOF
     N=${3:-2}
     for i in $(seq "$N"); do
       for c in ${CFGS//,/ }; do
-        case $c in C2) A="--steps 50" ;; C3) A="--steps 20" ;; *) A="--steps 5 --warmup 1" ;; esac
+        case $c in C2) A="--steps 400" ;; C3) A="--steps 20" ;; *) A="--steps 5 --warmup 1" ;; esac
         bash "$0" bench "${O#gpurun_out/}/${c}_new$i" "$c" $A --no-cpu-baseline || exit 1
         if [[ $ALT == *=* ]]; then
           env "$ALT" bash "$0" bench "${O#gpurun_out/}/${c}_alt$i" "$c" $A --no-cpu-baseline || exit 1
