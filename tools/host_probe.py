@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--depth", type=int, default=1,
                     help="batches submitted ahead of the one being finished (bench.py: 1)")
+    ap.add_argument("--burst", type=int, default=0,
+                    help="untimed steps run pipelined (one burst) right before the timed loop")
     ap.add_argument("--timer", action="store_true",
                     help="time the filter GEMM's launches as bench.py does (timer.only)")
     a = ap.parse_args()
@@ -55,6 +57,16 @@ def main():
     for _ in range(5):
         ebt.score_topk_finish(submit())
     torch.cuda.synchronize()
+
+    if a.burst:
+        prev = None
+        for _ in range(a.burst):
+            p = submit()
+            if prev is not None:
+                ebt.score_topk_finish(prev)
+            prev = p
+        ebt.score_topk_finish(prev)
+        torch.cuda.synchronize()
 
     # 1. the pipelined loop (bench.py's), with the host time of each call
     if timer is not None:
@@ -93,7 +105,7 @@ def main():
     torch.cuda.synchronize()
     gpu = e0.elapsed_time(e1) / n * 1e-3
     print(json.dumps({
-        "config": a.config, "steps": a.steps, "depth": a.depth,
+        "config": a.config, "steps": a.steps, "depth": a.depth, "burst": a.burst,
         "wall_ms_per_step": round(wall * 1e3, 4),
         "host_submit_ms": round(t_sub / a.steps * 1e3, 4),
         "host_finish_ms_incl_wait": round(t_fin / max(a.steps - a.depth, 1) * 1e3, 4),
