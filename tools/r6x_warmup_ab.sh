@@ -1,3 +1,5 @@
+# bench.py vs bench_prev.py (`git show HEAD:bench.py > bench_prev.py` before the run: the tree before
+# the warm-up-burst edit, which was then reverted); profiles/r6/host_probe/warmup_ab/
 set -e
 O=gpurun_out/r6x; mkdir -p $O
 for i in 1 2 3; do
