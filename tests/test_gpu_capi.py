@@ -16,6 +16,7 @@ import pytest
 import torch
 
 from inputs import COS_CASES, c1_catalog, cos_case_inputs
+from oracle import restatement as R
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -216,3 +217,49 @@ def test_workspace_allocation_failure_is_loud(cuda_device):
         torch.cuda.set_per_process_memory_fraction(1.0, dev)
     s, r = ebt.score_topk(cat, 100, queries=q[:8])
     assert (r >= 0).all()
+
+
+@pytest.mark.parametrize("buffer", ["pinned", "pageable"])
+def test_capi_submit_certificates_pinned_or_pageable(cuda_device, lib, buffer):
+    """ebt_cosine_topk_submit / _finish with the certificate buffer in pinned host memory (the
+    rescore writes it itself, ABI 0.3.3) or in pageable memory (a copy from the workspace):
+    both deliver every certificate and the same exact answer. A clustered catalog makes some
+    first-pass certificates 0 / -1, so the retries read what was delivered; a buffer left at a
+    non-certificate value would have failed the finish with EBT_EHIP."""
+    dev = cuda_device
+    rng = np.random.default_rng(29)
+    n, d, B, k, C = 60_000, 64, 256, 50, 16
+    centers = rng.standard_normal((C, d))
+    x = (centers[rng.integers(0, C, n)] + 0.03 * rng.standard_normal((n, d))).astype(np.float32)
+    qv = (centers[rng.integers(0, C, B)] + 0.015 * rng.standard_normal((B, d))).astype(np.float32)
+    emb = torch.from_numpy(x).to(dev)
+    q = torch.from_numpy(qv).to(dev)
+    cat, state = make_catalog(lib, emb)
+    lib.ebt_cosine_topk_submit.argtypes = [ctypes.POINTER(Catalog), VP, ctypes.c_int, I64, I64,
+                                           VP, VP, I32, VP, VP, VP, VP, SZ, VP, VP, VP, VP, VP,
+                                           VP]
+    lib.ebt_cosine_topk_finish.argtypes = [VP]
+    ws_bytes = lib.ebt_workspace_bytes(ctypes.byref(cat), B, k, None)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    s = torch.empty((B, k), dtype=torch.float64, device=dev)
+    r = torch.empty((B, k), dtype=torch.int64, device=dev)
+    if buffer == "pinned":
+        cert_t = torch.full((B + 1,), 9, dtype=torch.int32, pin_memory=True)
+        cert_np, cert_p = cert_t.numpy(), ctypes.c_void_p(cert_t.data_ptr())
+    else:
+        cert_np = np.full(B + 1, 9, dtype=np.int32)
+        cert_p = cert_np.ctypes.data_as(VP)
+    pend = ctypes.create_string_buffer(1024)            # struct ebt_pending (opaque here)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    rc = lib.ebt_cosine_topk_submit(ctypes.byref(cat), P(q), CODE[q.dtype], B, d, None, None, k,
+                                    None, None, None, P(ws), ws_bytes, P(s), P(r), cert_p, pend,
+                                    None, st)
+    assert rc == 0, lib.ebt_last_error()
+    rc = lib.ebt_cosine_topk_finish(pend)
+    assert rc == 0, lib.ebt_last_error()
+    first = cert_np[:B].copy()                          # the first pass's, as delivered
+    assert set(np.unique(first)) <= {1, 0, -1}, np.unique(first)
+    assert (first != 1).any(), "no retry exercised"
+    s_ref, r_ref = R.cosine_topk(qv.astype(np.float64), x.astype(np.float64), k)
+    np.testing.assert_array_equal(r.cpu().numpy(), r_ref)
+    np.testing.assert_allclose(s.cpu().numpy(), s_ref, rtol=0, atol=1e-12)
