@@ -69,7 +69,8 @@ extern "C" {
  *        ebt_timer_count_rows is device-aware.
  * 0.3.3: a pinned certificate buffer of ebt_cosine_topk_submit / ebt_cosine_topk_sharded_submit
  *        is written by the kernels themselves (no copy launch; EBT_EHIP from _finish if one was
- *        not delivered); the speculative screen's segment thresholds come from its wave merges. */
+ *        not delivered); the speculative screen's segment thresholds come from its wave merges;
+ *        ebt_merge_packed also flags a query with more than min(R k, 2 k + 256) entries. */
 int ebt_version(void);
 
 /* Message for the last non-zero return on this thread ("" if none). */
@@ -261,8 +262,9 @@ int ebt_merge_topk(const double* scores, const int64_t* rows, int32_t R, int64_t
  * >= cap are counted but not sent. After an all-gather of the R buffers
  * (recv, R * ebt_shard_pack_bytes bytes, rank order), ebt_merge_packed writes the same global
  * top-k as ebt_merge_topk over the full lists, and sets *incomplete (device int32; set to 1,
- * never cleared) when some rank's entries did not all fit its cap: the caller must then merge
- * the full lists instead (the rows of an incomplete batch are not final).
+ * never cleared) when some rank's entries did not all fit its cap, or (0.3.3) when one query
+ * received more than min(R k, 2 k + 256) entries (a floor band wider than k + 256): the caller
+ * must then merge the full lists instead (the rows of an incomplete batch are not final).
  * ebt_shard_pack_cap: the cap the library uses, B * ebt_shard_list_width(k, world), or 0 when
  * the compact form does not apply (world < 2, world * k > 8192, n_global >= 2^31).
  * ebt_shard_list_width(k, world) = min(k, ceil(1.5 k / world) + 8): also the per-shard width of

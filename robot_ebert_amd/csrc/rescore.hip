@@ -1222,8 +1222,18 @@ __global__ __launch_bounds__(RTHREADS) void merge_topk_corank_kernel(
 // a binary search in each (score desc, row asc; equal keys ordered by list). A list found
 // unsorted flags the batch incomplete (the caller merges the full lists instead): the packed
 // lists come sorted from ebt_shard_pack.
+// The entries one query's LDS holds: R k (every rank sending all of its k) is what a query can
+// receive, but a query's entries above the catalog-wide floor number about k + the floor's band
+// over all ranks together, so the room is min(R k, 2 k + 256) and a query with more (a band
+// wider than k + 256: clustered data) flags the batch incomplete -- the caller's full exchange,
+// as for a list cut by its capacity. At C5/8 (R 8, k 1000) that is 27 KiB instead of 94 KiB of
+// LDS per query: five waves per CU instead of one for the binary searches' LDS latency.
+__host__ __device__ inline int merge_packed_room(int R, int k) {
+  const int64_t all = (int64_t)R * k, room = 2LL * k + 256;
+  return (int)(all < room ? all : room);
+}
 size_t merge_packed_lds(int R, int k) {
-  const size_t n = (size_t)R * k;
+  const size_t n = (size_t)merge_packed_room(R, k);
   return n * 8 + ((n * 4 + 15) & ~(size_t)15) + (((size_t)(3 * R + 1) * 4 + 15) & ~(size_t)15);
 }
 
@@ -1235,7 +1245,7 @@ __global__ __launch_bounds__(MP_THREADS) void merge_packed_kernel(
     const PackedSrc src, int R, int64_t B, int k, double* __restrict__ out_s,
     int64_t* __restrict__ out_r, int32_t* __restrict__ incomplete) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nmax = R * k;
+  const int nmax = merge_packed_room(R, k);
   double* sc = (double*)smem;                                  // nmax
   int32_t* rw = (int32_t*)(sc + nmax);                         // nmax
   int* pst = (int*)((char*)rw + (((size_t)nmax * 4 + 15) & ~(size_t)15));  // R: packed start
@@ -1279,6 +1289,10 @@ __global__ __launch_bounds__(MP_THREADS) void merge_packed_kernel(
   if (tid == 0) off[R] = carry;
   __syncthreads();
   const int N = carry;
+  if (N > nmax) {   // more than the query's room (merge_packed_room): the full exchange
+    if (tid == 0) incomplete[0] = 1;
+    return;
+  }
   auto list_of = [&](int e) {   // the last list whose compact start is <= e (a non-empty one)
     int lo = 0, hi = R - 1;
     while (lo < hi) {

@@ -60,7 +60,7 @@ def test_pack_merge_equals_full_merge(cuda_device, R, B, k, ties):
     nbytes = L.load().ebt_shard_pack_bytes(B, cap)
     recv = torch.zeros(R * nbytes, dtype=torch.uint8, device=dev)
     tf = torch.from_numpy(floor).to(dev)
-    counts = []
+    counts, per_query = [], np.zeros(B, dtype=np.int64)
     for a in range(R):
         L.call("ebt_shard_pack", L.ptr(gs[a].contiguous()), L.ptr(gr[a].contiguous()), B, k,
                L.ptr(tf), cap, L.ptr(recv[a * nbytes:]), st)
@@ -71,12 +71,14 @@ def test_pack_merge_equals_full_merge(cuda_device, R, B, k, ties):
         np.testing.assert_array_equal(ln, want)
         np.testing.assert_array_equal(start, np.concatenate([[0], np.cumsum(want)[:-1]]))
         counts.append(int(want.sum()))
+        per_query += want
     out_s = torch.empty((B, k), dtype=torch.float64, device=dev)
     out_r = torch.empty((B, k), dtype=torch.int64, device=dev)
     inc = torch.zeros(1, dtype=torch.int32, device=dev)
     L.call("ebt_merge_packed", L.ptr(recv), R, B, k, cap, L.ptr(out_s), L.ptr(out_r), L.ptr(inc),
            st)
-    overflow = max(counts) > cap
+    # a rank over its cap, or (0.3.3) a query over the merge's room min(R k, 2 k + 256)
+    overflow = max(counts) > cap or int(per_query.max()) > min(R * k, 2 * k + 256)
     assert bool(inc.item()) == overflow
     if not overflow:
         assert torch.equal(out_r, full_r)
@@ -106,6 +108,38 @@ def test_pack_overflow_flags(cuda_device):
     L.call("ebt_merge_packed", L.ptr(recv), R, B, k, cap, L.ptr(out_s), L.ptr(out_r), L.ptr(inc),
            st)
     assert inc.item() == 1
+
+
+@pytest.mark.parametrize("per_rank,flagged", [(57, False), (58, True), (100, True)])
+def test_pack_merge_room(cuda_device, per_rank, flagged):
+    """The packed merge holds min(R k, 2 k + 256) entries per query (R 8, k 100: 456): with a
+    cap that every rank's entries fit, 8 x 57 = 456 entries per query merge exactly as the full
+    merge does, 8 x 58 = 464 flag the batch incomplete (the caller's full exchange)."""
+    L = _lib()
+    dev = cuda_device
+    R, B, k = 8, 16, 100
+    rng = np.random.default_rng(per_rank)
+    s, r = sorted_lists(rng, R, B, k, np.full((R, B), per_rank))
+    st = torch.cuda.current_stream(dev).cuda_stream
+    gs, gr = torch.from_numpy(s).to(dev), torch.from_numpy(r).to(dev)
+    full_s = torch.empty((B, k), dtype=torch.float64, device=dev)
+    full_r = torch.empty((B, k), dtype=torch.int64, device=dev)
+    L.call("ebt_merge_topk", L.ptr(gs), L.ptr(gr), R, B, k, L.ptr(full_s), L.ptr(full_r), st)
+    cap = B * k                                   # every rank's entries fit: only the room limits
+    nbytes = L.load().ebt_shard_pack_bytes(B, cap)
+    recv = torch.zeros(R * nbytes, dtype=torch.uint8, device=dev)
+    for a in range(R):   # no floor: every real entry is sent
+        L.call("ebt_shard_pack", L.ptr(gs[a].contiguous()), L.ptr(gr[a].contiguous()), B, k,
+               None, cap, L.ptr(recv[a * nbytes:]), st)
+    out_s = torch.empty((B, k), dtype=torch.float64, device=dev)
+    out_r = torch.empty((B, k), dtype=torch.int64, device=dev)
+    inc = torch.zeros(1, dtype=torch.int32, device=dev)
+    L.call("ebt_merge_packed", L.ptr(recv), R, B, k, cap, L.ptr(out_s), L.ptr(out_r), L.ptr(inc),
+           st)
+    assert bool(inc.item()) == flagged
+    if not flagged:
+        assert torch.equal(out_r, full_r)
+        assert torch.equal(out_s, full_s)
 
 
 @pytest.mark.parametrize("ld,k_eff,w", [(200, 100, 27), (1256, 1000, 196), (40, 40, 40),
