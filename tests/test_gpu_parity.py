@@ -1345,3 +1345,34 @@ def test_filter_split_launches_equal_one_launch(cuda_device):
     finally:
         lib.ebt_filter_split(prev)
     assert torch.equal(r0, r1) and torch.equal(s0, s1)
+
+
+def test_speculative_multi_segment_raise_in_merge(cuda_device):
+    """A C3-shaped speculative screen (1M rows, 4096 queries, top-100; d = 64 to keep it cheap)
+    runs several filter segments, each later one at the threshold the previous wave merge wrote
+    (spec_threshold's RAISE folded into the merge, round 6), with exclusions looked up in every
+    merge: the same rows and scores as the unfused path for all 4096 queries, bit for bit, and
+    the float64 oracle on 32 of them."""
+    ebt, L = _ebt()
+    n, d, B, k = 1_000_000, 64, 4096, 100
+    c = gaussian(71, n, d, "f32")
+    q = gaussian(72, B, d, "f32")
+    rng = np.random.default_rng(73)
+    excl = [np.sort(rng.choice(n, 16, replace=False)) for _ in range(B)]
+    cat = ebt.Catalog(_t(c, "f32", cuda_device))
+    qt = _t(q, "f32", cuda_device)
+    pl = ebt.search.plan(cat, B, k)
+    assert pl["fused"] and pl["spec"] is not None, pl
+    timer = ebt.Timer()
+    ex = [list(e) for e in excl]
+    s1, r1 = ebt.score_topk(cat, k, queries=qt, exclude=ex, timer=timer)
+    merges = timer.query("merge_select")[1]
+    assert merges >= 3, f"{merges} wave merges: the shape no longer runs several segments"
+    s2, r2 = ebt.score_topk(cat, k, queries=qt, exclude=ex, fuse=False)
+    assert torch.equal(r1, r2)
+    torch.testing.assert_close(s1, s2, rtol=0, atol=0)
+    idx = np.linspace(0, B - 1, 32).round().astype(np.int64)
+    s_ref, r_ref = R.cosine_topk(q[idx].astype(np.float64), c.astype(np.float64), k,
+                                 [ex[i] for i in idx])
+    ti = torch.from_numpy(idx).to(cuda_device)
+    assert_topk_equal(s1[ti], r1[ti], s_ref, r_ref)
