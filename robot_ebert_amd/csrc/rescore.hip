@@ -148,8 +148,11 @@ extern "C" int ebt_debug_rescore_stamps(unsigned long long* buf) {
 #else
 #define RST(i)
 #endif
+// (f32 rows with the query held in registers at d = 1536, C3's variant: 138 VGPRs would give
+// three waves per SIMD; bounded to 128 -- no spill -- it runs four, a quarter more row gathers
+// in flight. The other variants are at four or more already, or would spill under the bound.)
 template <int DT, bool VEC, int NU = 0>
-__global__ __launch_bounds__(RTHREADS) void rescore_kernel(
+__global__ __launch_bounds__(RTHREADS, (DT == EBT_F32 && NU == 6) ? 4 : 1) void rescore_kernel(
     const double* __restrict__ q64, int d, const void* __restrict__ cat, int64_t ld,
     const double* __restrict__ gnorm, int64_t row_offset, const float* __restrict__ cand_vals,
     const int64_t* __restrict__ cand_rows, int kprime, int kpp, int k, int64_t n_rows,
